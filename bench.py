@@ -1,0 +1,353 @@
+"""bench.py — device-resident KV Add+Get throughput (BASELINE.json metric).
+
+One step = one pass of the hot path over one batch set: a grouped Add of J
+push batches (1M keys each) followed by a grouped Get of the same J pull
+batches, on every rank's shard.  Inputs are resident in HBM before timing.
+
+  N = 1: configs[1] (cfg 2) — 1e8-key float shard, J x 1M contiguous-key
+         windows at seed-42 uniform 1M-aligned bases, vals U(-1,1), assign mode.
+  N > 1: configs[3] (cfg 4) — 1e9 keys range-partitioned over N GPUs (one
+         shard per rank, base/range_partition_manager.hpp's map); each rank's
+         producers push J x 1M windows routed to it by the range map
+         (weak scaling: per-GPU work fixed).  No collective on the data path;
+         torch.distributed (RCCL) only for the barrier and the max-time reduce.
+
+Prints ONE JSON line on rank 0 with roofline (dominant kernel, HIP events on
+the launch stream) and cpu_baseline (the oracle restatement of the reference
+storages timed on this host, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "device-resident KV Add+Get GB/s (grad+param bytes) at 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
+BYTES_PER_KEY = {"add": 12, "get": 12}  # f32 assign: Add key4+val4+param4; Get key4+param4+out4
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--batches", type=int, default=64, help="push/pull batches per step per GPU")
+    p.add_argument("--batch-keys", type=int, default=1_000_000)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-extra", action="store_true", help="skip the zipf / e2e side measurements")
+    p.add_argument("--cpu-batches", type=int, default=12)
+    return p.parse_args()
+
+
+def dist_init(args):
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    else:
+        torch.cuda.set_device(0)
+    return rank, world, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+
+
+def max_over_ranks(x, world, dev):
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x, world, dev):
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def make_workload(rank, world, J, B, dev):
+    import torch
+
+    from parameter_server_amd import workload
+
+    if world == 1:
+        key_space = 100_000_000
+        lo, hi = 0, key_space
+        bases = workload.dense_bases(J, key_space, B)
+    else:
+        key_space = 1_000_000_000
+        ranges = workload.rank_ranges(key_space, world)
+        lo, hi = ranges[rank]
+        bases = workload.rank_windows(rank, world, key_space, J, B)
+        routed = workload.route_windows(bases, B, ranges)
+        # every window of this rank's producers is routed to this rank, whole
+        assert all(len(routed[r]) == 0 for r in range(world) if r != rank)
+        assert len(routed[rank]) == J and all(n == B for _, _, n in routed[rank])
+    batches = []
+    for j, b in enumerate(bases):
+        keys = torch.arange(int(b), int(b) + B, dtype=torch.int64, device=dev).to(torch.int32)
+        g = torch.Generator(device=dev)
+        g.manual_seed(42 + j + 1000 * rank)
+        vals = torch.rand(B, generator=g, device=dev, dtype=torch.float32) * 2 - 1
+        batches.append((keys, vals))
+    outs = [torch.empty(B, dtype=torch.float32, device=dev) for _ in range(J)]
+    return key_space, lo, hi, bases, batches, outs
+
+
+def cpu_baseline(bases, B, n_batches):
+    """The oracle (C++ restatement of server/map_storage.hpp, 1 thread) on a
+    bounded sample of the same workload; plus VectorStorage at 1e5 keys (cfg 1
+    sample; it is O(stored x queried))."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test infrastructure: the CPU baseline leg
+
+    oracle.build()
+    rng = np.random.default_rng(42)
+    m = oracle.MapStorageRef(np.float32)
+    ks = [np.arange(int(b), int(b) + B, dtype=np.uint32) for b in bases[:n_batches]]
+    vs = [(rng.random(B, dtype=np.float32) * 2 - 1) for _ in ks]
+    t0 = time.perf_counter()
+    for k, v in zip(ks, vs):
+        m.add(k, v)
+    for k in ks:
+        m.get(k)
+    t_map = time.perf_counter() - t0
+    n = 100_000
+    vec = oracle.VectorStorageRef(np.float32)
+    k = np.arange(n, dtype=np.uint32)
+    v = (0.5 * k).astype(np.float32)
+    t0 = time.perf_counter()
+    vec.add(k, v)
+    got = vec.get(k)
+    t_vec = time.perf_counter() - t0
+    assert np.array_equal(got, v)
+    return {
+        "value": 24.0 * B * len(ks) / t_map / 1e9,
+        "unit": "GB/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"MapStorage restatement (std::map, 1 thread), {len(ks)} x {B} contiguous float keys of the "
+                  f"same workload, Add then Get, {t_map:.2f} s",
+        "vector_storage": {
+            "value": 24.0 * n / t_vec / 1e9, "unit": "GB/s", "seconds": t_vec,
+            "sample": f"VectorStorage restatement (append + O(stored x queried) scan), 1e5 contiguous float "
+                      f"keys (config 1 at 1/10 size; the 1e6 case is ~100x longer, quadratic)",
+        },
+        "host_cpu": _cpu_model(),
+    }
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def load_pmc(kernel_substr):
+    """HBM traffic per dispatch from the committed rocprofv3 --pmc summary, if any."""
+    path = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        d = json.load(f)
+    for name, rec in d.get("kernels", {}).items():
+        if kernel_substr in name and rec.get("hbm_bytes_per_dispatch"):
+            return rec["hbm_bytes_per_dispatch"], d.get("source", path)
+    return None, None
+
+
+def side_measurements(dev, B):
+    """Secondary numbers (same JSON line, under "extra"): cfg 3 Zipf through the
+    general path, and the end-to-end rate with host (pageable) buffers."""
+    import torch
+
+    import parameter_server_amd as ps
+    from parameter_server_amd import workload
+
+    out = {}
+    stream = torch.cuda.current_stream()
+    # cfg 3: Zipf(0.99) over 1e8 keys, unsorted, 8 x 1M pushes then pulls
+    space, J = 100_000_000, 8
+    zb = workload.zipf_batches(J, space, batch=B, device=dev)
+    zo = [torch.empty_like(v) for _, v in zb]
+    with ps.Shard(0, space, np.float32) as sh:
+        sh.set_stream(stream.cuda_stream)
+        for _ in range(2):
+            sh.add_grouped(zb)
+            sh.get_grouped([(k, o) for (k, _), o in zip(zb, zo)])
+        torch.cuda.synchronize()
+        reps = 5
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            sh.add_grouped(zb)
+            sh.get_grouped([(k, o) for (k, _), o in zip(zb, zo)])
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        uniq = int(torch.unique(zb[0][0]).numel())
+        sh.set_stream(None)
+    out["zipf"] = {"workload": "cfg 3: Zipf(0.99) over 1e8 keys, 8 x 1M unsorted pushes then pulls, assign",
+                   "GB/s": 24.0 * B * J * reps / dt / 1e9, "ms_per_step": dt / reps * 1e3,
+                   "unique_keys_per_batch": uniq}
+    del zb, zo
+    # end-to-end: keys/vals start in pageable host memory (the zmq frames), outputs return to host
+    rng = np.random.default_rng(0)
+    J = 8
+    hk = [np.arange(b, b + B, dtype=np.uint32) for b in workload.dense_bases(J, space, B)]
+    hv = [rng.random(B, dtype=np.float32) for _ in hk]
+    ho = [np.empty(B, np.float32) for _ in hk]
+    with ps.Shard(0, space, np.float32) as sh:
+        sh.add_grouped(list(zip(hk, hv)))
+        sh.get_grouped(list(zip(hk, ho)))
+        reps = 3
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            sh.add_grouped(list(zip(hk, hv)))
+            sh.get_grouped(list(zip(hk, ho)))
+        sh.sync()
+        dt = time.perf_counter() - t0
+    assert all(np.array_equal(o, v) for o, v in zip(ho, hv))
+    out["e2e_host_buffers"] = {"workload": "8 x 1M contiguous float keys from pageable host memory, Add then Get "
+                                           "(H2D + kernels + D2H, host sortedness check included)",
+                               "GB/s": 24.0 * B * J * reps / dt / 1e9}
+    return out
+
+
+def main():
+    args = parse()
+    import torch
+
+    import parameter_server_amd as ps
+    from parameter_server_amd import _lib
+
+    rank, world, local = dist_init(args)
+    dev = torch.device(f"cuda:{local}")
+    J, B = args.batches, args.batch_keys
+    key_space, lo, hi, bases, batches, outs = make_workload(rank, world, J, B, dev)
+    stream = torch.cuda.current_stream()
+    shard = ps.Shard(lo, hi, np.float32, device=local)
+    shard.set_stream(stream.cuda_stream)  # torch events and the kernels share one stream
+    gets = [(k, o) for (k, _), o in zip(batches, outs)]
+
+    def step():
+        shard.add_grouped(batches, sorted_hint=True)
+        shard.get_grouped(gets)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # correctness guard on the benchmarked state: every pull returns the last push of its window
+    last = {int(b): j for j, b in enumerate(bases)}
+    for j, b in enumerate(bases):
+        assert torch.equal(outs[j], batches[last[int(b)]][1]), "bench self-check failed"
+
+    shard.reset_timing()
+    shard.set_timing(True)
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier(world)
+    t1 = time.perf_counter()
+    shard.set_timing(False)
+    elapsed = max_over_ranks(t1 - t0, world, dev)
+
+    ktimes = {}
+    for k, name in _lib.KERNEL_NAMES.items():
+        t = shard.kernel_time(k)
+        if t["launches"]:
+            ktimes[name] = {"launches": t["launches"], "avg_ms": t["total_ms"] / t["launches"],
+                            "keys_per_launch": t["elements"] / t["launches"]}
+    shard.sync()
+    bytes_rank = float(J * B * (BYTES_PER_KEY["add"] + BYTES_PER_KEY["get"]) * args.steps)
+    total_bytes = sum_over_ranks(bytes_rank, world, dev)
+    value = total_bytes / elapsed / 1e9
+
+    # dominant kernel: the one with the most time in the timed region
+    dom = max(ktimes.items(), key=lambda kv: kv[1]["avg_ms"] * kv[1]["launches"])
+    per_key = BYTES_PER_KEY["get"] if dom[0] == "k_gather" else BYTES_PER_KEY["add"]
+    achieved = per_key * dom[1]["keys_per_launch"] / (dom[1]["avg_ms"] / 1e3) / 1e9
+    traffic, traffic_src = load_pmc(dom[0])
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": dom[0],
+            "algorithmic_bytes_per_key": per_key, "kernels": ktimes}
+    if traffic_src:
+        roof["traffic_source"] = traffic_src
+
+    result = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {
+            "workload": ("cfg 2 dense: 1e8-key float shard" if world == 1 else
+                         f"cfg 4 ranges: 1e9 keys over {world} range shards") +
+                        f", {J} x {B} contiguous-key push batches then the same pulls per step per GPU, "
+                        "assign (last-write-wins) mode, grouped launches",
+            "key_space": key_space,
+            "shard_keys_per_gpu": hi - lo,
+            "batches_per_step_per_gpu": J,
+            "batch_keys": B,
+            "bytes_per_key": BYTES_PER_KEY["add"] + BYTES_PER_KEY["get"],
+            "parallelism": f"range-sharded x{world} (no collective)",
+        },
+        "roofline": roof,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(bases, B, args.cpu_batches)
+    if rank == 0 and world == 1 and not args.no_extra:
+        shard.set_stream(None)
+        result["extra"] = side_measurements(dev, B)
+    shard.close()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+
+        barrier(world)
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

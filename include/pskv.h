@@ -1,0 +1,180 @@
+/*
+ * pskv.h — C ABI of the MI355X-native parameter-shard store (Add/Get hot path).
+ *
+ * This is the drop-in boundary that replaces the arithmetic of the reference's
+ * storage plugins:
+ *
+ *   reference interface                                   replaced by
+ *   ---------------------------------------------------  -----------------------------
+ *   AbstractStorage::SubAdd  server/abstract_storage.hpp:35-36   pskv_add / pskv_add_grouped
+ *   AbstractStorage::SubGet  server/abstract_storage.hpp:39      pskv_get / pskv_get_grouped
+ *   AbstractStorage::FinishIter server/abstract_storage.hpp:41   pskv_sync (the reference's is a no-op)
+ *   MapStorage<Val>()        server/map_storage.hpp:15           pskv_shard_create(..., PSKV_ASSIGN)
+ *   VectorStorage<Val>()     server/vector_storage.hpp:14        pskv_shard_create(..., PSKV_ASSIGN)
+ *   ~AbstractStorage (missing in the reference) pskv_shard_destroy
+ *   RangePartitionManager::Slice base/range_partition_manager.hpp:19-46,48-77  pskv_range_slice
+ *
+ * Semantics (PSKV_ASSIGN, the reference semantics; map_storage.hpp:22-23,
+ * vector_storage.hpp:21-43): a shard is a last-write-wins key/value store with
+ * uint32 keys (base/magic.hpp:7).  Within one call the LAST occurrence of a key
+ * wins (index order), across calls the later call wins (call order on the
+ * shard's stream).  A key that was never written reads as 0
+ * (map_storage.hpp:33-37; zero-filled SArray in vector_storage.hpp:33).  Values
+ * are copied bit-for-bit, so parity is bit-exact for every value type.
+ *
+ * PSKV_ACCUMULATE is the north-star gradient-reduction mode (param[k] += v for
+ * every occurrence).  It has no reference counterpart; float sums follow the
+ * tolerance stated in DESIGN.md (recursive-summation bound), int32 is exact.
+ *
+ * Keys outside [key_begin, key_end) are legal (the reference's last range
+ * server receives every out-of-range key, range_partition_manager.hpp:26-27):
+ * they live in a device-side overflow hash table with the same semantics.
+ *
+ * Threading: one shard handle is used by one host thread at a time (the
+ * reference calls a storage only from its ServerThread, server_thread.cpp:20-50);
+ * distinct handles may be used concurrently.  Every call selects the shard's
+ * device itself, so construction and use may happen on different threads
+ * (Engine::CreateTable constructs storages on the engine thread,
+ * driver/engine.hpp:100-109).
+ *
+ * Errors: every function returns 0 on success and a negative PSKV_E* code on
+ * failure; pskv_last_error() returns this thread's message for the last
+ * failure.  The C++ HipStorage adaptor (include/ps/hip_storage.hpp) turns a
+ * non-zero status into an abort, keeping the reference's glog CHECK convention
+ * (abstract_storage.hpp:15,20; map_storage.hpp:20).
+ */
+#ifndef PSKV_H_
+#define PSKV_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PSKV_ABI_VERSION 1
+
+/* status codes */
+#define PSKV_OK 0
+#define PSKV_EINVAL (-1)   /* bad argument (null pointer, bad dtype, n mismatch ...) */
+#define PSKV_EHIP (-2)     /* a HIP runtime call failed */
+#define PSKV_ENOMEM (-3)   /* device or pinned allocation failed */
+#define PSKV_ESTATE (-4)   /* sticky device-side error (overflow table exhausted) */
+
+/* value types used by the reference (driver/engine.cpp:254,261; apps use double) */
+enum pskv_dtype { PSKV_I32 = 0, PSKV_F32 = 1, PSKV_F64 = 2 };
+
+/* update semantics */
+enum pskv_mode {
+  PSKV_ASSIGN = 0,     /* reference: last write wins (drop-in default) */
+  PSKV_ACCUMULATE = 1  /* north star: scatter-accumulate (gradient reduction) */
+};
+
+/* call flags */
+#define PSKV_HOST 0x0        /* keys/vals/out are host memory (the zmq buffers of comm/mailbox.cpp) */
+#define PSKV_DEVICE 0x1      /* keys/vals/out are device memory on the shard's device */
+#define PSKV_SORTED_HINT 0x2 /* caller believes keys are non-decreasing: take the sorted path.
+                                The kernel verifies the claim and repairs the result on the
+                                device if it was wrong, so a wrong hint costs time, never
+                                correctness. */
+
+typedef struct pskv_shard pskv_shard;
+
+/* One push or pull batch of a grouped call.  For an Add `vals` is read
+ * (n values), for a Get `vals` is the output (n values). */
+typedef struct pskv_batch {
+  const uint32_t* keys;
+  void* vals;
+  uint64_t n;
+} pskv_batch;
+
+typedef struct pskv_info {
+  int device;
+  int dtype;
+  int mode;
+  int value_bytes;
+  uint32_t key_begin;
+  uint64_t key_end;          /* exclusive, may be 2^32 */
+  uint64_t dense_bytes;      /* HBM held by the dense parameter array */
+  uint64_t overflow_capacity;/* slots of the overflow hash table */
+  uint64_t overflow_count;   /* keys stored in the overflow table (as of the last sync) */
+  uint64_t n_add_calls;
+  uint64_t n_get_calls;
+  uint64_t n_sorted_launches;   /* sorted-path kernel launches */
+  uint64_t n_general_launches;  /* general (dedup) path launches, repairs included */
+} pskv_info;
+
+/* Kernel ids for pskv_kernel_time. */
+enum pskv_kernel {
+  PSKV_K_GATHER = 0,        /* K1: gather (Get) */
+  PSKV_K_ASSIGN_SORTED = 1, /* K2: sorted last-wins scatter (single batch) */
+  PSKV_K_ASSIGN_TILES = 2,  /* K2g: grouped sorted scatter, key-tile owner */
+  PSKV_K_GENERAL_MARK = 3,  /* K4a: chunk dedup + stamps / accumulate */
+  PSKV_K_GENERAL_COMMIT = 4,/* K4b: winner write */
+  PSKV_K_COUNT = 5
+};
+
+/* Create a shard owning keys [key_begin, key_end) on `device`.  The dense
+ * array ((key_end-key_begin) values) is allocated in HBM and zero-filled.
+ * key_end may be 2^32 (the whole key space: 17.2 GB for float). */
+int pskv_shard_create(int device, uint32_t key_begin, uint64_t key_end, int dtype, int mode,
+                      pskv_shard** out);
+/* As pskv_shard_create, with an explicit overflow-table capacity (slots, rounded
+ * up to a power of two; 0 = default). */
+int pskv_shard_create_ex(int device, uint32_t key_begin, uint64_t key_end, int dtype, int mode,
+                         uint64_t overflow_slots, pskv_shard** out);
+int pskv_shard_destroy(pskv_shard* s);
+
+/* Push: apply n (key, value) pairs.  Asynchronous on the shard's stream for
+ * PSKV_DEVICE inputs (the caller keeps them alive until the stream passes the
+ * call); host inputs are staged before return and may be reused immediately. */
+int pskv_add(pskv_shard* s, const uint32_t* keys, const void* vals, uint64_t n, int flags);
+/* Pull: out[i] = value of keys[i] (0 if never written).  Synchronous for host
+ * `out` (PSKV_HOST), stream-ordered for device `out` (PSKV_DEVICE). */
+int pskv_get(pskv_shard* s, const uint32_t* keys, uint64_t n, void* out, int flags);
+
+/* Grouped forms: nb batches in one call, semantically identical to nb
+ * consecutive pskv_add / pskv_get calls in array order, executed in a small,
+ * fixed number of kernel launches. */
+int pskv_add_grouped(pskv_shard* s, const pskv_batch* batches, uint64_t nb, int flags);
+int pskv_get_grouped(pskv_shard* s, const pskv_batch* batches, uint64_t nb, int flags);
+
+/* Wait for the shard's stream, grow the overflow table if needed, report
+ * sticky device errors. */
+int pskv_sync(pskv_shard* s);
+/* Zero every value (dense array and overflow table). */
+int pskv_clear(pskv_shard* s);
+
+/* Run the shard's work on an external hipStream_t (NULL = the shard's own stream). */
+int pskv_set_stream(pskv_shard* s, void* hip_stream);
+void* pskv_get_stream(pskv_shard* s);
+/* Device pointer of the dense array (for zero-copy inspection by tests/benches). */
+void* pskv_dense_ptr(pskv_shard* s);
+int pskv_shard_info(pskv_shard* s, pskv_info* info);
+
+/* Per-kernel timing with HIP events on the launch stream (off by default). */
+int pskv_set_timing(pskv_shard* s, int enable);
+int pskv_kernel_time(pskv_shard* s, int kernel, uint64_t* launches, double* total_ms,
+                     uint64_t* elements);
+int pskv_reset_timing(pskv_shard* s);
+
+/* Mirror of RangePartitionManager::Slice (base/range_partition_manager.hpp:19-46):
+ * walk `keys` once; a key goes to the current range if it lies in it or the
+ * current range is the last one, otherwise the range pointer advances.  Emits
+ * contiguous slices (range index, first key index, length) in order; at most
+ * nranges slices.  Returns the number of slices, or a negative error. */
+int pskv_range_slice(const uint64_t* range_begin, const uint64_t* range_end, int nranges,
+                     const uint32_t* keys, uint64_t n, int32_t* slice_range,
+                     uint64_t* slice_start, uint64_t* slice_len);
+
+const char* pskv_last_error(void);
+int pskv_abi_version(void);
+/* Number of HIP devices visible (0 when there is no GPU). */
+int pskv_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PSKV_H_ */

@@ -1,0 +1,14 @@
+"""parameter_server_amd — MI355X-native parameter-shard Add/Get (the server-side
+storage hot path of tkwong/parameter_server), as hand-written gfx950 HIP kernels
+behind a C ABI (include/pskv.h, libpskv.so).
+
+Importing this package loads libpskv.so and raises if it is missing: there is
+no CPU fallback on the product path.
+"""
+from ._lib import PskvError, lib  # noqa: F401  (fails loudly if the HIP library is absent)
+from .shard import Shard, device_count, range_slice  # noqa: F401
+from .storage import (AbstractStorage, CheckError, Flag, HipStorage, Message, Meta,  # noqa: F401
+                      RangePartitionManager, typed)
+
+__all__ = ["Shard", "HipStorage", "AbstractStorage", "Message", "Meta", "Flag",
+           "RangePartitionManager", "range_slice", "device_count", "CheckError", "PskvError"]

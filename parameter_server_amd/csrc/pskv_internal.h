@@ -1,0 +1,79 @@
+// pskv_internal.h — device-side data layout and kernel launch wrappers shared by
+// pskv_kernels.hip (device code) and pskv_shard.cpp (the C ABI host logic).
+//
+// HBM layout of one shard (DESIGN.md "Data layout in HBM"):
+//   dense[range]        value array, one slot per owned key, zero-initialised
+//   owner[range]        u64 last-writer stamps (epoch<<32 | group index), general path only
+//   ovf.keys[cap]       u64 overflow hash keys, EMPTY = ~0
+//   ovf.vals[cap]       overflow values
+//   ovf.owner[cap]      overflow stamps
+//   ovf.stat[2]         {occupied slots, sticky error bits}
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pskv {
+
+constexpr int kMaxBatches = 64;     // batches per grouped launch (kernarg budget)
+constexpr int kBlock = 256;         // threads per workgroup (4 waves)
+constexpr int kGatherVec = 4;       // keys per lane per step (16 B loads)
+constexpr int kGatherUnroll = 4;    // steps per lane
+constexpr int kGatherChunk = kBlock * kGatherVec * kGatherUnroll;  // 4096 keys / workgroup
+constexpr int kSortedUnroll = 2;
+constexpr int kSortedChunk = kBlock * 4 * kSortedUnroll;          // 2048 keys / workgroup
+constexpr int kGeneralChunk = 2048;  // keys per workgroup in the dedup path
+constexpr int kGeneralSlots = 4096;  // LDS hash slots (load factor <= 1/2)
+constexpr unsigned long long kEmpty64 = ~0ull;
+constexpr uint32_t kEmpty32 = 0xFFFFFFFFu;
+
+// Error bits in ovf.stat[1].
+constexpr uint32_t kErrOverflowFull = 1u;
+
+struct DevBatch {
+  const uint32_t* keys;
+  const void* vals;  // input values for Add, output for Get
+  uint64_t n;
+};
+
+// Passed by value as the kernel argument (fits the 4 KiB kernarg segment).
+struct GroupArgs {
+  int nb;
+  uint32_t wg_prefix[kMaxBatches + 1];  // first workgroup of each batch
+  uint64_t elem_prefix[kMaxBatches];    // group-wide index of each batch's first element
+  DevBatch b[kMaxBatches];
+};
+
+struct DenseView {
+  void* param;
+  uint32_t key_begin;
+  uint64_t range;  // number of owned keys, <= 2^32
+};
+
+struct Ovf {
+  unsigned long long* keys;
+  void* vals;
+  unsigned long long* owner;
+  uint32_t* stat;
+  uint64_t mask;  // capacity - 1 (capacity is a power of two)
+};
+
+// Launch wrappers (pskv_kernels.hip).  vb = value bytes (4 or 8), vec = all
+// pointers 16-byte aligned so 16 B vector accesses are legal.
+hipError_t launch_gather(int vb, bool vec, const GroupArgs& ga, uint32_t nwg, const DenseView& d,
+                         const Ovf& o, hipStream_t st);
+hipError_t launch_assign_sorted(int vb, bool vec, const uint32_t* keys, const void* vals,
+                                uint64_t n, const DenseView& d, uint32_t* flag, uint32_t epoch,
+                                hipStream_t st);
+hipError_t launch_assign_tiles(int vb, bool vec, const GroupArgs& ga, const DenseView& d,
+                               uint32_t tile_shift, uint64_t ntiles, uint32_t grid,
+                               uint32_t* flag, uint32_t epoch, hipStream_t st);
+hipError_t launch_general_mark(int dtype, int mode, const GroupArgs& ga, uint32_t nwg,
+                               const DenseView& d, const Ovf& o, unsigned long long* owner,
+                               const uint32_t* cond, uint32_t epoch, hipStream_t st);
+hipError_t launch_general_commit(int vb, const GroupArgs& ga, uint32_t nwg, const DenseView& d,
+                                 const Ovf& o, const unsigned long long* owner,
+                                 const uint32_t* cond, uint32_t epoch, hipStream_t st);
+hipError_t launch_ovf_rehash(int vb, const Ovf& from, uint64_t from_cap, const Ovf& to,
+                             hipStream_t st);
+
+}  // namespace pskv

@@ -1,0 +1,625 @@
+// pskv_kernels.hip — CDNA4 (gfx950) kernels of the parameter-shard Add/Get path.
+//
+// The reference does this work in libstdc++ containers on one CPU thread per
+// server (server/map_storage.hpp:17-45, server/vector_storage.hpp:16-49).  These
+// kernels are new, written for MI355X: 64-lane waves, 16-byte-per-lane HBM
+// accesses, LDS for per-workgroup duplicate resolution, no atomics on the
+// sorted path, and grouped launches so many push/pull batches share one
+// dispatch.  The work is HBM-bound byte movement (no MFMA); DESIGN.md prices
+// every kernel against the 8 TB/s HBM roofline.
+//
+//   K1  k_gather          Get: out[i] = value(keys[i])                 (map_storage.hpp:29-45)
+//   K2  k_assign_sorted   Add, one batch, sorted keys: the last element of
+//                         each equal-key run stores, nothing else does
+//   K2g k_assign_tiles    Add, grouped sorted batches: one workgroup owns a
+//                         key tile and applies the batches in call order
+//   K4a k_general_mark    Add, any order: per-workgroup LDS hash dedup, then
+//                         (assign) u64 last-writer stamps / (accumulate) one
+//                         atomic add per distinct key per workgroup
+//   K4b k_general_commit  Add, any order: the stamped winner of each key stores
+//
+// Semantics restated from the reference: last write wins within a call (index
+// order) and across calls (stream order) — map_storage.hpp:22-23 assigns in a
+// sequential loop; vector_storage.hpp:34-43 returns the LAST appended match.
+// A never-written key reads 0 (map_storage.hpp:33-37).
+#include "pskv_internal.h"
+
+namespace pskv {
+namespace {
+
+// ---------------------------------------------------------------- helpers
+
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
+}
+
+template <typename VT>
+struct Vec4;
+
+template <>
+struct Vec4<uint32_t> {
+  static __device__ __forceinline__ void load(const uint32_t* p, uint32_t (&v)[4]) {
+    const uint4 t = *reinterpret_cast<const uint4*>(p);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  }
+  static __device__ __forceinline__ void store(uint32_t* p, const uint32_t (&v)[4]) {
+    *reinterpret_cast<uint4*>(p) = make_uint4(v[0], v[1], v[2], v[3]);
+  }
+};
+
+template <>
+struct Vec4<unsigned long long> {
+  using T = unsigned long long;
+  static __device__ __forceinline__ void load(const T* p, T (&v)[4]) {
+    const ulonglong2 a = reinterpret_cast<const ulonglong2*>(p)[0];
+    const ulonglong2 b = reinterpret_cast<const ulonglong2*>(p)[1];
+    v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
+  }
+  static __device__ __forceinline__ void store(T* p, const T (&v)[4]) {
+    reinterpret_cast<ulonglong2*>(p)[0] = make_ulonglong2(v[0], v[1]);
+    reinterpret_cast<ulonglong2*>(p)[1] = make_ulonglong2(v[2], v[3]);
+  }
+};
+
+// Which batch of a grouped launch this workgroup serves (wave-uniform scan of
+// the kernarg prefix table; nb <= 64).
+__device__ __forceinline__ int batch_of(const GroupArgs& ga, uint32_t wg) {
+  int j = 0;
+  while (j + 1 < ga.nb && ga.wg_prefix[j + 1] <= wg) ++j;
+  return j;
+}
+
+// ------------------------------------------------------- overflow table
+// Open addressing with linear probing over u64 slots (EMPTY = ~0, so every
+// uint32 key is storable).  Keys are never deleted, so a non-EMPTY slot read
+// without an atomic is final; a stale EMPTY is resolved by the CAS.
+
+__device__ __forceinline__ long long ovf_find(const Ovf& o, uint32_t key) {
+  uint64_t h = fmix32(key) & o.mask;
+  for (uint64_t p = 0; p <= o.mask; ++p) {
+    const unsigned long long k = o.keys[h];
+    if (k == (unsigned long long)key) return (long long)h;
+    if (k == kEmpty64) return -1;
+    h = (h + 1) & o.mask;
+  }
+  return -1;
+}
+
+__device__ long long ovf_insert(const Ovf& o, uint32_t key) {
+  uint64_t h = fmix32(key) & o.mask;
+  for (uint64_t p = 0; p <= o.mask; ++p) {
+    const unsigned long long k = o.keys[h];
+    if (k == (unsigned long long)key) return (long long)h;
+    if (k == kEmpty64) {
+      const unsigned long long old = atomicCAS(&o.keys[h], kEmpty64, (unsigned long long)key);
+      if (old == kEmpty64) {
+        atomicAdd(&o.stat[0], 1u);
+        return (long long)h;
+      }
+      if (old == (unsigned long long)key) return (long long)h;
+    }
+    h = (h + 1) & o.mask;
+  }
+  atomicOr(&o.stat[1], kErrOverflowFull);
+  return -1;
+}
+
+template <typename VT>
+__device__ __forceinline__ VT load_one(const DenseView& d, const Ovf& o, uint32_t key) {
+  const uint32_t off = key - d.key_begin;
+  if ((uint64_t)off < d.range) return reinterpret_cast<const VT*>(d.param)[off];
+  const long long s = ovf_find(o, key);
+  return s >= 0 ? reinterpret_cast<const VT*>(o.vals)[s] : VT(0);
+}
+
+// ------------------------------------------------------------- K1 gather
+
+// Four keys of one lane: when they are four consecutive in-range keys starting
+// on a 4-aligned offset (dense pulls), one 16-byte (or 2x16-byte) load serves
+// them; otherwise four scalar gathers.
+template <typename VT>
+__device__ __forceinline__ void gather4(const DenseView& d, const Ovf& o, const uint32_t (&k)[4],
+                                        VT (&v)[4]) {
+  const uint32_t off0 = k[0] - d.key_begin;
+  const bool run = (k[1] == k[0] + 1u) & (k[2] == k[0] + 2u) & (k[3] == k[0] + 3u) &
+                   ((off0 & 3u) == 0u) & ((uint64_t)off0 + 3u < d.range);
+  if (run) {
+    Vec4<VT>::load(reinterpret_cast<const VT*>(d.param) + off0, v);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = load_one<VT>(d, o, k[e]);
+  }
+}
+
+template <typename VT, bool VEC>
+__global__ __launch_bounds__(kBlock) void k_gather(GroupArgs ga, DenseView d, Ovf o) {
+  const uint32_t wg = blockIdx.x;
+  const int j = batch_of(ga, wg);
+  const uint32_t* __restrict__ keys = ga.b[j].keys;
+  VT* __restrict__ out = reinterpret_cast<VT*>(const_cast<void*>(ga.b[j].vals));
+  const uint64_t n = ga.b[j].n;
+  const uint64_t base = (uint64_t)(wg - ga.wg_prefix[j]) * kGatherChunk;
+  const int tid = threadIdx.x;
+  if (VEC && base + kGatherChunk <= n) {
+    uint32_t k[kGatherUnroll][4];
+#pragma unroll
+    for (int u = 0; u < kGatherUnroll; ++u)
+      Vec4<uint32_t>::load(keys + base + (uint64_t)(u * kBlock + tid) * 4, k[u]);
+    VT v[kGatherUnroll][4];
+#pragma unroll
+    for (int u = 0; u < kGatherUnroll; ++u) gather4<VT>(d, o, k[u], v[u]);
+#pragma unroll
+    for (int u = 0; u < kGatherUnroll; ++u)
+      Vec4<VT>::store(out + base + (uint64_t)(u * kBlock + tid) * 4, v[u]);
+  } else {
+    const uint64_t end = n < base + kGatherChunk ? n : base + kGatherChunk;
+    for (uint64_t i = base + tid; i < end; i += kBlock) out[i] = load_one<VT>(d, o, keys[i]);
+  }
+}
+
+// ----------------------------------------------------- K2 sorted assign
+// In a non-decreasing batch the duplicates of a key are adjacent, so the last
+// occurrence is the element whose successor differs (or that has none).  Only
+// that element stores: deterministic last-write-wins without atomics.  Every
+// element also checks that it is in [lo, hi) and not greater than its
+// successor; a violation tags `flag` with the call's epoch and the general path
+// (launched behind it, conditional on the tag) recomputes every key of the
+// batch, so a wrong sorted hint costs time, never correctness.
+
+template <typename VT>
+__device__ __forceinline__ bool scalar_elem(const uint32_t* __restrict__ keys,
+                                            const VT* __restrict__ vals, uint64_t n, uint64_t i,
+                                            const DenseView& d, uint64_t lo, uint64_t hi) {
+  const uint32_t k = keys[i];
+  const bool hn = i + 1 < n;
+  const uint32_t nk = hn ? keys[i + 1] : 0u;
+  const uint64_t off = (uint32_t)(k - d.key_begin);
+  bool bad = hn && k > nk;
+  if (off < lo || off >= hi)
+    bad = true;
+  else if (!hn || k != nk)
+    reinterpret_cast<VT*>(d.param)[off] = vals[i];
+  return bad;
+}
+
+template <typename VT>
+__device__ __forceinline__ bool scatter4_sorted(const DenseView& d, const uint32_t (&k)[4],
+                                                const VT (&v)[4], uint32_t nk, bool has_next,
+                                                uint64_t lo, uint64_t hi) {
+  VT* __restrict__ param = reinterpret_cast<VT*>(d.param);
+  const uint32_t off0 = k[0] - d.key_begin;
+  const bool run = (k[1] == k[0] + 1u) & (k[2] == k[0] + 2u) & (k[3] == k[0] + 3u) &
+                   ((off0 & 3u) == 0u) & ((uint64_t)off0 >= lo) & ((uint64_t)off0 + 3u < hi);
+  bool bad = false;
+  if (run && !(has_next && nk <= k[3])) {
+    Vec4<VT>::store(param + off0, v);  // four distinct consecutive keys, last one ends its run
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const bool hn = e < 3 || has_next;
+      const uint32_t nx = e < 3 ? k[e + 1 < 4 ? e + 1 : 3] : nk;
+      const uint64_t off = (uint32_t)(k[e] - d.key_begin);
+      if (hn && k[e] > nx) bad = true;
+      if (off < lo || off >= hi)
+        bad = true;
+      else if (!hn || k[e] != nx)
+        param[off] = v[e];
+    }
+  }
+  return bad;
+}
+
+template <typename VT, bool VEC>
+__global__ __launch_bounds__(kBlock) void k_assign_sorted(const uint32_t* __restrict__ keys,
+                                                          const VT* __restrict__ vals, uint64_t n,
+                                                          DenseView d, uint32_t* flag,
+                                                          uint32_t epoch) {
+  const uint64_t base = (uint64_t)blockIdx.x * kSortedChunk;
+  const int tid = threadIdx.x;
+  bool bad = false;
+  if (VEC && base + kSortedChunk <= n) {
+    uint32_t k[kSortedUnroll][4];
+    VT v[kSortedUnroll][4];
+    uint32_t nk[kSortedUnroll];
+    bool hn[kSortedUnroll];
+#pragma unroll
+    for (int u = 0; u < kSortedUnroll; ++u) {
+      const uint64_t i = base + (uint64_t)(u * kBlock + tid) * 4;
+      Vec4<uint32_t>::load(keys + i, k[u]);
+      Vec4<VT>::load(vals + i, v[u]);
+      hn[u] = i + 4 < n;
+      nk[u] = hn[u] ? keys[i + 4] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < kSortedUnroll; ++u)
+      bad |= scatter4_sorted<VT>(d, k[u], v[u], nk[u], hn[u], 0, d.range);
+  } else {
+    const uint64_t end = n < base + kSortedChunk ? n : base + kSortedChunk;
+    for (uint64_t i = base + tid; i < end; i += kBlock)
+      bad |= scalar_elem<VT>(keys, vals, n, i, d, 0, d.range);
+  }
+  if (bad) *flag = epoch;
+}
+
+// --------------------------------------------- K2g grouped sorted assign
+// Grouped batches may share keys (a later batch must win), so the elementwise
+// K2 cannot run them concurrently.  Instead the key range is cut into tiles of
+// 2^tile_shift keys; ONE workgroup owns a tile and applies, in call order, the
+// slice of every batch that falls into it (a contiguous segment of a sorted
+// batch, found by interpolation + binary search).  A workgroup barrier between
+// batches orders the stores of one CU to one address; different tiles touch
+// disjoint keys, so no cross-workgroup ordering is needed and the stores stay
+// plain, coalesced and atomic-free.
+//
+// Verification: tile t of batch j gets segment [lb(lo_t), lb(hi_t)) with the
+// SAME deterministic search for a shared boundary, so the segments of one batch
+// chain without gaps from 0 (first tile) to n (last tile).  Each element checks
+// that it lies in its tile and does not exceed its successor; if every check
+// passes the whole batch was sorted.  Any failure tags `flag` for the repair.
+
+__device__ __forceinline__ uint64_t lower_bound_interp(const uint32_t* __restrict__ keys,
+                                                       uint64_t n, uint32_t x, uint32_t first,
+                                                       uint32_t last) {
+  // Called only when first < x <= last, so (for a sorted batch) the answer is
+  // in [1, n-1].  All probes stay in [0, n-1] whatever the data.
+  uint64_t lo = 1, hi = n - 1;
+  if (n > 2 && last > first) {
+    uint64_t g = (uint64_t)(x - first) * (n - 1) / (uint64_t)(last - first);
+    g = g < lo ? lo : (g > hi ? hi : g);
+    if (keys[g] >= x) {
+      if (keys[g - 1] < x) return g;
+      hi = g - 1;
+    } else {
+      lo = g + 1;
+    }
+  }
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (keys[mid] >= x)
+      hi = mid;
+    else
+      lo = mid + 1;
+  }
+  return lo;
+}
+
+template <typename VT, bool VEC>
+__device__ __forceinline__ bool apply_segment(const DevBatch& b, uint64_t s, uint64_t e,
+                                              const DenseView& d, uint64_t lo, uint64_t hi) {
+  const uint32_t* __restrict__ keys = b.keys;
+  const VT* __restrict__ vals = reinterpret_cast<const VT*>(b.vals);
+  const uint64_t n = b.n;
+  const int tid = threadIdx.x;
+  bool bad = false;
+  if (VEC) {
+    const uint64_t a = (s + 3) & ~3ull;
+    const uint64_t va = a < e ? a : e;
+    const uint64_t z0 = e & ~3ull;
+    const uint64_t vz = z0 > va ? z0 : va;
+    if ((uint64_t)tid < va - s) bad |= scalar_elem<VT>(keys, vals, n, s + tid, d, lo, hi);
+    if ((uint64_t)tid < e - vz) bad |= scalar_elem<VT>(keys, vals, n, vz + tid, d, lo, hi);
+    for (uint64_t g = va + (uint64_t)tid * 4; g < vz; g += (uint64_t)kBlock * 4) {
+      uint32_t k[4];
+      VT v[4];
+      Vec4<uint32_t>::load(keys + g, k);
+      Vec4<VT>::load(vals + g, v);
+      const bool hn = g + 4 < n;
+      const uint32_t nk = hn ? keys[g + 4] : 0u;
+      bad |= scatter4_sorted<VT>(d, k, v, nk, hn, lo, hi);
+    }
+  } else {
+    for (uint64_t i = s + tid; i < e; i += kBlock)
+      bad |= scalar_elem<VT>(keys, vals, n, i, d, lo, hi);
+  }
+  return bad;
+}
+
+template <typename VT, bool VEC>
+__global__ __launch_bounds__(kBlock) void k_assign_tiles(GroupArgs ga, DenseView d,
+                                                         uint32_t tile_shift, uint64_t ntiles,
+                                                         uint32_t* flag, uint32_t epoch) {
+  __shared__ uint64_t s_seg_s[kMaxBatches];
+  __shared__ uint64_t s_seg_e[kMaxBatches];
+  __shared__ unsigned long long s_mask;
+  const int tid = threadIdx.x;
+  // Wave 0, lane j keeps batch j's endpoints for the whole launch.
+  uint32_t first = 0, last = 0;
+  uint64_t n = 0;
+  bool ok = false;
+  const uint32_t* keys = nullptr;
+  if (tid < ga.nb) {
+    keys = ga.b[tid].keys;
+    n = ga.b[tid].n;
+    if (n > 0) {
+      first = keys[0];
+      last = keys[n - 1];
+      const uint64_t fo = (uint32_t)(first - d.key_begin);
+      const uint64_t lo_ = (uint32_t)(last - d.key_begin);
+      ok = fo < d.range && lo_ < d.range && first <= last;
+      if (!ok && blockIdx.x == 0) *flag = epoch;  // out-of-range or inverted endpoints
+    }
+  }
+  bool bad = false;
+  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const uint64_t tlo = t << tile_shift;
+    const uint64_t tend = tlo + (1ull << tile_shift);
+    const uint64_t thi = tend < d.range ? tend : d.range;
+    __syncthreads();  // previous tile's readers of s_mask / s_seg_* are done
+    if (tid < 64) {
+      bool act = false;
+      uint64_t s = 0, e = 0;
+      if (ok) {
+        const uint64_t fo = (uint32_t)(first - d.key_begin);
+        const uint64_t lo_ = (uint32_t)(last - d.key_begin);
+        if (fo < thi && lo_ >= tlo) {
+          s = fo >= tlo ? 0 : lower_bound_interp(keys, n, d.key_begin + (uint32_t)tlo, first, last);
+          e = lo_ < thi ? n : lower_bound_interp(keys, n, d.key_begin + (uint32_t)thi, first, last);
+          if (s > e)
+            bad = true;
+          else
+            act = s < e;
+        }
+      }
+      if (tid < kMaxBatches) {
+        s_seg_s[tid] = s;
+        s_seg_e[tid] = e;
+      }
+      const unsigned long long m = __ballot(act);
+      if (tid == 0) s_mask = m;
+    }
+    __syncthreads();
+    unsigned long long m = s_mask;
+    while (m) {
+      const int j = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      bad |= apply_segment<VT, VEC>(ga.b[j], s_seg_s[j], s_seg_e[j], d, tlo, thi);
+      __syncthreads();  // batch j's stores precede batch j+1's in this tile
+    }
+  }
+  if (bad) *flag = epoch;
+}
+
+// ------------------------------------------------ K4 general (any order)
+// K4a: a workgroup takes 2048 consecutive elements of one batch and folds them
+// into a 4096-slot LDS hash (key -> max element index, or key -> sum).  Then
+// each distinct key of the chunk does ONE global operation:
+//   assign:     atomicMax(owner[key], epoch<<32 | group index of its last occurrence)
+//   accumulate: atomicAdd(param[key], chunk sum)
+// so a Zipf-hot key costs one atomic per chunk, not one per occurrence.
+// K4b (assign): every element whose stamp won stores its value — exactly one
+// element per key, the last one in call order.  The stamp array is never reset:
+// epochs increase, so an old stamp always loses.
+
+template <typename AT>
+__device__ __forceinline__ void global_accumulate(const DenseView& d, const Ovf& o, uint32_t k,
+                                                  AT v) {
+  const uint32_t off = k - d.key_begin;
+  if ((uint64_t)off < d.range) {
+    atomicAdd(reinterpret_cast<AT*>(d.param) + off, v);
+  } else {
+    const long long s = ovf_insert(o, k);
+    if (s >= 0) atomicAdd(reinterpret_cast<AT*>(o.vals) + s, v);
+  }
+}
+
+__device__ __forceinline__ void global_stamp(const DenseView& d, const Ovf& o,
+                                             unsigned long long* owner, uint32_t k,
+                                             unsigned long long tag) {
+  const uint32_t off = k - d.key_begin;
+  if ((uint64_t)off < d.range) {
+    atomicMax(owner + off, tag);
+  } else {
+    const long long s = ovf_insert(o, k);
+    if (s >= 0) atomicMax(o.owner + s, tag);
+  }
+}
+
+template <typename AT, int MODE>
+__global__ __launch_bounds__(kBlock) void k_general_mark(GroupArgs ga, DenseView d, Ovf o,
+                                                         unsigned long long* owner,
+                                                         const uint32_t* cond, uint32_t epoch) {
+  if (cond != nullptr && *cond != epoch) return;  // repair launch, sorted path was right
+  __shared__ uint32_t hk[kGeneralSlots];
+  __shared__ uint32_t hidx[MODE == 0 ? kGeneralSlots : 1];
+  __shared__ AT hsum[MODE == 1 ? kGeneralSlots : 1];
+  const uint32_t wg = blockIdx.x;
+  const int j = batch_of(ga, wg);
+  const uint32_t* __restrict__ keys = ga.b[j].keys;
+  const AT* __restrict__ vals = reinterpret_cast<const AT*>(ga.b[j].vals);
+  const uint64_t n = ga.b[j].n;
+  const uint64_t base = (uint64_t)(wg - ga.wg_prefix[j]) * kGeneralChunk;
+  const uint64_t gbase = ga.elem_prefix[j] + base;
+  const int tid = threadIdx.x;
+  for (int s = tid; s < kGeneralSlots; s += kBlock) {
+    hk[s] = kEmpty32;
+    if (MODE == 0)
+      hidx[s] = 0;
+    else
+      hsum[s] = AT(0);
+  }
+  __syncthreads();
+#pragma unroll 2
+  for (int r = 0; r < kGeneralChunk / kBlock; ++r) {
+    const int li = r * kBlock + tid;
+    const uint64_t i = base + li;
+    if (i < n) {
+      const uint32_t k = keys[i];
+      if (k == kEmpty32) {  // the LDS sentinel itself: bypass the LDS table
+        if (MODE == 0)
+          global_stamp(d, o, owner, k, ((unsigned long long)epoch << 32) | (gbase + li));
+        else
+          global_accumulate<AT>(d, o, k, vals[i]);
+      } else {
+        uint32_t h = fmix32(k) & (kGeneralSlots - 1);
+        for (;;) {
+          const uint32_t old = atomicCAS(&hk[h], kEmpty32, k);
+          if (old == kEmpty32 || old == k) break;
+          h = (h + 1) & (kGeneralSlots - 1);
+        }
+        if (MODE == 0)
+          atomicMax(&hidx[h], (uint32_t)li);
+        else
+          atomicAdd(&hsum[h], vals[i]);
+      }
+    }
+  }
+  __syncthreads();
+  for (int s = tid; s < kGeneralSlots; s += kBlock) {
+    const uint32_t k = hk[s];
+    if (k == kEmpty32) continue;
+    if (MODE == 0)
+      global_stamp(d, o, owner, k, ((unsigned long long)epoch << 32) | (gbase + hidx[s]));
+    else
+      global_accumulate<AT>(d, o, k, hsum[s]);
+  }
+}
+
+template <typename VT>
+__global__ __launch_bounds__(kBlock) void k_general_commit(GroupArgs ga, DenseView d, Ovf o,
+                                                           const unsigned long long* owner,
+                                                           const uint32_t* cond, uint32_t epoch) {
+  if (cond != nullptr && *cond != epoch) return;
+  const uint32_t wg = blockIdx.x;
+  const int j = batch_of(ga, wg);
+  const uint32_t* __restrict__ keys = ga.b[j].keys;
+  const VT* __restrict__ vals = reinterpret_cast<const VT*>(ga.b[j].vals);
+  const uint64_t n = ga.b[j].n;
+  const uint64_t base = (uint64_t)(wg - ga.wg_prefix[j]) * kGeneralChunk;
+  const uint64_t gbase = ga.elem_prefix[j] + base;
+  const int tid = threadIdx.x;
+#pragma unroll 2
+  for (int r = 0; r < kGeneralChunk / kBlock; ++r) {
+    const int li = r * kBlock + tid;
+    const uint64_t i = base + li;
+    if (i >= n) break;
+    const uint32_t k = keys[i];
+    const unsigned long long tag = ((unsigned long long)epoch << 32) | (gbase + li);
+    const uint32_t off = k - d.key_begin;
+    if ((uint64_t)off < d.range) {
+      if (owner[off] == tag) reinterpret_cast<VT*>(d.param)[off] = vals[i];
+    } else {
+      const long long s = ovf_find(o, k);
+      if (s >= 0 && o.owner[s] == tag) reinterpret_cast<VT*>(o.vals)[s] = vals[i];
+    }
+  }
+}
+
+template <typename VT>
+__global__ __launch_bounds__(kBlock) void k_ovf_rehash(Ovf from, uint64_t from_cap, Ovf to) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < from_cap;
+       i += (uint64_t)gridDim.x * kBlock) {
+    const unsigned long long k = from.keys[i];
+    if (k == kEmpty64) continue;
+    const long long s = ovf_insert(to, (uint32_t)k);
+    if (s >= 0) reinterpret_cast<VT*>(to.vals)[s] = reinterpret_cast<const VT*>(from.vals)[i];
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------- launch wrappers
+
+hipError_t launch_gather(int vb, bool vec, const GroupArgs& ga, uint32_t nwg, const DenseView& d,
+                         const Ovf& o, hipStream_t st) {
+  if (nwg == 0) return hipSuccess;
+  if (vb == 4) {
+    if (vec)
+      k_gather<uint32_t, true><<<nwg, kBlock, 0, st>>>(ga, d, o);
+    else
+      k_gather<uint32_t, false><<<nwg, kBlock, 0, st>>>(ga, d, o);
+  } else {
+    if (vec)
+      k_gather<unsigned long long, true><<<nwg, kBlock, 0, st>>>(ga, d, o);
+    else
+      k_gather<unsigned long long, false><<<nwg, kBlock, 0, st>>>(ga, d, o);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_assign_sorted(int vb, bool vec, const uint32_t* keys, const void* vals,
+                                uint64_t n, const DenseView& d, uint32_t* flag, uint32_t epoch,
+                                hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const uint32_t nwg = (uint32_t)((n + kSortedChunk - 1) / kSortedChunk);
+  if (vb == 4) {
+    auto v = reinterpret_cast<const uint32_t*>(vals);
+    if (vec)
+      k_assign_sorted<uint32_t, true><<<nwg, kBlock, 0, st>>>(keys, v, n, d, flag, epoch);
+    else
+      k_assign_sorted<uint32_t, false><<<nwg, kBlock, 0, st>>>(keys, v, n, d, flag, epoch);
+  } else {
+    auto v = reinterpret_cast<const unsigned long long*>(vals);
+    if (vec)
+      k_assign_sorted<unsigned long long, true><<<nwg, kBlock, 0, st>>>(keys, v, n, d, flag, epoch);
+    else
+      k_assign_sorted<unsigned long long, false><<<nwg, kBlock, 0, st>>>(keys, v, n, d, flag, epoch);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_assign_tiles(int vb, bool vec, const GroupArgs& ga, const DenseView& d,
+                               uint32_t tile_shift, uint64_t ntiles, uint32_t grid,
+                               uint32_t* flag, uint32_t epoch, hipStream_t st) {
+  if (ntiles == 0 || grid == 0) return hipSuccess;
+  if (vb == 4) {
+    if (vec)
+      k_assign_tiles<uint32_t, true><<<grid, kBlock, 0, st>>>(ga, d, tile_shift, ntiles, flag, epoch);
+    else
+      k_assign_tiles<uint32_t, false><<<grid, kBlock, 0, st>>>(ga, d, tile_shift, ntiles, flag, epoch);
+  } else {
+    if (vec)
+      k_assign_tiles<unsigned long long, true><<<grid, kBlock, 0, st>>>(ga, d, tile_shift, ntiles,
+                                                                       flag, epoch);
+    else
+      k_assign_tiles<unsigned long long, false><<<grid, kBlock, 0, st>>>(ga, d, tile_shift, ntiles,
+                                                                        flag, epoch);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_general_mark(int dtype, int mode, const GroupArgs& ga, uint32_t nwg,
+                               const DenseView& d, const Ovf& o, unsigned long long* owner,
+                               const uint32_t* cond, uint32_t epoch, hipStream_t st) {
+  if (nwg == 0) return hipSuccess;
+  if (mode == 0) {
+    // assign: value bits are never read here; the AT parameter only sizes unused LDS
+    k_general_mark<uint32_t, 0><<<nwg, kBlock, 0, st>>>(ga, d, o, owner, cond, epoch);
+  } else if (dtype == 0) {
+    k_general_mark<int, 1><<<nwg, kBlock, 0, st>>>(ga, d, o, owner, cond, epoch);
+  } else if (dtype == 1) {
+    k_general_mark<float, 1><<<nwg, kBlock, 0, st>>>(ga, d, o, owner, cond, epoch);
+  } else {
+    k_general_mark<double, 1><<<nwg, kBlock, 0, st>>>(ga, d, o, owner, cond, epoch);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_general_commit(int vb, const GroupArgs& ga, uint32_t nwg, const DenseView& d,
+                                 const Ovf& o, const unsigned long long* owner,
+                                 const uint32_t* cond, uint32_t epoch, hipStream_t st) {
+  if (nwg == 0) return hipSuccess;
+  if (vb == 4)
+    k_general_commit<uint32_t><<<nwg, kBlock, 0, st>>>(ga, d, o, owner, cond, epoch);
+  else
+    k_general_commit<unsigned long long><<<nwg, kBlock, 0, st>>>(ga, d, o, owner, cond, epoch);
+  return hipGetLastError();
+}
+
+hipError_t launch_ovf_rehash(int vb, const Ovf& from, uint64_t from_cap, const Ovf& to,
+                             hipStream_t st) {
+  uint64_t g = (from_cap + kBlock - 1) / kBlock;
+  if (g > 4096) g = 4096;
+  if (g == 0) return hipSuccess;
+  if (vb == 4)
+    k_ovf_rehash<uint32_t><<<(uint32_t)g, kBlock, 0, st>>>(from, from_cap, to);
+  else
+    k_ovf_rehash<unsigned long long><<<(uint32_t)g, kBlock, 0, st>>>(from, from_cap, to);
+  return hipGetLastError();
+}
+
+}  // namespace pskv

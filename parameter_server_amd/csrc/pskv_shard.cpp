@@ -1,0 +1,773 @@
+// pskv_shard.cpp — host side of the C ABI declared in include/pskv.h.
+//
+// One pskv_shard is what the reference calls a storage: the object
+// Engine::CreateTable builds per server thread (driver/engine.hpp:100-109) and
+// the consistency model drives through AbstractStorage::Add/Get
+// (server/abstract_storage.hpp:14-32).  Here it owns a dense HBM array for its
+// key range, an overflow hash table for every other key, a stream, and
+// pinned/device staging for host (zmq-buffer) inputs.
+//
+// Call flow of an assign-mode Add (DESIGN.md "Add"):
+//   host inputs   → copy into pinned staging while checking "sorted and in
+//                   range" on the CPU → H2D → K2 if verified, else K4a+K4b.
+//   device inputs → PSKV_SORTED_HINT: K2 (one batch) or K2g (group), each
+//                   verifying on device, followed by K4a+K4b launched
+//                   conditional on the verification tag (they exit at once
+//                   when the hint held).  No hint: K4a+K4b.
+// Accumulate-mode Add: K4a (always correct, order free).
+// Get: K1 (one launch per group of <= 64 batches).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "pskv.h"
+#include "pskv_internal.h"
+
+using namespace pskv;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define PSKV_HIP(call)                                                                     \
+  do {                                                                                     \
+    hipError_t e_ = (call);                                                                \
+    if (e_ != hipSuccess)                                                                  \
+      return fail(PSKV_EHIP, std::string(#call) + ": " + hipGetErrorString(e_));           \
+  } while (0)
+
+int value_bytes(int dtype) {
+  switch (dtype) {
+    case PSKV_I32:
+    case PSKV_F32:
+      return 4;
+    case PSKV_F64:
+      return 8;
+    default:
+      return 0;
+  }
+}
+
+uint64_t next_pow2(uint64_t x) {
+  uint64_t p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+constexpr uint64_t kDefaultOverflowSlots = 1ull << 16;
+
+struct TimedLaunch {
+  int kernel;
+  hipEvent_t a, b;
+  uint64_t elems;
+};
+
+}  // namespace
+
+struct pskv_shard {
+  int device = 0;
+  int dtype = PSKV_F32;
+  int mode = PSKV_ASSIGN;
+  int vb = 4;
+  uint32_t key_begin = 0;
+  uint64_t range = 0;
+  void* dense = nullptr;
+  unsigned long long* owner = nullptr;  // u64 stamps, allocated on first general-path use
+  // overflow table
+  Ovf ovf{};
+  uint64_t ocap = 0;
+  uint64_t ocount_known = 0;
+  // device words: [0] verification tag
+  uint32_t* flag = nullptr;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  uint32_t epoch = 0;
+  // staging for host inputs/outputs
+  void* hstage = nullptr;
+  size_t hstage_bytes = 0;
+  hipEvent_t hstage_free = nullptr;
+  bool hstage_pending = false;
+  void* dstage = nullptr;
+  size_t dstage_bytes = 0;
+  // timing
+  bool timing = false;
+  std::vector<TimedLaunch> pending;
+  std::vector<hipEvent_t> event_pool;
+  uint64_t t_launches[PSKV_K_COUNT] = {};
+  double t_ms[PSKV_K_COUNT] = {};
+  uint64_t t_elems[PSKV_K_COUNT] = {};
+  // stats
+  uint64_t n_add = 0, n_get = 0, n_sorted = 0, n_general = 0;
+
+  DenseView dview() const { return DenseView{dense, key_begin, range}; }
+};
+
+namespace {
+
+int use_device(pskv_shard* s) {
+  PSKV_HIP(hipSetDevice(s->device));
+  return PSKV_OK;
+}
+
+hipEvent_t take_event(pskv_shard* s) {
+  if (!s->event_pool.empty()) {
+    hipEvent_t e = s->event_pool.back();
+    s->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+// Bracket one kernel launch with events when timing is on.
+struct LaunchTimer {
+  pskv_shard* s;
+  int kernel;
+  uint64_t elems;
+  hipEvent_t a = nullptr, b = nullptr;
+  LaunchTimer(pskv_shard* s_, int k, uint64_t e) : s(s_), kernel(k), elems(e) {
+    if (s->timing) {
+      a = take_event(s);
+      b = take_event(s);
+      if (a && b) (void)hipEventRecord(a, s->stream);
+    }
+  }
+  void done() {
+    if (a && b) {
+      (void)hipEventRecord(b, s->stream);
+      s->pending.push_back(TimedLaunch{kernel, a, b, elems});
+    }
+    a = b = nullptr;
+  }
+};
+
+int drain_timing(pskv_shard* s) {
+  for (auto& t : s->pending) {
+    PSKV_HIP(hipEventSynchronize(t.b));
+    float ms = 0.f;
+    PSKV_HIP(hipEventElapsedTime(&ms, t.a, t.b));
+    s->t_launches[t.kernel] += 1;
+    s->t_ms[t.kernel] += ms;
+    s->t_elems[t.kernel] += t.elems;
+    s->event_pool.push_back(t.a);
+    s->event_pool.push_back(t.b);
+  }
+  s->pending.clear();
+  return PSKV_OK;
+}
+
+int alloc_overflow(Ovf* o, uint64_t cap, int vb, hipStream_t st) {
+  *o = Ovf{};
+  PSKV_HIP(hipMalloc(&o->keys, cap * sizeof(unsigned long long)));
+  PSKV_HIP(hipMalloc(&o->vals, cap * (size_t)vb));
+  PSKV_HIP(hipMalloc(&o->owner, cap * sizeof(unsigned long long)));
+  PSKV_HIP(hipMalloc(&o->stat, 2 * sizeof(uint32_t)));
+  PSKV_HIP(hipMemsetAsync(o->keys, 0xFF, cap * sizeof(unsigned long long), st));
+  PSKV_HIP(hipMemsetAsync(o->vals, 0, cap * (size_t)vb, st));
+  PSKV_HIP(hipMemsetAsync(o->owner, 0, cap * sizeof(unsigned long long), st));
+  PSKV_HIP(hipMemsetAsync(o->stat, 0, 2 * sizeof(uint32_t), st));
+  o->mask = cap - 1;
+  return PSKV_OK;
+}
+
+void free_overflow(Ovf* o) {
+  if (o->keys) (void)hipFree(o->keys);
+  if (o->vals) (void)hipFree(o->vals);
+  if (o->owner) (void)hipFree(o->owner);
+  if (o->stat) (void)hipFree(o->stat);
+  *o = Ovf{};
+}
+
+// Grow the overflow table to at least `need` occupied slots at load <= 1/2.
+int grow_overflow(pskv_shard* s, uint64_t need) {
+  uint64_t cap = s->ocap;
+  while (cap < 2 * need) cap <<= 1;
+  if (cap == s->ocap) return PSKV_OK;
+  Ovf n{};
+  int rc = alloc_overflow(&n, cap, s->vb, s->stream);
+  if (rc) return rc;
+  PSKV_HIP(launch_ovf_rehash(s->vb, s->ovf, s->ocap, n, s->stream));
+  // carry the sticky error bits
+  PSKV_HIP(hipMemcpyAsync(n.stat + 1, s->ovf.stat + 1, sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                          s->stream));
+  PSKV_HIP(hipStreamSynchronize(s->stream));
+  free_overflow(&s->ovf);
+  s->ovf = n;
+  s->ocap = cap;
+  return PSKV_OK;
+}
+
+// Read {count, err} of the overflow table (synchronises the stream).
+int read_overflow_stat(pskv_shard* s, uint32_t* count, uint32_t* err) {
+  uint32_t st[2] = {0, 0};
+  PSKV_HIP(hipMemcpyAsync(st, s->ovf.stat, sizeof(st), hipMemcpyDeviceToHost, s->stream));
+  PSKV_HIP(hipStreamSynchronize(s->stream));
+  *count = st[0];
+  *err = st[1];
+  s->ocount_known = st[0];
+  return PSKV_OK;
+}
+
+int ensure_hstage(pskv_shard* s, size_t bytes) {
+  if (s->hstage_pending) {
+    PSKV_HIP(hipEventSynchronize(s->hstage_free));
+    s->hstage_pending = false;
+  }
+  if (s->hstage_bytes >= bytes) return PSKV_OK;
+  if (s->hstage) (void)hipHostFree(s->hstage);
+  s->hstage = nullptr;
+  size_t nb = std::max<size_t>(bytes + bytes / 2, 1 << 20);
+  if (hipHostMalloc(&s->hstage, nb, hipHostMallocDefault) != hipSuccess) {
+    s->hstage_bytes = 0;
+    return fail(PSKV_ENOMEM, "pinned staging allocation failed");
+  }
+  s->hstage_bytes = nb;
+  return PSKV_OK;
+}
+
+int ensure_dstage(pskv_shard* s, size_t bytes) {
+  if (s->dstage_bytes >= bytes) return PSKV_OK;
+  if (s->dstage) {
+    // stream-ordered free: the buffer may still be read by queued kernels
+    PSKV_HIP(hipStreamSynchronize(s->stream));
+    (void)hipFree(s->dstage);
+  }
+  s->dstage = nullptr;
+  size_t nb = std::max<size_t>(bytes + bytes / 2, 1 << 20);
+  if (hipMalloc(&s->dstage, nb) != hipSuccess) {
+    s->dstage_bytes = 0;
+    return fail(PSKV_ENOMEM, "device staging allocation failed");
+  }
+  s->dstage_bytes = nb;
+  return PSKV_OK;
+}
+
+size_t round16(size_t x) { return (x + 15) & ~size_t(15); }
+
+// Build the kernarg group descriptor for batches [b, e) with `chunk` elements
+// per workgroup.  Returns the workgroup count.
+uint32_t build_group(const std::vector<pskv_batch>& v, size_t b, size_t e, uint64_t chunk,
+                     GroupArgs* ga) {
+  std::memset(ga, 0, sizeof(*ga));
+  ga->nb = (int)(e - b);
+  uint64_t wg = 0, el = 0;
+  for (size_t i = b; i < e; ++i) {
+    const int j = (int)(i - b);
+    ga->wg_prefix[j] = (uint32_t)wg;
+    ga->elem_prefix[j] = el;
+    ga->b[j] = DevBatch{v[i].keys, v[i].vals, v[i].n};
+    wg += (v[i].n + chunk - 1) / chunk;
+    el += v[i].n;
+  }
+  ga->wg_prefix[e - b] = (uint32_t)wg;
+  return (uint32_t)wg;
+}
+
+uint32_t next_epoch(pskv_shard* s) {
+  // Stamps are epoch<<32|index; on wrap-around the stamp arrays are reset so
+  // that every old stamp still loses to the new epoch 1.
+  if (s->epoch == 0xFFFFFFFFu) {
+    if (s->owner) (void)hipMemsetAsync(s->owner, 0, s->range * sizeof(unsigned long long), s->stream);
+    (void)hipMemsetAsync(s->ovf.owner, 0, s->ocap * sizeof(unsigned long long), s->stream);
+    (void)hipMemsetAsync(s->flag, 0, sizeof(uint32_t), s->stream);
+    s->epoch = 0;
+  }
+  return ++s->epoch;
+}
+
+// Split a batch list into launch groups: <= kMaxBatches batches and < 2^32
+// elements each (the stamp index is 32 bits).  Empty batches are dropped.
+std::vector<std::pair<size_t, size_t>> split_groups(const std::vector<pskv_batch>& v) {
+  std::vector<std::pair<size_t, size_t>> out;
+  size_t b = 0;
+  while (b < v.size()) {
+    size_t e = b;
+    uint64_t el = 0;
+    while (e < v.size() && e - b < (size_t)kMaxBatches && el + v[e].n < (1ull << 32)) {
+      el += v[e].n;
+      ++e;
+    }
+    out.emplace_back(b, e);
+    b = e;
+  }
+  return out;
+}
+
+// The general (any order) Add over one launch group.  `cond` non-null makes
+// it a repair that runs only when the sorted path tagged `epoch`.
+int general_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t e,
+                uint32_t epoch, const uint32_t* cond) {
+  if (s->mode == PSKV_ASSIGN && !s->owner) {
+    // The stamp array is only needed once the general path can run: allocate it
+    // on first use (8 B per owned key).
+    const size_t bytes = s->range * sizeof(unsigned long long);
+    if (hipMalloc(&s->owner, bytes) != hipSuccess) {
+      s->owner = nullptr;
+      return fail(PSKV_ENOMEM, "stamp array allocation failed");
+    }
+    PSKV_HIP(hipMemsetAsync(s->owner, 0, bytes, s->stream));
+  }
+  GroupArgs ga;
+  const uint32_t nwg = build_group(v, b, e, kGeneralChunk, &ga);
+  uint64_t elems = 0;
+  for (size_t i = b; i < e; ++i) elems += v[i].n;
+  {
+    LaunchTimer t(s, PSKV_K_GENERAL_MARK, elems);
+    PSKV_HIP(launch_general_mark(s->dtype, s->mode, ga, nwg, s->dview(), s->ovf, s->owner, cond,
+                                 epoch, s->stream));
+    t.done();
+  }
+  s->n_general++;
+  if (s->mode == PSKV_ASSIGN) {
+    LaunchTimer t(s, PSKV_K_GENERAL_COMMIT, elems);
+    PSKV_HIP(launch_general_commit(s->vb, ga, nwg, s->dview(), s->ovf, s->owner, cond, epoch,
+                                   s->stream));
+    t.done();
+    s->n_general++;
+  }
+  return PSKV_OK;
+}
+
+// Sorted path over one launch group of device-resident batches (verifying);
+// `repair` adds the conditional general launches behind it.
+int sorted_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t e, bool vec,
+               uint32_t epoch, bool repair) {
+  uint64_t elems = 0;
+  for (size_t i = b; i < e; ++i) elems += v[i].n;
+  if (e - b == 1) {
+    LaunchTimer t(s, PSKV_K_ASSIGN_SORTED, elems);
+    PSKV_HIP(launch_assign_sorted(s->vb, vec, v[b].keys, v[b].vals, v[b].n, s->dview(), s->flag,
+                                  epoch, s->stream));
+    t.done();
+  } else {
+    GroupArgs ga;
+    build_group(v, b, e, 1, &ga);
+    // Tile: enough tiles for ~8 workgroups per CU of work, 4 Ki..64 Ki keys.
+    uint32_t shift = 16;
+    while (shift > 12 && (elems >> shift) < 2048) --shift;
+    const uint64_t ntiles = (s->range + (1ull << shift) - 1) >> shift;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(ntiles, 2048);
+    LaunchTimer t(s, PSKV_K_ASSIGN_TILES, elems);
+    PSKV_HIP(launch_assign_tiles(s->vb, vec, ga, s->dview(), shift, ntiles, grid, s->flag, epoch,
+                                 s->stream));
+    t.done();
+  }
+  s->n_sorted++;
+  if (repair) return general_add(s, v, b, e, epoch, s->flag);
+  return PSKV_OK;
+}
+
+// Stage host batches into one device buffer (keys then values per batch,
+// 16-byte aligned) through pinned memory, checking on the way whether every
+// batch is sorted and inside the dense range.  Returns device batch views.
+int stage_host_batches(pskv_shard* s, const std::vector<pskv_batch>& in,
+                       std::vector<pskv_batch>* out, bool* all_sorted_in_range,
+                       uint64_t* n_outside) {
+  size_t bytes = 0;
+  for (auto& b : in) bytes += round16(b.n * 4) + round16(b.n * (size_t)s->vb);
+  int rc = ensure_hstage(s, bytes);
+  if (rc) return rc;
+  rc = ensure_dstage(s, bytes);
+  if (rc) return rc;
+  char* h = static_cast<char*>(s->hstage);
+  char* d = static_cast<char*>(s->dstage);
+  size_t off = 0;
+  bool ok = true;
+  uint64_t outside = 0;
+  out->clear();
+  for (auto& b : in) {
+    uint32_t* hk = reinterpret_cast<uint32_t*>(h + off);
+    uint32_t prev = 0;
+    for (uint64_t i = 0; i < b.n; ++i) {
+      const uint32_t k = b.keys[i];
+      hk[i] = k;
+      const bool in_range = (uint64_t)(uint32_t)(k - s->key_begin) < s->range;
+      outside += !in_range;
+      ok &= in_range & (i == 0 || prev <= k);
+      prev = k;
+    }
+    pskv_batch db;
+    db.keys = reinterpret_cast<const uint32_t*>(d + off);
+    off += round16(b.n * 4);
+    std::memcpy(h + off, b.vals, b.n * (size_t)s->vb);
+    db.vals = d + off;
+    db.n = b.n;
+    off += round16(b.n * (size_t)s->vb);
+    out->push_back(db);
+  }
+  PSKV_HIP(hipMemcpyAsync(s->dstage, s->hstage, off, hipMemcpyHostToDevice, s->stream));
+  PSKV_HIP(hipEventRecord(s->hstage_free, s->stream));
+  s->hstage_pending = true;
+  *all_sorted_in_range = ok;
+  *n_outside = outside;
+  return PSKV_OK;
+}
+
+int add_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
+  std::vector<pskv_batch> v;
+  for (auto& b : in) {
+    if (b.n == 0) continue;
+    if (!b.keys || !b.vals) return fail(PSKV_EINVAL, "pskv_add: null keys/vals with n > 0");
+    v.push_back(b);
+  }
+  s->n_add++;
+  if (v.empty()) return PSKV_OK;
+  int rc = use_device(s);
+  if (rc) return rc;
+  const bool device = (flags & PSKV_DEVICE) != 0;
+  bool host_verified = false;
+  if (!device) {
+    std::vector<pskv_batch> staged;
+    uint64_t outside = 0;
+    rc = stage_host_batches(s, v, &staged, &host_verified, &outside);
+    if (rc) return rc;
+    if (outside) {
+      // exact bound on new overflow keys: grow before the kernels can fill the table
+      if (2 * (s->ocount_known + outside) > s->ocap) {
+        uint32_t cnt, err;
+        rc = read_overflow_stat(s, &cnt, &err);
+        if (rc) return rc;
+        rc = grow_overflow(s, cnt + outside);
+        if (rc) return rc;
+      }
+      s->ocount_known += outside;
+    }
+    v.swap(staged);
+  }
+  bool vec = true;
+  for (auto& b : v) vec &= aligned16(b.keys) & aligned16(b.vals);
+  for (auto& g : split_groups(v)) {
+    const uint32_t epoch = next_epoch(s);
+    if (s->mode == PSKV_ACCUMULATE) {
+      rc = general_add(s, v, g.first, g.second, epoch, nullptr);
+    } else if (!device && host_verified) {
+      // the CPU proved the batches sorted and in range while staging them
+      rc = sorted_add(s, v, g.first, g.second, vec, epoch, /*repair=*/false);
+    } else if (device && (flags & PSKV_SORTED_HINT)) {
+      rc = sorted_add(s, v, g.first, g.second, vec, epoch, /*repair=*/true);
+    } else {
+      rc = general_add(s, v, g.first, g.second, epoch, nullptr);
+    }
+    if (rc) return rc;
+  }
+  return PSKV_OK;
+}
+
+int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
+  std::vector<pskv_batch> v;
+  for (auto& b : in) {
+    if (b.n == 0) continue;
+    if (!b.keys || !b.vals) return fail(PSKV_EINVAL, "pskv_get: null keys/out with n > 0");
+    v.push_back(b);
+  }
+  s->n_get++;
+  if (v.empty()) return PSKV_OK;
+  int rc = use_device(s);
+  if (rc) return rc;
+  const bool device = (flags & PSKV_DEVICE) != 0;
+  std::vector<pskv_batch> dv = v;
+  size_t out_off = 0;
+  if (!device) {
+    // keys → pinned → device; outputs land after the keys in the device stage
+    size_t kbytes = 0, obytes = 0;
+    for (auto& b : v) {
+      kbytes += round16(b.n * 4);
+      obytes += round16(b.n * (size_t)s->vb);
+    }
+    rc = ensure_hstage(s, kbytes + obytes);
+    if (rc) return rc;
+    rc = ensure_dstage(s, kbytes + obytes);
+    if (rc) return rc;
+    char* h = static_cast<char*>(s->hstage);
+    char* d = static_cast<char*>(s->dstage);
+    size_t off = 0;
+    for (size_t i = 0; i < v.size(); ++i) {
+      std::memcpy(h + off, v[i].keys, v[i].n * 4);
+      dv[i].keys = reinterpret_cast<const uint32_t*>(d + off);
+      off += round16(v[i].n * 4);
+    }
+    PSKV_HIP(hipMemcpyAsync(d, h, off, hipMemcpyHostToDevice, s->stream));
+    out_off = off;
+    for (size_t i = 0; i < v.size(); ++i) {
+      dv[i].vals = d + off;
+      off += round16(v[i].n * (size_t)s->vb);
+    }
+  }
+  bool vec = true;
+  for (auto& b : dv) vec &= aligned16(b.keys) & aligned16(b.vals);
+  for (auto& g : split_groups(dv)) {
+    GroupArgs ga;
+    const uint32_t nwg = build_group(dv, g.first, g.second, kGatherChunk, &ga);
+    uint64_t elems = 0;
+    for (size_t i = g.first; i < g.second; ++i) elems += dv[i].n;
+    LaunchTimer t(s, PSKV_K_GATHER, elems);
+    PSKV_HIP(launch_gather(s->vb, vec, ga, nwg, s->dview(), s->ovf, s->stream));
+    t.done();
+  }
+  if (!device) {
+    char* h = static_cast<char*>(s->hstage);
+    char* d = static_cast<char*>(s->dstage);
+    size_t obytes = 0;
+    for (auto& b : v) obytes += round16(b.n * (size_t)s->vb);
+    PSKV_HIP(hipMemcpyAsync(h + out_off, d + out_off, obytes, hipMemcpyDeviceToHost, s->stream));
+    PSKV_HIP(hipStreamSynchronize(s->stream));
+    size_t off = out_off;
+    for (auto& b : v) {
+      std::memcpy(b.vals, h + off, b.n * (size_t)s->vb);
+      off += round16(b.n * (size_t)s->vb);
+    }
+  }
+  return PSKV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pskv_abi_version(void) { return PSKV_ABI_VERSION; }
+
+const char* pskv_last_error(void) { return g_last_error.c_str(); }
+
+int pskv_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int pskv_shard_create_ex(int device, uint32_t key_begin, uint64_t key_end, int dtype, int mode,
+                         uint64_t overflow_slots, pskv_shard** out) {
+  if (!out) return fail(PSKV_EINVAL, "pskv_shard_create: out is null");
+  *out = nullptr;
+  const int vb = value_bytes(dtype);
+  if (!vb) return fail(PSKV_EINVAL, "pskv_shard_create: bad dtype");
+  if (mode != PSKV_ASSIGN && mode != PSKV_ACCUMULATE)
+    return fail(PSKV_EINVAL, "pskv_shard_create: bad mode");
+  if (key_end <= (uint64_t)key_begin || key_end > (1ull << 32))
+    return fail(PSKV_EINVAL, "pskv_shard_create: need key_begin < key_end <= 2^32");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+    return fail(PSKV_EINVAL, "pskv_shard_create: no such HIP device");
+  pskv_shard* s = new pskv_shard();
+  s->device = device;
+  s->dtype = dtype;
+  s->mode = mode;
+  s->vb = vb;
+  s->key_begin = key_begin;
+  s->range = key_end - key_begin;
+  auto bail = [&](int rc) {
+    pskv_shard_destroy(s);
+    return rc;
+  };
+  int rc = use_device(s);
+  if (rc) return bail(rc);
+  if (hipStreamCreateWithFlags(&s->own_stream, hipStreamNonBlocking) != hipSuccess)
+    return bail(fail(PSKV_EHIP, "hipStreamCreate failed"));
+  s->stream = s->own_stream;
+  if (hipEventCreateWithFlags(&s->hstage_free, hipEventDisableTiming) != hipSuccess)
+    return bail(fail(PSKV_EHIP, "hipEventCreate failed"));
+  if (hipMalloc(&s->dense, s->range * (size_t)vb) != hipSuccess)
+    return bail(fail(PSKV_ENOMEM, "dense parameter allocation failed"));
+  if (hipMemsetAsync(s->dense, 0, s->range * (size_t)vb, s->stream) != hipSuccess)
+    return bail(fail(PSKV_EHIP, "hipMemsetAsync failed"));
+  if (hipMalloc(&s->flag, 16) != hipSuccess) return bail(fail(PSKV_ENOMEM, "flag allocation failed"));
+  if (hipMemsetAsync(s->flag, 0, 16, s->stream) != hipSuccess)
+    return bail(fail(PSKV_EHIP, "hipMemsetAsync failed"));
+  s->ocap = next_pow2(std::max<uint64_t>(overflow_slots ? overflow_slots : kDefaultOverflowSlots, 64));
+  rc = alloc_overflow(&s->ovf, s->ocap, vb, s->stream);
+  if (rc) return bail(rc);
+  if (hipStreamSynchronize(s->stream) != hipSuccess)
+    return bail(fail(PSKV_EHIP, "hipStreamSynchronize failed"));
+  *out = s;
+  return PSKV_OK;
+}
+
+int pskv_shard_create(int device, uint32_t key_begin, uint64_t key_end, int dtype, int mode,
+                      pskv_shard** out) {
+  return pskv_shard_create_ex(device, key_begin, key_end, dtype, mode, 0, out);
+}
+
+int pskv_shard_destroy(pskv_shard* s) {
+  if (!s) return PSKV_OK;
+  (void)hipSetDevice(s->device);
+  if (s->own_stream) (void)hipStreamSynchronize(s->own_stream);
+  if (s->stream && s->stream != s->own_stream) (void)hipStreamSynchronize(s->stream);
+  for (auto& t : s->pending) {
+    (void)hipEventDestroy(t.a);
+    (void)hipEventDestroy(t.b);
+  }
+  for (auto e : s->event_pool) (void)hipEventDestroy(e);
+  if (s->dense) (void)hipFree(s->dense);
+  if (s->owner) (void)hipFree(s->owner);
+  if (s->flag) (void)hipFree(s->flag);
+  free_overflow(&s->ovf);
+  if (s->dstage) (void)hipFree(s->dstage);
+  if (s->hstage) (void)hipHostFree(s->hstage);
+  if (s->hstage_free) (void)hipEventDestroy(s->hstage_free);
+  if (s->own_stream) (void)hipStreamDestroy(s->own_stream);
+  delete s;
+  return PSKV_OK;
+}
+
+int pskv_add(pskv_shard* s, const uint32_t* keys, const void* vals, uint64_t n, int flags) {
+  if (!s) return fail(PSKV_EINVAL, "pskv_add: null shard");
+  pskv_batch b{keys, const_cast<void*>(vals), n};
+  return add_impl(s, std::vector<pskv_batch>{b}, flags);
+}
+
+int pskv_get(pskv_shard* s, const uint32_t* keys, uint64_t n, void* out, int flags) {
+  if (!s) return fail(PSKV_EINVAL, "pskv_get: null shard");
+  pskv_batch b{keys, out, n};
+  return get_impl(s, std::vector<pskv_batch>{b}, flags);
+}
+
+int pskv_add_grouped(pskv_shard* s, const pskv_batch* batches, uint64_t nb, int flags) {
+  if (!s) return fail(PSKV_EINVAL, "pskv_add_grouped: null shard");
+  if (nb && !batches) return fail(PSKV_EINVAL, "pskv_add_grouped: null batches");
+  return add_impl(s, std::vector<pskv_batch>(batches, batches + nb), flags);
+}
+
+int pskv_get_grouped(pskv_shard* s, const pskv_batch* batches, uint64_t nb, int flags) {
+  if (!s) return fail(PSKV_EINVAL, "pskv_get_grouped: null shard");
+  if (nb && !batches) return fail(PSKV_EINVAL, "pskv_get_grouped: null batches");
+  return get_impl(s, std::vector<pskv_batch>(batches, batches + nb), flags);
+}
+
+int pskv_sync(pskv_shard* s) {
+  if (!s) return fail(PSKV_EINVAL, "pskv_sync: null shard");
+  int rc = use_device(s);
+  if (rc) return rc;
+  uint32_t cnt = 0, err = 0;
+  rc = read_overflow_stat(s, &cnt, &err);
+  if (rc) return rc;
+  rc = drain_timing(s);
+  if (rc) return rc;
+  if (err & kErrOverflowFull)
+    return fail(PSKV_ESTATE,
+                "overflow table exhausted: out-of-range keys were dropped; create the shard "
+                "with more overflow slots (pskv_shard_create_ex)");
+  if (2 * (uint64_t)cnt > s->ocap) return grow_overflow(s, cnt);
+  return PSKV_OK;
+}
+
+int pskv_clear(pskv_shard* s) {
+  if (!s) return fail(PSKV_EINVAL, "pskv_clear: null shard");
+  int rc = use_device(s);
+  if (rc) return rc;
+  PSKV_HIP(hipMemsetAsync(s->dense, 0, s->range * (size_t)s->vb, s->stream));
+  PSKV_HIP(hipMemsetAsync(s->ovf.keys, 0xFF, s->ocap * sizeof(unsigned long long), s->stream));
+  PSKV_HIP(hipMemsetAsync(s->ovf.vals, 0, s->ocap * (size_t)s->vb, s->stream));
+  PSKV_HIP(hipMemsetAsync(s->ovf.stat, 0, 2 * sizeof(uint32_t), s->stream));
+  s->ocount_known = 0;
+  PSKV_HIP(hipStreamSynchronize(s->stream));
+  return PSKV_OK;
+}
+
+int pskv_set_stream(pskv_shard* s, void* hip_stream) {
+  if (!s) return fail(PSKV_EINVAL, "pskv_set_stream: null shard");
+  int rc = use_device(s);
+  if (rc) return rc;
+  // order the switch: everything queued so far completes before the new stream's work
+  PSKV_HIP(hipStreamSynchronize(s->stream));
+  s->stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : s->own_stream;
+  return PSKV_OK;
+}
+
+void* pskv_get_stream(pskv_shard* s) { return s ? static_cast<void*>(s->stream) : nullptr; }
+
+void* pskv_dense_ptr(pskv_shard* s) { return s ? s->dense : nullptr; }
+
+int pskv_shard_info(pskv_shard* s, pskv_info* info) {
+  if (!s || !info) return fail(PSKV_EINVAL, "pskv_shard_info: null argument");
+  info->device = s->device;
+  info->dtype = s->dtype;
+  info->mode = s->mode;
+  info->value_bytes = s->vb;
+  info->key_begin = s->key_begin;
+  info->key_end = (uint64_t)s->key_begin + s->range;
+  info->dense_bytes = s->range * (uint64_t)s->vb;
+  info->overflow_capacity = s->ocap;
+  info->overflow_count = s->ocount_known;
+  info->n_add_calls = s->n_add;
+  info->n_get_calls = s->n_get;
+  info->n_sorted_launches = s->n_sorted;
+  info->n_general_launches = s->n_general;
+  return PSKV_OK;
+}
+
+int pskv_set_timing(pskv_shard* s, int enable) {
+  if (!s) return fail(PSKV_EINVAL, "pskv_set_timing: null shard");
+  s->timing = enable != 0;
+  return PSKV_OK;
+}
+
+int pskv_kernel_time(pskv_shard* s, int kernel, uint64_t* launches, double* total_ms,
+                     uint64_t* elements) {
+  if (!s || kernel < 0 || kernel >= PSKV_K_COUNT)
+    return fail(PSKV_EINVAL, "pskv_kernel_time: bad argument");
+  int rc = use_device(s);
+  if (rc) return rc;
+  rc = drain_timing(s);
+  if (rc) return rc;
+  if (launches) *launches = s->t_launches[kernel];
+  if (total_ms) *total_ms = s->t_ms[kernel];
+  if (elements) *elements = s->t_elems[kernel];
+  return PSKV_OK;
+}
+
+int pskv_reset_timing(pskv_shard* s) {
+  if (!s) return fail(PSKV_EINVAL, "pskv_reset_timing: null shard");
+  int rc = use_device(s);
+  if (rc) return rc;
+  rc = drain_timing(s);
+  if (rc) return rc;
+  for (int k = 0; k < PSKV_K_COUNT; ++k) {
+    s->t_launches[k] = 0;
+    s->t_ms[k] = 0;
+    s->t_elems[k] = 0;
+  }
+  return PSKV_OK;
+}
+
+int pskv_range_slice(const uint64_t* range_begin, const uint64_t* range_end, int nranges,
+                     const uint32_t* keys, uint64_t n, int32_t* slice_range,
+                     uint64_t* slice_start, uint64_t* slice_len) {
+  // Restates RangePartitionManager::Slice (base/range_partition_manager.hpp:19-46):
+  // the range pointer only moves forward; a key stays with the current range if
+  // it lies in it or the current range is the last one.
+  if (n == 0) return 0;
+  if (nranges <= 0 || !range_begin || !range_end || !keys || !slice_range || !slice_start ||
+      !slice_len)
+    return fail(PSKV_EINVAL, "pskv_range_slice: bad argument");
+  int r = 0, cur = -1, ns = 0;
+  for (uint64_t i = 0; i < n;) {
+    const uint64_t k = keys[i];
+    if ((k >= range_begin[r] && k < range_end[r]) || r + 1 >= nranges) {
+      if (cur < r) {
+        cur = r;
+        slice_range[ns] = r;
+        slice_start[ns] = i;
+        slice_len[ns] = 0;
+        ++ns;
+      }
+      slice_len[ns - 1]++;
+      ++i;
+    } else {
+      ++r;
+    }
+  }
+  return ns;
+}
+
+}  // extern "C"

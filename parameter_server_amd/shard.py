@@ -1,0 +1,239 @@
+"""Shard: Python handle on one HBM-resident parameter shard (pskv_shard).
+
+Host inputs are numpy arrays (they stand for the zmq receive buffers the
+reference storage sees, comm/mailbox.cpp:246-257); device inputs are torch
+tensors on the shard's GPU (PyTorch only supplies memory and streams — every
+byte of the Add/Get work is done by the HIP kernels in libpskv.so).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+
+_NP_DTYPE = {_lib.PSKV_I32: np.dtype(np.int32), _lib.PSKV_F32: np.dtype(np.float32),
+             _lib.PSKV_F64: np.dtype(np.float64)}
+_DTYPE_CODE = {v: k for k, v in _NP_DTYPE.items()}
+
+
+def dtype_code(dtype) -> int:
+    try:
+        import torch
+
+        if isinstance(dtype, torch.dtype):
+            dtype = {torch.int32: np.int32, torch.float32: np.float32, torch.float64: np.float64}[dtype]
+    except ImportError:
+        pass
+    return _DTYPE_CODE[np.dtype(dtype)]
+
+
+def _is_torch(x) -> bool:
+    return type(x).__module__.startswith("torch")
+
+
+def device_count() -> int:
+    return int(lib.pskv_device_count())
+
+
+class Shard:
+    """A key range [key_begin, key_end) of uint32 keys held in HBM.
+
+    mode "assign" is the reference semantics (last write wins, missing -> 0);
+    "accumulate" is the gradient-reduction mode (param[k] += v)."""
+
+    def __init__(self, key_begin: int = 0, key_end: int = 1 << 32, dtype=np.float32,
+                 mode: str = "assign", device: int = 0, overflow_slots: int = 0):
+        self.dtype = np.dtype(dtype) if not _is_torch(dtype) else _NP_DTYPE[dtype_code(dtype)]
+        self.code = dtype_code(self.dtype)
+        self.mode = {"assign": _lib.PSKV_ASSIGN, "accumulate": _lib.PSKV_ACCUMULATE}[mode]
+        self.key_begin, self.key_end, self.device = int(key_begin), int(key_end), int(device)
+        h = ctypes.c_void_p()
+        check(lib.pskv_shard_create_ex(self.device, self.key_begin, self.key_end, self.code,
+                                       self.mode, int(overflow_slots), ctypes.byref(h)))
+        self._h = h
+
+    # ------------------------------------------------------------ lifetime
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib.pskv_shard_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    # ------------------------------------------------------------ helpers
+    def _host_keys(self, keys):
+        return np.ascontiguousarray(keys, dtype=np.uint32)
+
+    def _host_vals(self, vals, n):
+        v = np.ascontiguousarray(vals, dtype=self.dtype)
+        if v.size != n:
+            raise ValueError(f"CHECK_EQ(keys.size(), vals.size()) failed: {n} vs {v.size}")
+        return v
+
+    # ------------------------------------------------------------ Add / Get
+    def add(self, keys, vals, sorted_hint: bool = False):
+        """Push one batch.  numpy -> host path; torch CUDA tensors -> device path."""
+        if _is_torch(keys):
+            self._check_dev(keys, vals)
+            flags = _lib.PSKV_DEVICE | (_lib.PSKV_SORTED_HINT if sorted_hint else 0)
+            if vals.numel() != keys.numel():
+                raise ValueError("CHECK_EQ(keys.size(), vals.size()) failed")
+            check(lib.pskv_add(self._h, keys.data_ptr(), vals.data_ptr(), keys.numel(), flags))
+            return
+        k = self._host_keys(keys)
+        v = self._host_vals(vals, k.size)
+        check(lib.pskv_add(self._h, k.ctypes.data, v.ctypes.data, k.size, _lib.PSKV_HOST))
+
+    def get(self, keys, out=None):
+        """Pull one batch.  numpy keys -> returns a numpy array (synchronous);
+        torch keys -> fills/returns a torch tensor (stream-ordered)."""
+        if _is_torch(keys):
+            import torch
+
+            if out is None:
+                out = torch.empty(keys.numel(), dtype=_torch_dtype(self.dtype), device=keys.device)
+            self._check_dev(keys, out)
+            check(lib.pskv_get(self._h, keys.data_ptr(), keys.numel(), out.data_ptr(),
+                               _lib.PSKV_DEVICE))
+            return out
+        k = self._host_keys(keys)
+        res = np.empty(k.size, dtype=self.dtype) if out is None else out
+        check(lib.pskv_get(self._h, k.ctypes.data, k.size, res.ctypes.data, _lib.PSKV_HOST))
+        return res
+
+    def add_grouped(self, batches, sorted_hint: bool = False):
+        """batches: list of (keys, vals); all torch-device or all numpy-host."""
+        arr, keep, flags = self._batch_array(batches, is_get=False)
+        if sorted_hint and flags & _lib.PSKV_DEVICE:
+            flags |= _lib.PSKV_SORTED_HINT
+        check(lib.pskv_add_grouped(self._h, arr, len(batches), flags))
+        del keep
+
+    def get_grouped(self, batches):
+        """batches: list of (keys, out) pairs; out is filled in place."""
+        arr, keep, flags = self._batch_array(batches, is_get=True)
+        check(lib.pskv_get_grouped(self._h, arr, len(batches), flags))
+        del keep
+
+    def _batch_array(self, batches, is_get):
+        arr = (_lib.PskvBatch * max(1, len(batches)))()
+        keep = []
+        dev = None
+        for i, (k, v) in enumerate(batches):
+            t = _is_torch(k)
+            if dev is None:
+                dev = t
+            if t != dev:
+                raise ValueError("mixed host/device batches in one grouped call")
+            if t:
+                self._check_dev(k, v)
+                if v.numel() != k.numel():
+                    raise ValueError("CHECK_EQ(keys.size(), vals.size()) failed")
+                arr[i] = _lib.PskvBatch(k.data_ptr(), v.data_ptr(), k.numel())
+            else:
+                kk = self._host_keys(k)
+                if is_get:
+                    if not (isinstance(v, np.ndarray) and v.dtype == self.dtype and v.flags.c_contiguous):
+                        raise ValueError("get_grouped host outputs must be C-contiguous arrays of the shard dtype")
+                    vv = v
+                else:
+                    vv = self._host_vals(v, kk.size)
+                keep += [kk, vv]
+                arr[i] = _lib.PskvBatch(kk.ctypes.data, vv.ctypes.data, kk.size)
+        return arr, keep, (_lib.PSKV_DEVICE if dev else _lib.PSKV_HOST)
+
+    def _check_dev(self, *ts):
+        for t in ts:
+            if not t.is_cuda or t.device.index != self.device or not t.is_contiguous():
+                raise ValueError("device tensors must be contiguous and on the shard's GPU")
+
+    # ------------------------------------------------------------ control
+    def sync(self):
+        check(lib.pskv_sync(self._h))
+
+    def clear(self):
+        check(lib.pskv_clear(self._h))
+
+    def set_stream(self, stream_handle):
+        """stream_handle: int hipStream_t (e.g. torch.cuda.current_stream().cuda_stream) or None."""
+        check(lib.pskv_set_stream(self._h, stream_handle))
+
+    def dense_ptr(self) -> int:
+        return int(lib.pskv_dense_ptr(self._h) or 0)
+
+    def info(self) -> dict:
+        i = _lib.PskvInfo()
+        check(lib.pskv_shard_info(self._h, ctypes.byref(i)))
+        return {f: getattr(i, f) for f, _ in _lib.PskvInfo._fields_}
+
+    def set_timing(self, on: bool):
+        check(lib.pskv_set_timing(self._h, 1 if on else 0))
+
+    def reset_timing(self):
+        check(lib.pskv_reset_timing(self._h))
+
+    def kernel_time(self, kernel: int):
+        n, ms, el = ctypes.c_uint64(), ctypes.c_double(), ctypes.c_uint64()
+        check(lib.pskv_kernel_time(self._h, kernel, ctypes.byref(n), ctypes.byref(ms), ctypes.byref(el)))
+        return {"launches": n.value, "total_ms": ms.value, "elements": el.value}
+
+    def dense_view(self):
+        """A torch tensor aliasing the dense HBM array (tests only; no copy)."""
+        import torch
+
+        n = self.key_end - self.key_begin
+        ptr = self.dense_ptr()
+        return _tensor_from_ptr(ptr, n, _torch_dtype(self.dtype), self.device)
+
+
+def _torch_dtype(npdt):
+    import torch
+
+    return {np.dtype(np.int32): torch.int32, np.dtype(np.float32): torch.float32,
+            np.dtype(np.float64): torch.float64}[np.dtype(npdt)]
+
+
+def _tensor_from_ptr(ptr, n, tdtype, device):
+    """Wrap raw device memory as a torch tensor via __cuda_array_interface__."""
+    import torch
+
+    typestr = {torch.int32: "<i4", torch.float32: "<f4", torch.float64: "<f8"}[tdtype]
+
+    class _Holder:
+        __cuda_array_interface__ = {"shape": (n,), "typestr": typestr, "data": (ptr, False),
+                                    "version": 2, "strides": None}
+
+    with torch.cuda.device(device):
+        return torch.as_tensor(_Holder(), device=f"cuda:{device}")
+
+
+def range_slice(ranges, keys):
+    """Mirror of RangePartitionManager::Slice through the product library
+    (pskv_range_slice).  Returns [(range_index, start, length), ...]."""
+    k = np.ascontiguousarray(keys, dtype=np.uint32)
+    nr = len(ranges)
+    rb = np.ascontiguousarray([b for b, _ in ranges], dtype=np.uint64)
+    re = np.ascontiguousarray([e for _, e in ranges], dtype=np.uint64)
+    sr = np.empty(max(nr, 1), dtype=np.int32)
+    ss = np.empty(max(nr, 1), dtype=np.uint64)
+    sl = np.empty(max(nr, 1), dtype=np.uint64)
+    ns = check(lib.pskv_range_slice(rb.ctypes.data, re.ctypes.data, nr, k.ctypes.data, k.size,
+                                    sr.ctypes.data, ss.ctypes.data, sl.ctypes.data))
+    return [(int(sr[i]), int(ss[i]), int(sl[i])) for i in range(ns)]

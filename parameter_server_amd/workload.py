@@ -1,0 +1,113 @@
+"""Synthetic push/pull workloads of BASELINE.json's configs.
+
+  cfg 2  dense:  shard [0, 1e8) float; batches of 1M contiguous keys at base
+                 b_j = seed-42 uniform multiple of 1M; vals U(-1, 1), seed 42+j
+  cfg 3  zipf:   key space 1e8; 1M keys per batch, Zipf(s=0.99) over ranks
+                 1..1e8, rank -> key by a seed-7 random permutation, unsorted
+  cfg 4  ranges: G range shards; every rank owns [r*K/G, (r+1)*K/G) and its
+                 producers push contiguous 1M windows inside it (weak scaling:
+                 per-GPU work fixed), routed through the range shard map
+
+Generation uses torch on the target device (outside any timed region).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+MILLION = 1_000_000
+
+
+def dense_bases(n_batches: int, key_space: int, batch: int = MILLION, seed: int = 42,
+                lo: int = 0) -> np.ndarray:
+    """Uniform multiples of `batch` in [lo, lo+key_space) (cfg 2 / cfg 4 windows)."""
+    rng = np.random.default_rng(seed)
+    slots = key_space // batch
+    return lo + rng.integers(0, slots, size=n_batches, dtype=np.int64) * batch
+
+
+def dense_batches(n_batches, key_space, batch=MILLION, device="cuda:0", dtype=None, seed=42,
+                  lo=0):
+    """[(keys u32 tensor, vals tensor)] for cfg 2 (keys sorted, contiguous)."""
+    import torch
+
+    dtype = dtype or torch.float32
+    out = []
+    for j, b in enumerate(dense_bases(n_batches, key_space, batch, seed, lo)):
+        keys = torch.arange(int(b), int(b) + batch, dtype=torch.int64, device=device).to(torch.int32)
+        g = torch.Generator(device=device)
+        g.manual_seed(seed + j)
+        if dtype in (torch.float32, torch.float64):
+            vals = torch.rand(batch, generator=g, device=device, dtype=dtype) * 2 - 1
+        else:
+            vals = torch.randint(-2**31, 2**31 - 1, (batch,), generator=g, device=device, dtype=dtype)
+        out.append((keys, vals))
+    return out
+
+
+def zipf_batches(n_batches, key_space, batch=MILLION, s=0.99, device="cuda:0", dtype=None,
+                 perm_seed=7, seed=42):
+    """cfg 3: exact discrete Zipf(s) ranks via an inverse CDF, mapped to keys
+    by a seeded permutation; order unsorted."""
+    import torch
+
+    dtype = dtype or torch.float32
+    w = torch.arange(1, key_space + 1, dtype=torch.float64, device=device).pow_(-s)
+    cdf = torch.cumsum(w, 0)
+    cdf /= cdf[-1].clone()
+    del w
+    gp = torch.Generator(device=device)
+    gp.manual_seed(perm_seed)
+    perm = torch.randperm(key_space, generator=gp, device=device)
+    out = []
+    for j in range(n_batches):
+        g = torch.Generator(device=device)
+        g.manual_seed(seed + j)
+        u = torch.rand(batch, generator=g, device=device, dtype=torch.float64)
+        ranks = torch.searchsorted(cdf, u).clamp_(max=key_space - 1)
+        keys = perm[ranks].to(torch.int32)
+        if dtype in (torch.float32, torch.float64):
+            vals = torch.rand(batch, generator=g, device=device, dtype=dtype) * 2 - 1
+        else:
+            vals = torch.randint(-2**31, 2**31 - 1, (batch,), generator=g, device=device, dtype=dtype)
+        out.append((keys, vals))
+    del cdf, perm
+    return out
+
+
+def rank_ranges(key_space: int, world: int):
+    """Equal contiguous key ranges, one per GPU (range_partition_manager.hpp's map)."""
+    step = key_space // world
+    return [(r * step, (r + 1) * step if r + 1 < world else key_space) for r in range(world)]
+
+
+def rank_windows(rank: int, world: int, key_space: int, n_windows: int, batch: int = MILLION):
+    """cfg 4 producer windows for one rank: stream s of rank r draws its base with
+    seed 1000 + (r * n_windows + s), a uniform multiple of `batch` inside the rank's
+    range.  Returns base offsets (int64)."""
+    lo, hi = rank_ranges(key_space, world)[rank]
+    slots = (hi - lo) // batch
+    bases = []
+    for s in range(n_windows):
+        rng = np.random.default_rng(1000 + rank * n_windows + s)
+        bases.append(lo + int(rng.integers(0, slots)) * batch)
+    return np.asarray(bases, dtype=np.int64)
+
+
+def route_windows(bases, batch, ranges):
+    """Slice every window [b, b+batch) with the range shard map (mirror of
+    RangePartitionManager::Slice over a sorted window).  Returns, per range,
+    a list of (window index, start offset, length).  A window that straddles a
+    boundary splits into two slices."""
+    per = [[] for _ in ranges]
+    for w, b in enumerate(bases):
+        b = int(b)
+        e = b + batch
+        r = 0
+        pos = b
+        while pos < e:
+            while r + 1 < len(ranges) and not (ranges[r][0] <= pos < ranges[r][1]):
+                r += 1
+            end = e if r + 1 == len(ranges) else min(e, ranges[r][1])
+            per[r].append((w, pos - b, end - pos))
+            pos = end
+    return per

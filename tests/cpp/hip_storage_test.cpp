@@ -1,0 +1,151 @@
+// hip_storage_test.cpp — the reference's storage known-answer tests, restated
+// against HipStorage<Val> through the AbstractStorage interface, the way a
+// consistency model holds it (std::unique_ptr<AbstractStorage>,
+// server/consistency/ssp_model.hpp:42).
+//
+//   AddGetInt / AddGetFloat / SubAddSubGet   server/vector_storage_test.cpp:19-78,
+//                                            server/map_storage_test.cpp:19-75
+//   LastWriteWins                            SURVEY.md §0.1 probe of both reference storages:
+//                                            Add{5:1,5:2,7:3}; Add{7:10}; Get{5,7,9} -> {2,10,0}
+//   SliceKeys / SliceKVs                     base/range_partition_manager_test.cpp:17-56
+//   SliceFallthrough                         SURVEY.md §0.4 probes
+//
+// Needs a GPU for the storage cases (run by tests/test_gpu_parity.py);
+// `--host-only` runs the range-map cases alone.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "ps/hip_storage.hpp"
+#include "ps/range_partition_manager.hpp"
+
+using namespace csci5570;
+
+static int g_fail = 0, g_pass = 0;
+#define EXPECT(cond)                                                            \
+  do {                                                                          \
+    if (cond) {                                                                 \
+      ++g_pass;                                                                 \
+    } else {                                                                    \
+      ++g_fail;                                                                 \
+      std::printf("  FAIL %s:%d: %s\n", __FILE__, __LINE__, #cond);             \
+    }                                                                           \
+  } while (0)
+
+template <typename V>
+static void AddGet(const std::vector<V>& vals, const char* name) {
+  std::printf("[ RUN ] %s\n", name);
+  std::unique_ptr<AbstractStorage> s(new HipStorage<V>());
+  Message m;
+  third_party::SArray<Key> s_keys({13, 14, 15});
+  third_party::SArray<V> s_vals(vals);
+  m.AddData(s_keys);
+  m.AddData(s_vals);
+  s->Add(m);
+  Message m2;
+  m2.meta.sender = 7;
+  m2.meta.recver = 1000;
+  m2.meta.flag = Flag::kGet;
+  m2.meta.model_id = 3;
+  m2.AddData(s_keys);
+  Message rep = s->Get(m2);
+  EXPECT(rep.data.size() == 2);
+  EXPECT(rep.meta.sender == 1000 && rep.meta.recver == 7);
+  EXPECT(rep.meta.flag == Flag::kGet && rep.meta.model_id == 3);
+  auto rep_keys = third_party::SArray<Key>(rep.data[0]);
+  auto rep_vals = third_party::SArray<V>(rep.data[1]);
+  EXPECT(rep_keys.size() == 3 && rep_vals.size() == 3);
+  EXPECT(rep_keys.data() == s_keys.data());  // reply keys alias the request (abstract_storage.hpp:27)
+  for (size_t i = 0; i < s_keys.size(); ++i) {
+    EXPECT(rep_keys[i] == s_keys[i]);
+    EXPECT(std::memcmp(&rep_vals[i], &s_vals[i], sizeof(V)) == 0);
+  }
+}
+
+static void SubAddSubGet() {
+  std::printf("[ RUN ] SubAddSubGet\n");
+  HipStorage<float> s;
+  third_party::SArray<Key> s_keys({13, 14, 15});
+  third_party::SArray<float> s_vals({0.1f, 0.2f, 0.3f});
+  s.SubAdd(s_keys, third_party::SArray<char>(s_vals));
+  auto ret = third_party::SArray<float>(s.SubGet(s_keys));
+  for (size_t i = 0; i < s_keys.size(); ++i) EXPECT(ret[i] == s_vals[i]);
+  s.FinishIter();
+}
+
+template <typename V>
+static void LastWriteWins(uint32_t key_begin, uint64_t key_end, const char* name) {
+  std::printf("[ RUN ] %s [%u, %llu)\n", name, key_begin, (unsigned long long)key_end);
+  std::unique_ptr<AbstractStorage> s(new HipStorage<V>(0, key_begin, key_end));
+  {
+    Message m;
+    m.AddData(third_party::SArray<Key>({5, 5, 7}));
+    m.AddData(third_party::SArray<V>({V(1), V(2), V(3)}));
+    s->Add(m);
+  }
+  {
+    Message m;
+    m.AddData(third_party::SArray<Key>({7}));
+    m.AddData(third_party::SArray<V>({V(10)}));
+    s->Add(m);
+  }
+  Message g;
+  g.AddData(third_party::SArray<Key>({5, 7, 9}));
+  Message rep = s->Get(g);
+  auto v = third_party::SArray<V>(rep.data[1]);
+  EXPECT(v.size() == 3);
+  EXPECT(v[0] == V(2) && v[1] == V(10) && v[2] == V(0));
+  s->FinishIter();
+}
+
+static void SliceCases() {
+  std::printf("[ RUN ] SliceKeys / SliceKVs / SliceFallthrough\n");
+  {
+    RangeShardMap pm({0, 1, 2}, {{2, 4}, {4, 7}, {7, 10}});
+    std::vector<std::pair<int, RangeShardMap::Keys>> sl;
+    pm.Slice(third_party::SArray<uint32_t>({2, 8, 9}), &sl);
+    EXPECT(sl.size() == 2);
+    EXPECT(sl[0].first == 0 && sl[1].first == 2);
+    EXPECT(sl[0].second.size() == 1 && sl[0].second[0] == 2);
+    EXPECT(sl[1].second.size() == 2 && sl[1].second[0] == 8 && sl[1].second[1] == 9);
+  }
+  {
+    RangeShardMap pm({0, 1, 2}, {{0, 4}, {4, 8}, {8, 10}});
+    std::vector<std::pair<int, RangeShardMap::Keys>> sl;
+    pm.Slice(third_party::SArray<uint32_t>({2, 5, 9}), &sl);
+    EXPECT(sl.size() == 3);
+    for (int i = 0; i < 3; ++i) EXPECT(sl[i].first == i && sl[i].second.size() == 1);
+  }
+  {  // unsorted input misroutes: {5,1,9} over [0,4),[4,8),[8,12) -> srv1:5, srv2:1 9
+    RangeShardMap pm({0, 1, 2}, {{0, 4}, {4, 8}, {8, 12}});
+    std::vector<std::pair<int, RangeShardMap::Keys>> sl;
+    pm.Slice(third_party::SArray<uint32_t>({5, 1, 9}), &sl);
+    EXPECT(sl.size() == 2);
+    EXPECT(sl[0].first == 1 && sl[0].second.size() == 1 && sl[0].second[0] == 5);
+    EXPECT(sl[1].first == 2 && sl[1].second.size() == 2 && sl[1].second[0] == 1);
+  }
+  {  // below the first range falls to the last: [2,4),[4,8) keys {0,5} -> srv1: 0 5
+    RangeShardMap pm({0, 1}, {{2, 4}, {4, 8}});
+    std::vector<std::pair<int, RangeShardMap::Keys>> sl;
+    pm.Slice(third_party::SArray<uint32_t>({0, 5}), &sl);
+    EXPECT(sl.size() == 1 && sl[0].first == 1 && sl[0].second.size() == 2);
+  }
+}
+
+int main(int argc, char** argv) {
+  const bool host_only = argc > 1 && std::strcmp(argv[1], "--host-only") == 0;
+  SliceCases();
+  if (!host_only) {
+    AddGet<int>({1, 2, 3}, "AddGetInt");
+    AddGet<float>({0.1f, 0.2f, 0.3f}, "AddGetFloat");
+    AddGet<double>({0.1, 0.2, 0.3}, "AddGetDouble");
+    SubAddSubGet();
+    LastWriteWins<int>(0, 1ull << 20, "LastWriteWinsInt");
+    LastWriteWins<float>(0, 1ull << 20, "LastWriteWinsFloat");
+    LastWriteWins<double>(6, 8, "LastWriteWinsDoubleOverflow");  // 5 and 9 live in the overflow table
+  }
+  std::printf("%d passed, %d failed\n", g_pass, g_fail);
+  return g_fail ? 1 : 0;
+}

@@ -1,0 +1,169 @@
+"""CPU tests of the boundary: libpskv.so loads and exports every symbol
+include/pskv.h declares; host-only entry points (range slicing) match the
+oracle; the Python mirror of the reference interface behaves like the
+reference's template methods.  No kernel is launched here (no GPU)."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    with open(os.path.join(ROOT, "include", "pskv.h")) as f:
+        txt = f.read()
+    return sorted(set(re.findall(r"^\s*(?:[\w\*]+\s+)+\**(pskv_\w+)\(", txt, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    from parameter_server_amd import _lib
+
+    syms = header_symbols()
+    assert len(syms) >= 20
+    assert sorted(_lib.EXPORTED) == syms
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (pskv_\w+)", out))
+    missing = [s for s in syms if s not in exported]
+    assert not missing, missing
+
+
+def test_library_is_gfx950_hip_code():
+    from parameter_server_amd import _lib
+
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-S", _lib.LIB_PATH],
+                         capture_output=True, text=True).stdout
+    assert ".hip_fatbin" in out
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_abi_version_and_no_device_here():
+    from parameter_server_amd import _lib
+
+    assert _lib.lib.pskv_abi_version() == 1
+    assert _lib.lib.pskv_device_count() >= 0
+
+
+def test_bad_arguments_fail_cleanly():
+    import ctypes
+
+    from parameter_server_amd import _lib
+
+    h = ctypes.c_void_p()
+    assert _lib.lib.pskv_shard_create(0, 10, 5, _lib.PSKV_F32, 0, ctypes.byref(h)) == _lib.PSKV_EINVAL
+    assert b"key_begin" in _lib.lib.pskv_last_error()
+    assert _lib.lib.pskv_shard_create(0, 0, 100, 7, 0, ctypes.byref(h)) == _lib.PSKV_EINVAL
+    assert _lib.lib.pskv_add(None, None, None, 0, 0) == _lib.PSKV_EINVAL
+    assert _lib.lib.pskv_sync(None) == _lib.PSKV_EINVAL
+
+
+def test_shard_without_gpu_raises_loudly():
+    import torch
+
+    from parameter_server_amd import PskvError, Shard
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    with pytest.raises(PskvError):
+        Shard(0, 1000)
+
+
+def test_range_slice_matches_reference_cases(oracle_mod):
+    import json
+
+    from parameter_server_amd import range_slice
+
+    with open(os.path.join(ROOT, "tests", "golden", "reference_known_answers.json")) as f:
+        cases = json.load(f)["slice_cases"]
+    for c in cases:
+        ranges = [tuple(r) for r in c["ranges"]]
+        got = [[r, [c["keys"][i] for i in range(s, s + n)]] for r, s, n in range_slice(ranges, c["keys"])]
+        assert got == c["expect"], c["cite"]
+
+
+def test_range_slice_random_vs_oracle(oracle_mod):
+    from parameter_server_amd import range_slice
+
+    rng = np.random.default_rng(1)
+    for _ in range(200):
+        nr = int(rng.integers(1, 9))
+        cuts = np.sort(rng.choice(np.arange(1, 2**20), size=nr, replace=False))
+        lo = int(rng.integers(0, cuts[0]))
+        ranges = [(int(a), int(b)) for a, b in zip(np.r_[lo, cuts[:-1]], cuts)]
+        keys = rng.integers(0, 2**20 + 100, size=int(rng.integers(0, 300))).astype(np.uint32)
+        if rng.random() < 0.6:
+            keys.sort()
+        want = oracle_mod.range_slice_ref(ranges, keys)
+        got = [(r, [int(k) for k in keys[s:s + n]]) for r, s, n in range_slice(ranges, keys)]
+        assert got == want
+
+
+def test_cpp_boundary_host_cases():
+    """tests/cpp/hip_storage_test.cpp range-map cases (host only)."""
+    exe = os.path.join(ROOT, "parameter_server_amd", "bin", "hip_storage_test")
+    if not os.path.exists(exe):
+        from parameter_server_amd import build
+
+        build.build_cpp_tests()
+    r = subprocess.run([exe, "--host-only"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 failed" in r.stdout
+
+
+class FakeStorage:
+    pass
+
+
+def test_python_mirror_template_methods():
+    """AbstractStorage.Add/Get restate server/abstract_storage.hpp:14-32."""
+    from parameter_server_amd import AbstractStorage, CheckError, Flag, Message
+
+    class Fake(AbstractStorage):
+        def __init__(self):
+            self.added = []
+
+        def SubAdd(self, keys, vals):
+            self.added.append((keys.copy(), vals.copy()))
+
+        def SubGet(self, keys):
+            return (keys.astype(np.int32) * 10).view(np.uint8)
+
+        def FinishIter(self):
+            pass
+
+    s = Fake()
+    m = Message()
+    m.AddData(np.array([13, 14, 15], np.uint32))
+    m.AddData(np.array([1, 2, 3], np.int32))
+    s.Add(m)
+    assert list(s.added[0][0]) == [13, 14, 15]
+    g = Message()
+    g.meta.sender, g.meta.recver, g.meta.flag, g.meta.model_id = 2, 0, Flag.kGet, 5
+    g.AddData(np.array([7, 8], np.uint32))
+    rep = s.Get(g)
+    assert (rep.meta.sender, rep.meta.recver, rep.meta.flag, rep.meta.model_id) == (0, 2, Flag.kGet, 5)
+    assert len(rep.data) == 2
+    assert list(rep.data[1].view(np.int32)) == [70, 80]
+    assert np.shares_memory(rep.data[0], g.data[0])  # reply keys alias the request
+    with pytest.raises(CheckError):
+        s.Add(Message())
+    bad = Message()
+    bad.AddData(np.array([1], np.uint32))
+    bad.AddData(np.array([1], np.uint32))
+    with pytest.raises(CheckError):
+        s.Get(bad)
+
+
+def test_python_range_partition_manager_mirror():
+    from parameter_server_amd import RangePartitionManager
+
+    pm = RangePartitionManager([0, 1, 2], [(0, 4), (4, 8), (8, 10)])
+    sl = pm.Slice((np.array([2, 5, 9], np.uint32), np.array([.2, .5, .9])))
+    assert [s for s, _ in sl] == [0, 1, 2]
+    assert [float(kv[1][0]) for _, kv in sl] == [.2, .5, .9]
+    pm2 = RangePartitionManager([0, 1, 2], [(2, 4), (4, 7), (7, 10)])
+    sl2 = pm2.Slice(np.array([2, 8, 9], np.uint32))
+    assert [(s, list(k)) for s, k in sl2] == [(0, [2]), (2, [8, 9])]

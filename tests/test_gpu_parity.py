@@ -1,0 +1,379 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle.
+
+Bar: bit-exact for assign mode (every dtype: the server does no arithmetic),
+exact for int32 accumulate, and for float accumulate the recursive-summation
+bound stated in DESIGN.md:
+    |gpu - ref64| <= 1.01 * (m + 1) * u * (|p0| + sum|v_i|),  u = 2^-24 (f32) / 2^-53 (f64)
+with m the number of pushes of that key.
+"""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+DT = {"int32": np.int32, "float32": np.float32, "float64": np.float64}
+
+
+def tdev(a, cuda, offset=0):
+    """numpy -> device tensor (uint32 keys travel as int32 bits).  offset > 0
+    returns a view that starts `offset` elements into a larger buffer, so its
+    pointer is NOT 16-byte aligned (exercises the scalar kernel variants)."""
+    import torch
+
+    a = np.ascontiguousarray(a)
+    if a.dtype == np.uint32:
+        a = a.view(np.int32)
+    t = torch.from_numpy(a.copy())
+    if offset:
+        pad = torch.zeros(a.size + offset, dtype=t.dtype)
+        pad[offset:] = t
+        return pad.to(cuda)[offset:]
+    return t.to(cuda)
+
+
+def bits(x):
+    x = np.asarray(x)
+    return x.view({4: np.uint32, 8: np.uint64}[x.dtype.itemsize])
+
+
+def assert_bits_equal(got, want, msg=""):
+    g, w = bits(got), bits(want)
+    if not np.array_equal(g, w):
+        bad = np.nonzero(g != w)[0]
+        raise AssertionError(f"{msg}: {bad.size} mismatches, first at {bad[:5]}: got {np.asarray(got)[bad[:5]]} "
+                             f"want {np.asarray(want)[bad[:5]]}")
+
+
+def test_cpp_boundary_program(cuda):
+    """tests/cpp/hip_storage_test.cpp: the reference's storage unit tests through
+    HipStorage<Val> held as std::unique_ptr<AbstractStorage>."""
+    exe = os.path.join(ROOT, "parameter_server_amd", "bin", "hip_storage_test")
+    r = subprocess.run(["timeout", "-k", "10", "300", exe], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert " 0 failed" in r.stdout
+
+
+def known():
+    with open(os.path.join(GOLDEN, "reference_known_answers.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("case", known()["storage_cases"], ids=lambda c: c["name"])
+def test_reference_known_answers_hipstorage(cuda, case):
+    from parameter_server_amd import HipStorage, Message
+
+    dt = DT[case["dtype"]]
+    s = HipStorage(dt, 0, 1 << 20)
+    try:
+        for op in case["ops"]:
+            m = Message()
+            m.AddData(np.array(op[1], np.uint32))
+            if op[0] == "add":
+                m.AddData(np.array(op[2], dt))
+                s.Add(m)
+            else:
+                rep = s.Get(m)
+                assert len(rep.data) == 2
+                assert list(rep.data[0].view(np.uint32)) == op[1]
+                assert_bits_equal(rep.data[1].view(dt), np.array(op[2], dt), case["cite"])
+        s.FinishIter()
+    finally:
+        s.close()
+
+
+def golden_cases():
+    with open(os.path.join(GOLDEN, "assign_vectors.json")) as f:
+        return json.load(f)["cases"]
+
+
+@pytest.mark.parametrize("layout", [(0, 5000), (2**31 - 700, 2**31 + 700)], ids=["low", "mid"])
+@pytest.mark.parametrize("path", ["host", "device", "device_hint", "device_grouped_hint", "device_unaligned"])
+@pytest.mark.parametrize("case", golden_cases(), ids=lambda c: c["name"])
+def test_golden_vectors(cuda, case, path, layout):
+    import parameter_server_amd as ps
+
+    z = np.load(os.path.join(GOLDEN, "assign_vectors.npz"))
+    dt = DT[case["dtype"]]
+    name = case["name"]
+    with ps.Shard(layout[0], layout[1], dt, overflow_slots=1 << 14) as sh:
+        adds = [(z[f"{name}/add{j}/keys"], z[f"{name}/add{j}/vals"]) for j in range(case["n_adds"])]
+        if path == "host":
+            for k, v in adds:
+                sh.add(k, v)
+        elif path == "device_grouped_hint":
+            sh.add_grouped([(tdev(k, cuda), tdev(v, cuda)) for k, v in adds], sorted_hint=True)
+        else:
+            off = 1 if path == "device_unaligned" else 0
+            for k, v in adds:
+                sh.add(tdev(k, cuda, off), tdev(v, cuda, off), sorted_hint=(path == "device_hint"))
+        q = z[f"{name}/get/keys"]
+        got = sh.get(q)
+        sh.sync()
+    assert_bits_equal(got, z[f"{name}/get/expect"], f"{name}/{path}/{layout}")
+
+
+@pytest.mark.parametrize("dt", [np.int32, np.float32, np.float64])
+def test_random_assign_parity_all_paths(cuda, oracle_mod, dt):
+    import torch
+
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(123)
+    kb, ke = 10_000, 10_000 + 300_000
+    ref = oracle_mod.MapStorageRef(dt)
+    with ps.Shard(kb, ke, dt, overflow_slots=1 << 16) as sh:
+        for step in range(12):
+            n = int(rng.integers(0, 70_000))
+            kind = step % 4
+            if kind == 0:      # unsorted, duplicates, some out of range
+                k = rng.integers(kb - 2000, ke + 2000, size=n)
+            elif kind == 1:    # sorted with runs of duplicates
+                k = np.sort(rng.integers(kb, ke, size=n))
+            elif kind == 2:    # contiguous window (dense)
+                b = int(rng.integers(kb, ke - n - 1)) if n < ke - kb - 2 else kb
+                k = np.arange(b, b + n)
+            else:              # sorted but with out-of-range tail -> sorted hint must repair
+                k = np.sort(rng.integers(kb, ke + 50, size=n))
+            k = k.astype(np.uint32)
+            v = (rng.standard_normal(n) * 1e3).astype(dt)
+            mode = step % 3
+            if mode == 0:
+                sh.add(k, v)
+            elif mode == 1:
+                sh.add(tdev(k, cuda), tdev(v, cuda), sorted_hint=True)
+            else:
+                sh.add(tdev(k, cuda, 3), tdev(v, cuda, 3), sorted_hint=bool(step & 1))
+            ref.add(k, v)
+        q = np.concatenate([np.arange(kb - 3000, ke + 3000),
+                            rng.integers(0, 2**32, size=5000)]).astype(np.uint32)
+        got_h = sh.get(q)
+        got_d = sh.get(tdev(q, cuda)).cpu().numpy().view(dt)
+        torch.cuda.synchronize()
+        sh.sync()
+    want = ref.get(q)
+    assert_bits_equal(got_h, want, "host get")
+    assert_bits_equal(got_d, want, "device get")
+
+
+def test_sorted_hint_on_unsorted_data_is_repaired(cuda, oracle_mod):
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(9)
+    ref = oracle_mod.MapStorageRef(np.float32)
+    with ps.Shard(0, 100_000, np.float32) as sh:
+        before = sh.info()["n_general_launches"]
+        k = rng.integers(0, 100_000, size=50_000).astype(np.uint32)   # unsorted, duplicates
+        v = rng.standard_normal(k.size).astype(np.float32)
+        sh.add(tdev(k, cuda), tdev(v, cuda), sorted_hint=True)
+        ref.add(k, v)
+        got = sh.get(np.arange(100_000, dtype=np.uint32))
+        assert sh.info()["n_general_launches"] > before
+    assert_bits_equal(got, ref.get(np.arange(100_000, dtype=np.uint32)), "repair")
+
+
+@pytest.mark.parametrize("nb", [2, 7, 64, 70])
+def test_grouped_overlapping_batches_later_wins(cuda, oracle_mod, nb):
+    """Grouped sorted Add (K2g key-tile owner): batches overlap; call order decides."""
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(nb)
+    size = 200_000
+    dense = np.zeros(size, np.float32)
+    batches = []
+    for j in range(nb):
+        n = int(rng.integers(1, 40_000))
+        if j % 3 == 0:
+            b = int(rng.integers(0, size - n))
+            k = np.arange(b, b + n)
+        else:
+            k = np.sort(rng.integers(0, size, size=n))
+        k = k.astype(np.uint32)
+        v = rng.standard_normal(n).astype(np.float32)
+        batches.append((k, v))
+        oracle_mod.dense_last_wins(dense, 0, k, v)
+    with ps.Shard(0, size, np.float32) as sh:
+        sh.add_grouped([(tdev(k, cuda), tdev(v, cuda)) for k, v in batches], sorted_hint=True)
+        got = sh.get(np.arange(size, dtype=np.uint32))
+        info = sh.info()
+    assert info["n_sorted_launches"] >= 1
+    assert_bits_equal(got, dense, f"grouped nb={nb}")
+
+
+def test_grouped_get_matches_single(cuda):
+    import torch
+
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(4)
+    with ps.Shard(0, 1 << 20, np.float64) as sh:
+        k = np.arange(1 << 20, dtype=np.uint32)
+        v = rng.standard_normal(k.size)
+        sh.add(k, v)
+        qs = [rng.integers(0, 1 << 21, size=int(n)).astype(np.uint32) for n in (1, 5, 4096, 100_001, 0, 77)]
+        outs = [torch.empty(q.size, dtype=torch.float64, device=cuda) for q in qs]
+        sh.get_grouped([(tdev(q, cuda), o) for q, o in zip(qs, outs)])
+        torch.cuda.synchronize()
+        for q, o in zip(qs, outs):
+            assert_bits_equal(o.cpu().numpy(), sh.get(q), "grouped get")
+            want = np.where(q < (1 << 20), v[np.minimum(q, (1 << 20) - 1)], 0.0)
+            assert_bits_equal(o.cpu().numpy(), want, "vs numpy")
+
+
+@pytest.mark.parametrize("dt", [np.int32, np.float32, np.float64])
+def test_accumulate_mode(cuda, dt):
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(77)
+    kb, size = 500, 50_000
+    p64 = np.zeros(size, np.float64)
+    a64 = np.zeros(size, np.float64)
+    cnt = np.zeros(size, np.int64)
+    acc_i = np.zeros(size, np.int64)
+    with ps.Shard(kb, kb + size, dt, mode="accumulate") as sh:
+        for step in range(6):
+            n = int(rng.integers(1000, 80_000))
+            k = (rng.zipf(1.2, size=n) % size + kb).astype(np.uint32) if step % 2 else \
+                np.sort(rng.integers(kb, kb + size, size=n)).astype(np.uint32)
+            if dt is np.int32:
+                v = rng.integers(-2**31, 2**31 - 1, size=n, dtype=np.int64).astype(np.int32)
+            else:
+                v = rng.standard_normal(n).astype(dt)
+            if step % 3 == 2:
+                sh.add(tdev(k, cuda), tdev(v, cuda), sorted_hint=True)
+            else:
+                sh.add(k, v)
+            idx = k.astype(np.int64) - kb
+            np.add.at(p64, idx, v.astype(np.float64))
+            np.add.at(a64, idx, np.abs(v.astype(np.float64)))
+            np.add.at(cnt, idx, 1)
+            np.add.at(acc_i, idx, v.astype(np.int64))
+        got = sh.get(np.arange(kb, kb + size, dtype=np.uint32))
+    if dt is np.int32:
+        want = ((acc_i + 2**31) % 2**32 - 2**31).astype(np.int32)  # wrap-around sum is exact
+        assert_bits_equal(got, want, "int32 accumulate")
+    else:
+        u = 2.0**-24 if dt is np.float32 else 2.0**-53
+        tol = 1.01 * (cnt + 1) * u * a64
+        err = np.abs(got.astype(np.float64) - p64)
+        assert np.all(err <= tol), f"max err/tol {np.max(err / np.maximum(tol, 1e-300))}"
+
+
+def test_baseline_size_dense_roundtrip(cuda):
+    """cfg 2 at full size: 1e8-float shard, 1M-key contiguous windows at seed-42
+    bases; grouped sorted Add then grouped Get returns the last write of every
+    key (windows may repeat: later wins), untouched keys read 0."""
+    import torch
+
+    import parameter_server_amd as ps
+    from parameter_server_amd import workload
+
+    space, J = 100_000_000, 16
+    bases = workload.dense_bases(J, space)
+    batches = workload.dense_batches(J, space, device=cuda)
+    with ps.Shard(0, space, np.float32) as sh:
+        sh.add_grouped(batches, sorted_hint=True)
+        outs = [torch.empty_like(v) for _, v in batches]
+        sh.get_grouped([(k, o) for (k, _), o in zip(batches, outs)])
+        last = {}
+        for j, b in enumerate(bases):
+            last[int(b)] = j
+        for j, b in enumerate(bases):
+            want = batches[last[int(b)]][1]
+            assert torch.equal(outs[j].view(torch.int32), want.view(torch.int32)), f"window {j}"
+        # a never-written window reads zeros
+        free = next(x for x in range(0, space, 1_000_000) if x not in last)
+        z = sh.get(torch.arange(free, free + 1_000_000, dtype=torch.int32, device=cuda))
+        assert int(torch.count_nonzero(z)) == 0
+        dv = sh.dense_view()
+        b0 = int(bases[0])
+        assert torch.equal(dv[b0:b0 + 1_000_000].view(torch.int32), outs[0].view(torch.int32))
+        sh.sync()
+
+
+def test_zipf_batches_parity(cuda, oracle_mod):
+    """cfg 3 shape at reduced key space: unsorted Zipf(0.99) pushes with heavy
+    duplicates go through K4 (LDS dedup + stamps) and match the oracle."""
+    import torch
+
+    import parameter_server_amd as ps
+    from parameter_server_amd import workload
+
+    space = 2_000_000
+    batches = workload.zipf_batches(4, space, batch=262_144, device=cuda)
+    dense = np.zeros(space, np.float32)
+    with ps.Shard(0, space, np.float32) as sh:
+        sh.add_grouped(batches[:2])
+        for k, v in batches[2:]:
+            sh.add(k, v)
+        for k, v in batches:
+            oracle_mod.dense_last_wins(dense, 0, k.cpu().numpy().view(np.uint32), v.cpu().numpy())
+        got = sh.get(torch.arange(space, dtype=torch.int32, device=cuda)).cpu().numpy()
+    hot = np.bincount(batches[0][0].cpu().numpy().view(np.uint32).astype(np.int64)).max()
+    assert hot > 1000  # the hot key really is hot
+    assert_bits_equal(got, dense, "zipf")
+
+
+def test_overflow_table_growth_and_edges(cuda, oracle_mod):
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(31)
+    ref = oracle_mod.MapStorageRef(np.float32)
+    with ps.Shard(2**32 - 1000, 2**32, np.float32, overflow_slots=64) as sh:
+        for step in range(5):
+            k = rng.integers(0, 2**32, size=30_000).astype(np.uint32)   # almost all overflow
+            k[:10] = 0xFFFFFFFF                                         # the LDS sentinel key, in range
+            k[10:20] = 2**32 - 1000
+            v = rng.standard_normal(k.size).astype(np.float32)
+            sh.add(k, v)                     # host path sizes the table itself
+            ref.add(k, v)
+            sh.sync()
+        info = sh.info()
+        assert info["overflow_capacity"] >= 2 * info["overflow_count"] > 0
+        q = np.concatenate([k, rng.integers(0, 2**32, size=1000).astype(np.uint32),
+                            np.array([0xFFFFFFFF, 0, 2**32 - 1000], np.uint32)])
+        got = sh.get(q)
+        # empty calls are no-ops
+        sh.add(np.zeros(0, np.uint32), np.zeros(0, np.float32))
+        assert sh.get(np.zeros(0, np.uint32)).size == 0
+        sh.add_grouped([])
+    assert_bits_equal(got, ref.get(q), "overflow")
+
+
+def test_size_mismatch_is_rejected(cuda):
+    from parameter_server_amd import CheckError, HipStorage, Message
+
+    s = HipStorage(np.float32, 0, 1000)
+    m = Message()
+    m.AddData(np.array([1, 2, 3], np.uint32))
+    m.AddData(np.array([1.0, 2.0], np.float32))
+    with pytest.raises(CheckError):
+        s.Add(m)
+    s.close()
+
+
+def test_external_stream_and_timing(cuda):
+    import torch
+
+    import parameter_server_amd as ps
+    from parameter_server_amd import _lib
+
+    st = torch.cuda.Stream()
+    with ps.Shard(0, 1 << 22, np.float32) as sh:
+        sh.set_stream(st.cuda_stream)
+        sh.set_timing(True)
+        with torch.cuda.stream(st):
+            k = torch.arange(1 << 22, dtype=torch.int32, device=cuda)
+            v = torch.rand(1 << 22, device=cuda)
+            sh.add(k, v, sorted_hint=True)
+            out = sh.get(k)
+        st.synchronize()
+        assert torch.equal(out, v)
+        t = sh.kernel_time(_lib.PSKV_K_GATHER)
+        assert t["launches"] == 1 and t["total_ms"] > 0 and t["elements"] == 1 << 22
+        sh.set_stream(None)

@@ -1,0 +1,103 @@
+"""CPU tests: pin the oracle (the CPU restatement) to the reference's own known
+answers, and check its restatements against each other.  No GPU."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+DT = {"int32": np.int32, "float32": np.float32, "float64": np.float64}
+
+
+def known():
+    with open(os.path.join(GOLDEN, "reference_known_answers.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("kind", ["map", "vector"])
+@pytest.mark.parametrize("case", known()["storage_cases"], ids=lambda c: c["name"])
+def test_oracle_reference_known_answers(oracle_mod, kind, case):
+    dt = DT[case["dtype"]]
+    ref = (oracle_mod.MapStorageRef if kind == "map" else oracle_mod.VectorStorageRef)(dt)
+    for op in case["ops"]:
+        if op[0] == "add":
+            ref.add(np.array(op[1], np.uint32), np.array(op[2], dt))
+        else:
+            got = ref.get(np.array(op[1], np.uint32))
+            want = np.array(op[2], dt)  # SArray<float>({0.1,...}) rounds the double literal to float
+            assert np.array_equal(got.view(np.uint8), want.view(np.uint8)), (case["cite"], got, want)
+
+
+@pytest.mark.parametrize("case", known()["slice_cases"], ids=lambda c: c["cite"][:40])
+def test_range_slice_ref_known_answers(oracle_mod, case):
+    got = oracle_mod.range_slice_ref([tuple(r) for r in case["ranges"]], case["keys"])
+    assert [[r, ks] for r, ks in got] == case["expect"], case["cite"]
+    # the C restatement assigns the same range to every key
+    ra = oracle_mod.range_assign([tuple(r) for r in case["ranges"]], case["keys"])
+    flat = [r for r, ks in case["expect"] for _ in ks]
+    assert list(ra) == flat
+
+
+def test_range_assign_matches_python(oracle_mod):
+    rng = np.random.default_rng(3)
+    for _ in range(50):
+        nr = int(rng.integers(1, 6))
+        cuts = np.sort(rng.choice(np.arange(1, 1000), size=nr, replace=False))
+        ranges = [(int(a), int(b)) for a, b in zip(np.r_[int(rng.integers(0, 50)), cuts[:-1]], cuts)]
+        keys = rng.integers(0, 1100, size=int(rng.integers(0, 200)))
+        if rng.random() < 0.5:
+            keys = np.sort(keys)
+        py = oracle_mod.range_slice_ref(ranges, keys)
+        flat = [r for r, ks in py for _ in ks]
+        assert list(oracle_mod.range_assign(ranges, keys)) == flat
+
+
+@pytest.mark.parametrize("dt", [np.int32, np.float32, np.float64])
+def test_vector_and_map_storage_are_equivalent(oracle_mod, dt):
+    """both reference storages are last-write-wins with default 0."""
+    rng = np.random.default_rng(11)
+    m, v = oracle_mod.MapStorageRef(dt), oracle_mod.VectorStorageRef(dt)
+    for _ in range(6):
+        n = int(rng.integers(0, 700))
+        k = rng.integers(0, 900, size=n).astype(np.uint32)
+        x = (rng.standard_normal(n) * 1000).astype(dt)
+        m.add(k, x)
+        v.add(k, x)
+        q = rng.integers(0, 1000, size=500).astype(np.uint32)
+        assert np.array_equal(m.get(q).view(np.uint8), v.get(q).view(np.uint8))
+    assert v.size() >= m.size()
+
+
+def test_dense_last_wins_matches_map(oracle_mod):
+    rng = np.random.default_rng(5)
+    m = oracle_mod.MapStorageRef(np.float32)
+    dense = np.zeros(4000, np.float32)
+    for _ in range(10):
+        n = int(rng.integers(1, 3000))
+        k = (rng.zipf(1.5, size=n) % 4000).astype(np.uint32)
+        x = rng.standard_normal(n).astype(np.float32)
+        m.add(k, x)
+        oracle_mod.dense_last_wins(dense, 0, k, x)
+    q = np.arange(4000, dtype=np.uint32)
+    assert np.array_equal(m.get(q).view(np.uint32), dense.view(np.uint32))
+
+
+def test_golden_vectors_reproduce_with_both_restatements(oracle_mod):
+    z = np.load(os.path.join(GOLDEN, "assign_vectors.npz"))
+    with open(os.path.join(GOLDEN, "assign_vectors.json")) as f:
+        meta = json.load(f)
+    for c in meta["cases"]:
+        dt = DT[c["dtype"]]
+        for cls in (oracle_mod.MapStorageRef, oracle_mod.VectorStorageRef):
+            ref = cls(dt)
+            for j in range(c["n_adds"]):
+                ref.add(z[f"{c['name']}/add{j}/keys"], z[f"{c['name']}/add{j}/vals"])
+            got = ref.get(z[f"{c['name']}/get/keys"])
+            assert np.array_equal(got.view(np.uint8), z[f"{c['name']}/get/expect"].view(np.uint8)), c
+
+
+def test_oracle_rejects_mismatched_sizes(oracle_mod):
+    ref = oracle_mod.MapStorageRef(np.float32)
+    with pytest.raises(ValueError):
+        ref.add(np.arange(3, dtype=np.uint32), np.zeros(2, np.float32))
