@@ -146,7 +146,8 @@ int pskv_sync(pskv_shard* s);
 /* Zero every value (dense array and overflow table). */
 int pskv_clear(pskv_shard* s);
 
-/* Run the shard's work on an external hipStream_t (NULL = the shard's own stream). */
+/* Run the shard's work on an external hipStream_t (NULL = the shard's own
+ * stream, a blocking stream that orders against the legacy default stream). */
 int pskv_set_stream(pskv_shard* s, void* hip_stream);
 void* pskv_get_stream(pskv_shard* s);
 /* Device pointer of the dense array (for zero-copy inspection by tests/benches). */

@@ -572,7 +572,9 @@ int pskv_shard_create_ex(int device, uint32_t key_begin, uint64_t key_end, int d
   };
   int rc = use_device(s);
   if (rc) return bail(rc);
-  if (hipStreamCreateWithFlags(&s->own_stream, hipStreamNonBlocking) != hipSuccess)
+  // A blocking stream: it orders against the legacy default stream, on which
+  // frameworks (torch) stage device inputs and read device outputs.
+  if (hipStreamCreateWithFlags(&s->own_stream, hipStreamDefault) != hipSuccess)
     return bail(fail(PSKV_EHIP, "hipStreamCreate failed"));
   s->stream = s->own_stream;
   if (hipEventCreateWithFlags(&s->hstage_free, hipEventDisableTiming) != hipSuccess)
