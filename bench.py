@@ -31,7 +31,18 @@ sys.path.insert(0, ROOT)
 
 METRIC = "device-resident KV Add+Get GB/s (grad+param bytes) at 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
-BYTES_PER_KEY = {"add": 12, "get": 12}  # f32 assign: Add key4+val4+param4; Get key4+param4+out4
+V = 4  # f32 values
+# Algorithmic bytes, counted conservatively per step:
+#   Add (assign): n*(4+V) input + u*V param write, u = DISTINCT keys pushed in the
+#                 step (a window pushed twice in one step is written once: the
+#                 grouped Add skips writes a later batch overwrites)
+#   Get:          q*(4+2V) (key read + param read + value write)
+
+
+def step_bytes(n_push, u_push, n_pull):
+    add = n_push * (4 + V) + u_push * V
+    get = n_pull * (4 + 2 * V)
+    return add, get
 
 
 def parse():
@@ -216,10 +227,13 @@ def side_measurements(dev, B):
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         uniq = int(torch.unique(zb[0][0]).numel())
+        u_all = int(torch.unique(torch.cat([k for k, _ in zb])).numel())
         sh.set_stream(None)
-    out["zipf"] = {"workload": "cfg 3: Zipf(0.99) over 1e8 keys, 8 x 1M unsorted pushes then pulls, assign",
-                   "GB/s": 24.0 * B * J * reps / dt / 1e9, "ms_per_step": dt / reps * 1e3,
-                   "unique_keys_per_batch": uniq}
+    add_b, get_b = step_bytes(J * B, u_all, J * B)
+    out["zipf"] = {"workload": "cfg 3: Zipf(0.99) over 1e8 keys, 8 x 1M unsorted pushes then pulls, assign "
+                               "(general path: LDS dedup + stamps)",
+                   "GB/s": (add_b + get_b) * reps / dt / 1e9, "ms_per_step": dt / reps * 1e3,
+                   "unique_keys_per_batch": uniq, "distinct_keys_per_step": u_all}
     del zb, zo
     # end-to-end: keys/vals start in pageable host memory (the zmq frames), outputs return to host
     rng = np.random.default_rng(0)
@@ -239,9 +253,10 @@ def side_measurements(dev, B):
         dt = time.perf_counter() - t0
     last = {int(k[0]): j for j, k in enumerate(hk)}  # repeated windows: the later push wins
     assert all(np.array_equal(o, hv[last[int(k[0])]]) for o, k in zip(ho, hk))
+    add_b, get_b = step_bytes(J * B, len(set(int(k[0]) for k in hk)) * B, J * B)
     out["e2e_host_buffers"] = {"workload": "8 x 1M contiguous float keys from pageable host memory, Add then Get "
                                            "(H2D + kernels + D2H, host sortedness check included)",
-                               "GB/s": 24.0 * B * J * reps / dt / 1e9}
+                               "GB/s": (add_b + get_b) * reps / dt / 1e9}
     return out
 
 
@@ -259,10 +274,11 @@ def main():
     stream = torch.cuda.current_stream()
     shard = ps.Shard(lo, hi, np.float32, device=local)
     shard.set_stream(stream.cuda_stream)  # torch events and the kernels share one stream
-    gets = [(k, o) for (k, _), o in zip(batches, outs)]
+    adds = shard.prepare(batches)
+    gets = shard.prepare([(k, o) for (k, _), o in zip(batches, outs)], is_get=True)
 
     def step():
-        shard.add_grouped(batches, sorted_hint=True)
+        shard.add_grouped(adds, sorted_hint=True)
         shard.get_grouped(gets)
 
     for _ in range(args.warmup):
@@ -274,7 +290,8 @@ def main():
         assert torch.equal(outs[j], batches[last[int(b)]][1]), "bench self-check failed"
 
     shard.reset_timing()
-    shard.set_timing(True)
+    # HIP events bracket the two streaming kernels of the step (on the launch stream)
+    shard.set_timing(True, kernels=[_lib.PSKV_K_GATHER, _lib.PSKV_K_ASSIGN_TILES])
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -293,18 +310,24 @@ def main():
             ktimes[name] = {"launches": t["launches"], "avg_ms": t["total_ms"] / t["launches"],
                             "keys_per_launch": t["elements"] / t["launches"]}
     shard.sync()
-    bytes_rank = float(J * B * (BYTES_PER_KEY["add"] + BYTES_PER_KEY["get"]) * args.steps)
-    total_bytes = sum_over_ranks(bytes_rank, world, dev)
+    u_push = len(set(int(b) for b in bases)) * B  # distinct keys pushed per step
+    add_b, get_b = step_bytes(J * B, u_push, J * B)
+    total_bytes = sum_over_ranks(float((add_b + get_b) * args.steps), world, dev)
     value = total_bytes / elapsed / 1e9
 
     # dominant kernel: the one with the most time in the timed region
     dom = max(ktimes.items(), key=lambda kv: kv[1]["avg_ms"] * kv[1]["launches"])
-    per_key = BYTES_PER_KEY["get"] if dom[0] == "k_gather" else BYTES_PER_KEY["add"]
-    achieved = per_key * dom[1]["keys_per_launch"] / (dom[1]["avg_ms"] / 1e3) / 1e9
+    launch_bytes = get_b if dom[0] == "k_gather" else add_b  # one launch = one step's Add or Get
+    achieved = launch_bytes / (dom[1]["avg_ms"] / 1e3) / 1e9
     traffic, traffic_src = load_pmc(dom[0])
+    for name, kt in ktimes.items():
+        kt["algorithmic_bytes"] = get_b if name == "k_gather" else add_b
+        kt["GB/s"] = kt["algorithmic_bytes"] / (kt["avg_ms"] / 1e3) / 1e9
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": dom[0],
-            "algorithmic_bytes_per_key": per_key, "kernels": ktimes}
+            "algorithmic_bytes_per_launch": launch_bytes,
+            "bytes_per_unit": "Add n*(4+V)+u*V, Get q*(4+2V); V=4, u=distinct pushed keys",
+            "kernels": ktimes}
     if traffic_src:
         roof["traffic_source"] = traffic_src
 
@@ -330,7 +353,8 @@ def main():
             "shard_keys_per_gpu": hi - lo,
             "batches_per_step_per_gpu": J,
             "batch_keys": B,
-            "bytes_per_key": BYTES_PER_KEY["add"] + BYTES_PER_KEY["get"],
+            "bytes_per_step_per_gpu": add_b + get_b,
+            "distinct_pushed_keys_per_step": u_push,
             "parallelism": f"range-sharded x{world} (no collective)",
         },
         "roofline": roof,

@@ -154,8 +154,11 @@ void* pskv_get_stream(pskv_shard* s);
 void* pskv_dense_ptr(pskv_shard* s);
 int pskv_shard_info(pskv_shard* s, pskv_info* info);
 
-/* Per-kernel timing with HIP events on the launch stream (off by default). */
+/* Per-kernel timing with HIP events on the launch stream (off by default).
+ * pskv_set_timing brackets every kernel; pskv_set_timing_mask only the kernels
+ * whose bit (1 << pskv_kernel) is set. */
 int pskv_set_timing(pskv_shard* s, int enable);
+int pskv_set_timing_mask(pskv_shard* s, uint32_t kernel_mask);
 int pskv_kernel_time(pskv_shard* s, int kernel, uint64_t* launches, double* total_ms,
                      uint64_t* elements);
 int pskv_reset_timing(pskv_shard* s);

@@ -42,7 +42,7 @@ KERNEL_NAMES = {
 EXPORTED = [
     "pskv_shard_create", "pskv_shard_create_ex", "pskv_shard_destroy", "pskv_add", "pskv_get",
     "pskv_add_grouped", "pskv_get_grouped", "pskv_sync", "pskv_clear", "pskv_set_stream",
-    "pskv_get_stream", "pskv_dense_ptr", "pskv_shard_info", "pskv_set_timing",
+    "pskv_get_stream", "pskv_dense_ptr", "pskv_shard_info", "pskv_set_timing", "pskv_set_timing_mask",
     "pskv_kernel_time", "pskv_reset_timing", "pskv_range_slice", "pskv_last_error",
     "pskv_abi_version", "pskv_device_count",
 ]
@@ -91,6 +91,7 @@ def _load():
         "pskv_dense_ptr": ([vp], vp),
         "pskv_shard_info": ([vp, ctypes.POINTER(PskvInfo)], i32),
         "pskv_set_timing": ([vp, i32], i32),
+        "pskv_set_timing_mask": ([vp, u32], i32),
         "pskv_kernel_time": ([vp, i32, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_double),
                               ctypes.POINTER(u64)], i32),
         "pskv_reset_timing": ([vp], i32),

@@ -17,9 +17,8 @@ namespace pskv {
 constexpr int kMaxBatches = 64;     // batches per grouped launch (kernarg budget)
 constexpr int kBlock = 256;         // threads per workgroup (4 waves)
 constexpr int kGatherVec = 4;       // keys per lane per step (16 B loads)
-constexpr int kGatherUnroll = 4;    // steps per lane
-constexpr int kGatherChunk = kBlock * kGatherVec * kGatherUnroll;  // 4096 keys / workgroup
 constexpr int kSortedUnroll = 2;
+inline int stream_chunk(int unroll) { return kBlock * 4 * unroll; }  // keys per gather / dense chunk
 constexpr int kSortedChunk = kBlock * 4 * kSortedUnroll;          // 2048 keys / workgroup
 constexpr int kGeneralChunk = 2048;  // keys per workgroup in the dedup path
 constexpr int kGeneralSlots = 4096;  // LDS hash slots (load factor <= 1/2)
@@ -59,14 +58,18 @@ struct Ovf {
 
 // Launch wrappers (pskv_kernels.hip).  vb = value bytes (4 or 8), vec = all
 // pointers 16-byte aligned so 16 B vector accesses are legal.
-hipError_t launch_gather(int vb, bool vec, const GroupArgs& ga, uint32_t nwg, const DenseView& d,
-                         const Ovf& o, hipStream_t st);
+// unroll: 4 or 8 groups of 4 keys per lane (chunk = 256*4*unroll keys);
+// nt: non-temporal loads/stores of the streamed push/pull buffers.
+hipError_t launch_gather(int vb, bool vec, int unroll, bool nt, const GroupArgs& ga, uint32_t nwg,
+                         const DenseView& d, const Ovf& o, hipStream_t st);
 hipError_t launch_assign_sorted(int vb, bool vec, const uint32_t* keys, const void* vals,
                                 uint64_t n, const DenseView& d, uint32_t* flag, uint32_t epoch,
                                 hipStream_t st);
-hipError_t launch_assign_tiles(int vb, bool vec, const GroupArgs& ga, const DenseView& d,
-                               uint32_t tile_shift, uint64_t ntiles, uint32_t grid,
-                               uint32_t* flag, uint32_t epoch, hipStream_t st);
+// Grouped sorted Add.  `ga` must be built with stream_chunk(unroll) elements per chunk
+// (used by the dense-window mode); the tile mode ignores the chunking.
+hipError_t launch_assign_group(int vb, bool vec, int unroll, bool nt, const GroupArgs& ga,
+                               const DenseView& d, uint32_t tile_shift, uint64_t ntiles,
+                               uint32_t grid, uint32_t* flag, uint32_t epoch, hipStream_t st);
 hipError_t launch_general_mark(int dtype, int mode, const GroupArgs& ga, uint32_t nwg,
                                const DenseView& d, const Ovf& o, unsigned long long* owner,
                                const uint32_t* cond, uint32_t epoch, hipStream_t st);

@@ -38,31 +38,52 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
   return h;
 }
 
+// 16-byte accesses through clang vector types; NT = non-temporal (streamed
+// once: keys/values of a push, outputs of a pull).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(const void* p) {
+  if (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  return *reinterpret_cast<const u32x4*>(p);
+}
+template <bool NT>
+__device__ __forceinline__ void st16(void* p, u32x4 v) {
+  if (NT)
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+  else
+    *reinterpret_cast<u32x4*>(p) = v;
+}
+
 template <typename VT>
 struct Vec4;
 
 template <>
 struct Vec4<uint32_t> {
+  template <bool NT = false>
   static __device__ __forceinline__ void load(const uint32_t* p, uint32_t (&v)[4]) {
-    const uint4 t = *reinterpret_cast<const uint4*>(p);
+    const u32x4 t = ld16<NT>(p);
     v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
   }
+  template <bool NT = false>
   static __device__ __forceinline__ void store(uint32_t* p, const uint32_t (&v)[4]) {
-    *reinterpret_cast<uint4*>(p) = make_uint4(v[0], v[1], v[2], v[3]);
+    st16<NT>(p, u32x4{v[0], v[1], v[2], v[3]});
   }
 };
 
 template <>
 struct Vec4<unsigned long long> {
   using T = unsigned long long;
+  template <bool NT = false>
   static __device__ __forceinline__ void load(const T* p, T (&v)[4]) {
-    const ulonglong2 a = reinterpret_cast<const ulonglong2*>(p)[0];
-    const ulonglong2 b = reinterpret_cast<const ulonglong2*>(p)[1];
-    v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
+    const u32x4 a = ld16<NT>(p), b = ld16<NT>(p + 2);
+    v[0] = (T)a.x | ((T)a.y << 32); v[1] = (T)a.z | ((T)a.w << 32);
+    v[2] = (T)b.x | ((T)b.y << 32); v[3] = (T)b.z | ((T)b.w << 32);
   }
+  template <bool NT = false>
   static __device__ __forceinline__ void store(T* p, const T (&v)[4]) {
-    reinterpret_cast<ulonglong2*>(p)[0] = make_ulonglong2(v[0], v[1]);
-    reinterpret_cast<ulonglong2*>(p)[1] = make_ulonglong2(v[2], v[3]);
+    st16<NT>(p, u32x4{(uint32_t)v[0], (uint32_t)(v[0] >> 32), (uint32_t)v[1], (uint32_t)(v[1] >> 32)});
+    st16<NT>(p + 2, u32x4{(uint32_t)v[2], (uint32_t)(v[2] >> 32), (uint32_t)v[3], (uint32_t)(v[3] >> 32)});
   }
 };
 
@@ -136,28 +157,29 @@ __device__ __forceinline__ void gather4(const DenseView& d, const Ovf& o, const 
   }
 }
 
-template <typename VT, bool VEC>
+template <typename VT, bool VEC, int U, bool NT>
 __global__ __launch_bounds__(kBlock) void k_gather(GroupArgs ga, DenseView d, Ovf o) {
+  constexpr int CH = kBlock * 4 * U;
   const uint32_t wg = blockIdx.x;
   const int j = batch_of(ga, wg);
   const uint32_t* __restrict__ keys = ga.b[j].keys;
   VT* __restrict__ out = reinterpret_cast<VT*>(const_cast<void*>(ga.b[j].vals));
   const uint64_t n = ga.b[j].n;
-  const uint64_t base = (uint64_t)(wg - ga.wg_prefix[j]) * kGatherChunk;
+  const uint64_t base = (uint64_t)(wg - ga.wg_prefix[j]) * CH;
   const int tid = threadIdx.x;
-  if (VEC && base + kGatherChunk <= n) {
-    uint32_t k[kGatherUnroll][4];
+  if (VEC && base + CH <= n) {
+    uint32_t k[U][4];
 #pragma unroll
-    for (int u = 0; u < kGatherUnroll; ++u)
-      Vec4<uint32_t>::load(keys + base + (uint64_t)(u * kBlock + tid) * 4, k[u]);
-    VT v[kGatherUnroll][4];
+    for (int u = 0; u < U; ++u)
+      Vec4<uint32_t>::load<NT>(keys + base + (uint64_t)(u * kBlock + tid) * 4, k[u]);
+    VT v[U][4];
 #pragma unroll
-    for (int u = 0; u < kGatherUnroll; ++u) gather4<VT>(d, o, k[u], v[u]);
+    for (int u = 0; u < U; ++u) gather4<VT>(d, o, k[u], v[u]);
 #pragma unroll
-    for (int u = 0; u < kGatherUnroll; ++u)
-      Vec4<VT>::store(out + base + (uint64_t)(u * kBlock + tid) * 4, v[u]);
+    for (int u = 0; u < U; ++u)
+      Vec4<VT>::template store<NT>(out + base + (uint64_t)(u * kBlock + tid) * 4, v[u]);
   } else {
-    const uint64_t end = n < base + kGatherChunk ? n : base + kGatherChunk;
+    const uint64_t end = n < base + CH ? n : base + CH;
     for (uint64_t i = base + tid; i < end; i += kBlock) out[i] = load_one<VT>(d, o, keys[i]);
   }
 }
@@ -319,57 +341,144 @@ __device__ __forceinline__ bool apply_segment(const DevBatch& b, uint64_t s, uin
   return bad;
 }
 
-template <typename VT, bool VEC>
-__global__ __launch_bounds__(kBlock) void k_assign_tiles(GroupArgs ga, DenseView d,
+// Mode A (all batches dense): batch j of the group is a contiguous run
+// first_j .. first_j + n_j - 1 (the vector_storage push of a whole parameter
+// slice).  "A later call wins" is then an interval test: key k of batch j is
+// stored unless some later batch j' > j covers k.  Work is split by elements
+// (4096 per chunk, grid-stride), so the launch is balanced like the gather;
+// each chunk intersects its key interval with the later batches' intervals
+// once (a 64-lane ballot) and elements test only the few that overlap.
+// Every element verifies k == first_j + i; a batch whose endpoints look dense
+// but whose keys are not is caught there and tagged for the repair.
+template <typename VT, bool VEC, int U, bool NT>
+__device__ __forceinline__ bool dense_chunk(const GroupArgs& ga, const DenseView& d, uint32_t c,
+                                            const uint32_t* s_first, const uint32_t* s_last) {
+  constexpr int CH = kBlock * 4 * U;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int j = batch_of(ga, c);
+  const uint32_t* __restrict__ keys = ga.b[j].keys;
+  const VT* __restrict__ vals = reinterpret_cast<const VT*>(ga.b[j].vals);
+  const uint64_t n = ga.b[j].n;
+  const uint64_t base = (uint64_t)(c - ga.wg_prefix[j]) * CH;
+  const uint64_t end = n < base + CH ? n : base + CH;
+  const uint32_t first = s_first[j];
+  const uint32_t c_lo = first + (uint32_t)base, c_hi = first + (uint32_t)(end - 1);
+  // later batches whose interval meets this chunk's interval (every wave computes it)
+  const bool ov = lane > j && lane < ga.nb && s_first[lane] <= c_hi && s_last[lane] >= c_lo;
+  const unsigned long long later = __ballot(ov);
+  VT* __restrict__ param = reinterpret_cast<VT*>(d.param);
+  bool bad = false;
+  auto shadowed = [&](uint32_t k) {
+    unsigned long long m = later;
+    bool sh = false;
+    while (m) {
+      const int q = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      sh |= (k >= s_first[q]) & (k <= s_last[q]);
+    }
+    return sh;
+  };
+  if (VEC && end - base == CH) {
+    uint32_t k[U][4];
+    VT v[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = base + (uint64_t)(u * kBlock + tid) * 4;
+      Vec4<uint32_t>::load<NT>(keys + i, k[u]);
+      Vec4<VT>::template load<NT>(vals + i, v[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = base + (uint64_t)(u * kBlock + tid) * 4;
+      const uint32_t k0 = first + (uint32_t)i;
+      bad |= (k[u][0] != k0) | (k[u][1] != k0 + 1u) | (k[u][2] != k0 + 2u) | (k[u][3] != k0 + 3u);
+      const uint32_t off0 = k0 - d.key_begin;
+      if (later == 0 && (off0 & 3u) == 0u) {
+        Vec4<VT>::store(param + off0, v[u]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (!shadowed(k0 + e)) param[off0 + e] = v[u][e];
+      }
+    }
+  } else {
+    for (uint64_t i = base + tid; i < end; i += kBlock) {
+      const uint32_t k = keys[i];
+      bad |= k != first + (uint32_t)i;
+      if (!shadowed(first + (uint32_t)i)) param[(first + (uint32_t)i) - d.key_begin] = vals[i];
+    }
+  }
+  return bad;
+}
+
+// Mode B (general sorted batches): key-tile owner, static strided schedule.
+template <typename VT, bool VEC, int U, bool NT>
+__global__ __launch_bounds__(kBlock) void k_assign_group(GroupArgs ga, DenseView d,
                                                          uint32_t tile_shift, uint64_t ntiles,
                                                          uint32_t* flag, uint32_t epoch) {
   __shared__ uint64_t s_seg_s[kMaxBatches];
   __shared__ uint64_t s_seg_e[kMaxBatches];
+  __shared__ uint32_t s_first[kMaxBatches];
+  __shared__ uint32_t s_last[kMaxBatches];
   __shared__ unsigned long long s_mask;
+  __shared__ int s_dense;
   const int tid = threadIdx.x;
-  // Wave 0, lane j keeps batch j's endpoints for the whole launch.
+  const int jb = tid & 63;
+  // Lanes of waves 0 and 1 keep batch jb's endpoints for the whole launch.
   uint32_t first = 0, last = 0;
   uint64_t n = 0;
   bool ok = false;
   const uint32_t* keys = nullptr;
-  if (tid < ga.nb) {
-    keys = ga.b[tid].keys;
-    n = ga.b[tid].n;
+  if (tid < 128 && jb < ga.nb) {
+    keys = ga.b[jb].keys;
+    n = ga.b[jb].n;
     if (n > 0) {
       first = keys[0];
       last = keys[n - 1];
-      const uint64_t fo = (uint32_t)(first - d.key_begin);
-      const uint64_t lo_ = (uint32_t)(last - d.key_begin);
-      ok = fo < d.range && lo_ < d.range && first <= last;
-      if (!ok && blockIdx.x == 0) *flag = epoch;  // out-of-range or inverted endpoints
+      const uint64_t fo0 = (uint32_t)(first - d.key_begin);
+      const uint64_t lo0 = (uint32_t)(last - d.key_begin);
+      ok = fo0 < d.range && lo0 < d.range && first <= last;
+      if (!ok && blockIdx.x == 0 && tid < 64) *flag = epoch;  // out-of-range or inverted endpoints
     }
   }
+  if (tid < 64) {
+    const bool dense_j = jb >= ga.nb || (ok && (uint64_t)(last - first) == n - 1);
+    if (jb < kMaxBatches) {
+      s_first[jb] = first;
+      s_last[jb] = last;
+    }
+    const unsigned long long m = __ballot(!dense_j);
+    if (tid == 0) s_dense = m == 0;
+  }
+  __syncthreads();
   bool bad = false;
+  if (s_dense) {
+    const uint32_t nchunks = ga.wg_prefix[ga.nb];
+    for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x)
+      bad |= dense_chunk<VT, VEC, U, NT>(ga, d, c, s_first, s_last);
+    if (bad) *flag = epoch;
+    return;
+  }
+  const uint64_t fo = (uint32_t)(first - d.key_begin);
+  const uint64_t lo_ = (uint32_t)(last - d.key_begin);
   for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const uint64_t tlo = t << tile_shift;
     const uint64_t tend = tlo + (1ull << tile_shift);
     const uint64_t thi = tend < d.range ? tend : d.range;
-    __syncthreads();  // previous tile's readers of s_mask / s_seg_* are done
+    const bool ov = ok && fo < thi && lo_ >= tlo;
+    // wave 0 searches segment starts, wave 1 segment ends, concurrently
     if (tid < 64) {
-      bool act = false;
-      uint64_t s = 0, e = 0;
-      if (ok) {
-        const uint64_t fo = (uint32_t)(first - d.key_begin);
-        const uint64_t lo_ = (uint32_t)(last - d.key_begin);
-        if (fo < thi && lo_ >= tlo) {
-          s = fo >= tlo ? 0 : lower_bound_interp(keys, n, d.key_begin + (uint32_t)tlo, first, last);
-          e = lo_ < thi ? n : lower_bound_interp(keys, n, d.key_begin + (uint32_t)thi, first, last);
-          if (s > e)
-            bad = true;
-          else
-            act = s < e;
-        }
-      }
-      if (tid < kMaxBatches) {
-        s_seg_s[tid] = s;
-        s_seg_e[tid] = e;
-      }
-      const unsigned long long m = __ballot(act);
+      if (jb < kMaxBatches)
+        s_seg_s[jb] = !ov ? 0 : (fo >= tlo ? 0 : lower_bound_interp(keys, n, d.key_begin + (uint32_t)tlo, first, last));
+    } else if (tid < 128) {
+      s_seg_e[jb] = !ov ? 0 : (lo_ < thi ? n : lower_bound_interp(keys, n, d.key_begin + (uint32_t)thi, first, last));
+    }
+    __syncthreads();
+    if (tid < 64) {
+      const uint64_t s = s_seg_s[jb], e = s_seg_e[jb];
+      if (ov && s > e) bad = true;
+      const unsigned long long m = __ballot(ov && s < e);
       if (tid == 0) s_mask = m;
     }
     __syncthreads();
@@ -427,55 +536,59 @@ __global__ __launch_bounds__(kBlock) void k_general_mark(GroupArgs ga, DenseView
   __shared__ uint32_t hk[kGeneralSlots];
   __shared__ uint32_t hidx[MODE == 0 ? kGeneralSlots : 1];
   __shared__ AT hsum[MODE == 1 ? kGeneralSlots : 1];
-  const uint32_t wg = blockIdx.x;
-  const int j = batch_of(ga, wg);
-  const uint32_t* __restrict__ keys = ga.b[j].keys;
-  const AT* __restrict__ vals = reinterpret_cast<const AT*>(ga.b[j].vals);
-  const uint64_t n = ga.b[j].n;
-  const uint64_t base = (uint64_t)(wg - ga.wg_prefix[j]) * kGeneralChunk;
-  const uint64_t gbase = ga.elem_prefix[j] + base;
   const int tid = threadIdx.x;
-  for (int s = tid; s < kGeneralSlots; s += kBlock) {
-    hk[s] = kEmpty32;
-    if (MODE == 0)
-      hidx[s] = 0;
-    else
-      hsum[s] = AT(0);
-  }
-  __syncthreads();
+  const uint32_t nvwg = ga.wg_prefix[ga.nb];
+  // grid-stride over virtual workgroups (one 2048-key chunk each)
+  for (uint32_t wg = blockIdx.x; wg < nvwg; wg += gridDim.x) {
+    const int j = batch_of(ga, wg);
+    const uint32_t* __restrict__ keys = ga.b[j].keys;
+    const AT* __restrict__ vals = reinterpret_cast<const AT*>(ga.b[j].vals);
+    const uint64_t n = ga.b[j].n;
+    const uint64_t base = (uint64_t)(wg - ga.wg_prefix[j]) * kGeneralChunk;
+    const uint64_t gbase = ga.elem_prefix[j] + base;
+    for (int s = tid; s < kGeneralSlots; s += kBlock) {
+      hk[s] = kEmpty32;
+      if (MODE == 0)
+        hidx[s] = 0;
+      else
+        hsum[s] = AT(0);
+    }
+    __syncthreads();
 #pragma unroll 2
-  for (int r = 0; r < kGeneralChunk / kBlock; ++r) {
-    const int li = r * kBlock + tid;
-    const uint64_t i = base + li;
-    if (i < n) {
-      const uint32_t k = keys[i];
-      if (k == kEmpty32) {  // the LDS sentinel itself: bypass the LDS table
-        if (MODE == 0)
-          global_stamp(d, o, owner, k, ((unsigned long long)epoch << 32) | (gbase + li));
-        else
-          global_accumulate<AT>(d, o, k, vals[i]);
-      } else {
-        uint32_t h = fmix32(k) & (kGeneralSlots - 1);
-        for (;;) {
-          const uint32_t old = atomicCAS(&hk[h], kEmpty32, k);
-          if (old == kEmpty32 || old == k) break;
-          h = (h + 1) & (kGeneralSlots - 1);
+    for (int r = 0; r < kGeneralChunk / kBlock; ++r) {
+      const int li = r * kBlock + tid;
+      const uint64_t i = base + li;
+      if (i < n) {
+        const uint32_t k = keys[i];
+        if (k == kEmpty32) {  // the LDS sentinel itself: bypass the LDS table
+          if (MODE == 0)
+            global_stamp(d, o, owner, k, ((unsigned long long)epoch << 32) | (gbase + li));
+          else
+            global_accumulate<AT>(d, o, k, vals[i]);
+        } else {
+          uint32_t h = fmix32(k) & (kGeneralSlots - 1);
+          for (;;) {
+            const uint32_t old = atomicCAS(&hk[h], kEmpty32, k);
+            if (old == kEmpty32 || old == k) break;
+            h = (h + 1) & (kGeneralSlots - 1);
+          }
+          if (MODE == 0)
+            atomicMax(&hidx[h], (uint32_t)li);
+          else
+            atomicAdd(&hsum[h], vals[i]);
         }
-        if (MODE == 0)
-          atomicMax(&hidx[h], (uint32_t)li);
-        else
-          atomicAdd(&hsum[h], vals[i]);
       }
     }
-  }
-  __syncthreads();
-  for (int s = tid; s < kGeneralSlots; s += kBlock) {
-    const uint32_t k = hk[s];
-    if (k == kEmpty32) continue;
-    if (MODE == 0)
-      global_stamp(d, o, owner, k, ((unsigned long long)epoch << 32) | (gbase + hidx[s]));
-    else
-      global_accumulate<AT>(d, o, k, hsum[s]);
+    __syncthreads();
+    for (int s = tid; s < kGeneralSlots; s += kBlock) {
+      const uint32_t k = hk[s];
+      if (k == kEmpty32) continue;
+      if (MODE == 0)
+        global_stamp(d, o, owner, k, ((unsigned long long)epoch << 32) | (gbase + hidx[s]));
+      else
+        global_accumulate<AT>(d, o, k, hsum[s]);
+    }
+    __syncthreads();  // the table is re-initialised for the next chunk
   }
 }
 
@@ -484,27 +597,29 @@ __global__ __launch_bounds__(kBlock) void k_general_commit(GroupArgs ga, DenseVi
                                                            const unsigned long long* owner,
                                                            const uint32_t* cond, uint32_t epoch) {
   if (cond != nullptr && *cond != epoch) return;
-  const uint32_t wg = blockIdx.x;
-  const int j = batch_of(ga, wg);
-  const uint32_t* __restrict__ keys = ga.b[j].keys;
-  const VT* __restrict__ vals = reinterpret_cast<const VT*>(ga.b[j].vals);
-  const uint64_t n = ga.b[j].n;
-  const uint64_t base = (uint64_t)(wg - ga.wg_prefix[j]) * kGeneralChunk;
-  const uint64_t gbase = ga.elem_prefix[j] + base;
   const int tid = threadIdx.x;
+  const uint32_t nvwg = ga.wg_prefix[ga.nb];
+  for (uint32_t wg = blockIdx.x; wg < nvwg; wg += gridDim.x) {
+    const int j = batch_of(ga, wg);
+    const uint32_t* __restrict__ keys = ga.b[j].keys;
+    const VT* __restrict__ vals = reinterpret_cast<const VT*>(ga.b[j].vals);
+    const uint64_t n = ga.b[j].n;
+    const uint64_t base = (uint64_t)(wg - ga.wg_prefix[j]) * kGeneralChunk;
+    const uint64_t gbase = ga.elem_prefix[j] + base;
 #pragma unroll 2
-  for (int r = 0; r < kGeneralChunk / kBlock; ++r) {
-    const int li = r * kBlock + tid;
-    const uint64_t i = base + li;
-    if (i >= n) break;
-    const uint32_t k = keys[i];
-    const unsigned long long tag = ((unsigned long long)epoch << 32) | (gbase + li);
-    const uint32_t off = k - d.key_begin;
-    if ((uint64_t)off < d.range) {
-      if (owner[off] == tag) reinterpret_cast<VT*>(d.param)[off] = vals[i];
-    } else {
-      const long long s = ovf_find(o, k);
-      if (s >= 0 && o.owner[s] == tag) reinterpret_cast<VT*>(o.vals)[s] = vals[i];
+    for (int r = 0; r < kGeneralChunk / kBlock; ++r) {
+      const int li = r * kBlock + tid;
+      const uint64_t i = base + li;
+      if (i >= n) break;
+      const uint32_t k = keys[i];
+      const unsigned long long tag = ((unsigned long long)epoch << 32) | (gbase + li);
+      const uint32_t off = k - d.key_begin;
+      if ((uint64_t)off < d.range) {
+        if (owner[off] == tag) reinterpret_cast<VT*>(d.param)[off] = vals[i];
+      } else {
+        const long long s = ovf_find(o, k);
+        if (s >= 0 && o.owner[s] == tag) reinterpret_cast<VT*>(o.vals)[s] = vals[i];
+      }
     }
   }
 }
@@ -524,19 +639,35 @@ __global__ __launch_bounds__(kBlock) void k_ovf_rehash(Ovf from, uint64_t from_c
 
 // ------------------------------------------------------- launch wrappers
 
-hipError_t launch_gather(int vb, bool vec, const GroupArgs& ga, uint32_t nwg, const DenseView& d,
-                         const Ovf& o, hipStream_t st) {
+template <typename VT, bool VEC>
+static void gather_dispatch(int unroll, bool nt, uint32_t nwg, const GroupArgs& ga,
+                            const DenseView& d, const Ovf& o, hipStream_t st) {
+  if (unroll == 8) {
+    if (nt)
+      k_gather<VT, VEC, 8, true><<<nwg, kBlock, 0, st>>>(ga, d, o);
+    else
+      k_gather<VT, VEC, 8, false><<<nwg, kBlock, 0, st>>>(ga, d, o);
+  } else {
+    if (nt)
+      k_gather<VT, VEC, 4, true><<<nwg, kBlock, 0, st>>>(ga, d, o);
+    else
+      k_gather<VT, VEC, 4, false><<<nwg, kBlock, 0, st>>>(ga, d, o);
+  }
+}
+
+hipError_t launch_gather(int vb, bool vec, int unroll, bool nt, const GroupArgs& ga, uint32_t nwg,
+                         const DenseView& d, const Ovf& o, hipStream_t st) {
   if (nwg == 0) return hipSuccess;
   if (vb == 4) {
     if (vec)
-      k_gather<uint32_t, true><<<nwg, kBlock, 0, st>>>(ga, d, o);
+      gather_dispatch<uint32_t, true>(unroll, nt, nwg, ga, d, o, st);
     else
-      k_gather<uint32_t, false><<<nwg, kBlock, 0, st>>>(ga, d, o);
+      gather_dispatch<uint32_t, false>(unroll, nt, nwg, ga, d, o, st);
   } else {
     if (vec)
-      k_gather<unsigned long long, true><<<nwg, kBlock, 0, st>>>(ga, d, o);
+      gather_dispatch<unsigned long long, true>(unroll, nt, nwg, ga, d, o, st);
     else
-      k_gather<unsigned long long, false><<<nwg, kBlock, 0, st>>>(ga, d, o);
+      gather_dispatch<unsigned long long, false>(unroll, nt, nwg, ga, d, o, st);
   }
   return hipGetLastError();
 }
@@ -562,30 +693,56 @@ hipError_t launch_assign_sorted(int vb, bool vec, const uint32_t* keys, const vo
   return hipGetLastError();
 }
 
-hipError_t launch_assign_tiles(int vb, bool vec, const GroupArgs& ga, const DenseView& d,
-                               uint32_t tile_shift, uint64_t ntiles, uint32_t grid,
-                               uint32_t* flag, uint32_t epoch, hipStream_t st) {
-  if (ntiles == 0 || grid == 0) return hipSuccess;
+template <typename VT, bool VEC>
+static void group_dispatch(int unroll, bool nt, uint32_t grid, const GroupArgs& ga,
+                           const DenseView& d, uint32_t shift, uint64_t ntiles, uint32_t* flag,
+                           uint32_t epoch, hipStream_t st) {
+  if (unroll == 8) {
+    if (nt)
+      k_assign_group<VT, VEC, 8, true><<<grid, kBlock, 0, st>>>(ga, d, shift, ntiles, flag, epoch);
+    else
+      k_assign_group<VT, VEC, 8, false><<<grid, kBlock, 0, st>>>(ga, d, shift, ntiles, flag, epoch);
+  } else {
+    if (nt)
+      k_assign_group<VT, VEC, 4, true><<<grid, kBlock, 0, st>>>(ga, d, shift, ntiles, flag, epoch);
+    else
+      k_assign_group<VT, VEC, 4, false><<<grid, kBlock, 0, st>>>(ga, d, shift, ntiles, flag, epoch);
+  }
+}
+
+hipError_t launch_assign_group(int vb, bool vec, int unroll, bool nt, const GroupArgs& ga,
+                               const DenseView& d, uint32_t tile_shift, uint64_t ntiles,
+                               uint32_t grid, uint32_t* flag, uint32_t epoch, hipStream_t st) {
+  if (grid == 0) return hipSuccess;
   if (vb == 4) {
     if (vec)
-      k_assign_tiles<uint32_t, true><<<grid, kBlock, 0, st>>>(ga, d, tile_shift, ntiles, flag, epoch);
+      group_dispatch<uint32_t, true>(unroll, nt, grid, ga, d, tile_shift, ntiles, flag, epoch, st);
     else
-      k_assign_tiles<uint32_t, false><<<grid, kBlock, 0, st>>>(ga, d, tile_shift, ntiles, flag, epoch);
+      group_dispatch<uint32_t, false>(unroll, nt, grid, ga, d, tile_shift, ntiles, flag, epoch, st);
   } else {
     if (vec)
-      k_assign_tiles<unsigned long long, true><<<grid, kBlock, 0, st>>>(ga, d, tile_shift, ntiles,
-                                                                       flag, epoch);
+      group_dispatch<unsigned long long, true>(unroll, nt, grid, ga, d, tile_shift, ntiles, flag,
+                                               epoch, st);
     else
-      k_assign_tiles<unsigned long long, false><<<grid, kBlock, 0, st>>>(ga, d, tile_shift, ntiles,
-                                                                        flag, epoch);
+      group_dispatch<unsigned long long, false>(unroll, nt, grid, ga, d, tile_shift, ntiles, flag,
+                                                epoch, st);
   }
   return hipGetLastError();
+}
+
+// Grid of a general-path launch: a conditional (repair) launch usually exits at
+// once, so it gets few workgroups; otherwise enough to fill 256 CUs several
+// times over, each looping over 2048-key chunks.
+static uint32_t general_grid(uint32_t nwg, const uint32_t* cond) {
+  const uint32_t cap = cond ? 256u : 4096u;
+  return nwg < cap ? nwg : cap;
 }
 
 hipError_t launch_general_mark(int dtype, int mode, const GroupArgs& ga, uint32_t nwg,
                                const DenseView& d, const Ovf& o, unsigned long long* owner,
                                const uint32_t* cond, uint32_t epoch, hipStream_t st) {
   if (nwg == 0) return hipSuccess;
+  nwg = general_grid(nwg, cond);
   if (mode == 0) {
     // assign: value bits are never read here; the AT parameter only sizes unused LDS
     k_general_mark<uint32_t, 0><<<nwg, kBlock, 0, st>>>(ga, d, o, owner, cond, epoch);
@@ -603,6 +760,7 @@ hipError_t launch_general_commit(int vb, const GroupArgs& ga, uint32_t nwg, cons
                                  const Ovf& o, const unsigned long long* owner,
                                  const uint32_t* cond, uint32_t epoch, hipStream_t st) {
   if (nwg == 0) return hipSuccess;
+  nwg = general_grid(nwg, cond);
   if (vb == 4)
     k_general_commit<uint32_t><<<nwg, kBlock, 0, st>>>(ga, d, o, owner, cond, epoch);
   else

@@ -118,19 +118,23 @@ class Shard:
         check(lib.pskv_get(self._h, k.ctypes.data, k.size, res.ctypes.data, _lib.PSKV_HOST))
         return res
 
+    def prepare(self, batches, is_get: bool = False) -> "BatchSet":
+        """Validate and pack a batch list once, for repeated grouped calls."""
+        arr, keep, flags = self._batch_array(batches, is_get=is_get)
+        return BatchSet(arr, len(batches), flags, keep)
+
     def add_grouped(self, batches, sorted_hint: bool = False):
-        """batches: list of (keys, vals); all torch-device or all numpy-host."""
-        arr, keep, flags = self._batch_array(batches, is_get=False)
+        """batches: list of (keys, vals) (all torch-device or all numpy-host) or a BatchSet."""
+        bs = batches if isinstance(batches, BatchSet) else self.prepare(batches)
+        flags = bs.flags
         if sorted_hint and flags & _lib.PSKV_DEVICE:
             flags |= _lib.PSKV_SORTED_HINT
-        check(lib.pskv_add_grouped(self._h, arr, len(batches), flags))
-        del keep
+        check(lib.pskv_add_grouped(self._h, bs.arr, bs.n, flags))
 
     def get_grouped(self, batches):
-        """batches: list of (keys, out) pairs; out is filled in place."""
-        arr, keep, flags = self._batch_array(batches, is_get=True)
-        check(lib.pskv_get_grouped(self._h, arr, len(batches), flags))
-        del keep
+        """batches: list of (keys, out) pairs (out filled in place) or a BatchSet."""
+        bs = batches if isinstance(batches, BatchSet) else self.prepare(batches, is_get=True)
+        check(lib.pskv_get_grouped(self._h, bs.arr, bs.n, bs.flags))
 
     def _batch_array(self, batches, is_get):
         arr = (_lib.PskvBatch * max(1, len(batches)))()
@@ -146,6 +150,7 @@ class Shard:
                 self._check_dev(k, v)
                 if v.numel() != k.numel():
                     raise ValueError("CHECK_EQ(keys.size(), vals.size()) failed")
+                keep += [k, v]
                 arr[i] = _lib.PskvBatch(k.data_ptr(), v.data_ptr(), k.numel())
             else:
                 kk = self._host_keys(k)
@@ -183,8 +188,15 @@ class Shard:
         check(lib.pskv_shard_info(self._h, ctypes.byref(i)))
         return {f: getattr(i, f) for f, _ in _lib.PskvInfo._fields_}
 
-    def set_timing(self, on: bool):
-        check(lib.pskv_set_timing(self._h, 1 if on else 0))
+    def set_timing(self, on, kernels=None):
+        """on: bool; kernels: optional list of kernel ids (_lib.PSKV_K_*) to time."""
+        if kernels is None:
+            check(lib.pskv_set_timing(self._h, 1 if on else 0))
+        else:
+            mask = 0
+            for k in kernels:
+                mask |= 1 << k
+            check(lib.pskv_set_timing_mask(self._h, mask if on else 0))
 
     def reset_timing(self):
         check(lib.pskv_reset_timing(self._h))
@@ -201,6 +213,13 @@ class Shard:
         n = self.key_end - self.key_begin
         ptr = self.dense_ptr()
         return _tensor_from_ptr(ptr, n, _torch_dtype(self.dtype), self.device)
+
+
+class BatchSet:
+    """A packed pskv_batch array (plus references keeping its buffers alive)."""
+
+    def __init__(self, arr, n, flags, keep):
+        self.arr, self.n, self.flags, self._keep = arr, n, flags, keep
 
 
 def _torch_dtype(npdt):

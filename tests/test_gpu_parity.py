@@ -377,3 +377,53 @@ def test_external_stream_and_timing(cuda):
         t = sh.kernel_time(_lib.PSKV_K_GATHER)
         assert t["launches"] == 1 and t["total_ms"] > 0 and t["elements"] == 1 << 22
         sh.set_stream(None)
+
+
+@pytest.mark.parametrize("nb", [2, 9, 64, 65])
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_grouped_dense_windows_mode(cuda, oracle_mod, nb, dtype):
+    """All batches contiguous windows (dense mode of the grouped sorted Add):
+    unaligned bases, overlaps, ragged lengths; later batches win."""
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(100 + nb)
+    size = 300_000
+    dense = np.zeros(size, dtype)
+    batches = []
+    for j in range(nb):
+        n = int(rng.integers(1, 50_000))
+        b = int(rng.integers(0, size - n))
+        k = np.arange(b, b + n, dtype=np.uint32)
+        v = rng.standard_normal(n).astype(dtype)
+        batches.append((k, v))
+        oracle_mod.dense_last_wins(dense, 0, k, v)
+    with ps.Shard(0, size, dtype) as sh:
+        before = sh.info()["n_general_launches"]
+        sh.add_grouped([(tdev(k, cuda), tdev(v, cuda)) for k, v in batches], sorted_hint=True)
+        got = sh.get(np.arange(size, dtype=np.uint32))
+    assert_bits_equal(got, dense, f"dense windows nb={nb}")
+
+
+def test_grouped_dense_lookalike_is_repaired(cuda, oracle_mod):
+    """Endpoints say 'dense window' but the keys are not contiguous (two swapped,
+    one duplicated): the per-element check must tag the group for repair."""
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(8)
+    size = 100_000
+    dense = np.zeros(size, np.float32)
+    batches = []
+    for j in range(6):
+        b = int(rng.integers(0, size - 20_000))
+        k = np.arange(b, b + 20_000, dtype=np.uint32)
+        if j == 2:
+            k[100], k[200] = k[200], k[100]      # unsorted, same endpoints
+        if j == 4:
+            k[5000] = k[5001]                    # duplicate, same endpoints
+        v = rng.standard_normal(k.size).astype(np.float32)
+        batches.append((k, v))
+        oracle_mod.dense_last_wins(dense, 0, k, v)
+    with ps.Shard(0, size, np.float32) as sh:
+        sh.add_grouped([(tdev(k, cuda), tdev(v, cuda)) for k, v in batches], sorted_hint=True)
+        got = sh.get(np.arange(size, dtype=np.uint32))
+    assert_bits_equal(got, dense, "lookalike")

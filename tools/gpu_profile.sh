@@ -1,0 +1,20 @@
+#!/bin/bash
+# Profile bench.py on the GPU box: kernel trace + stats, then two separate PMC
+# passes (FETCH_SIZE, WRITE_SIZE) summarised by tools/collect_pmc.py.
+# Every GPU step has its own time limit; the script stops at the first failure.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$PWD}
+export TMPDIR=/tmp
+OUT=$R/gpurun_out/${1:-prof}
+shift || true
+mkdir -p "$OUT"
+ARGS="--steps 10 --warmup 2 --no-cpu-baseline --no-extra $*"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT" -o trace -- \
+  python3 "$R/bench.py" $ARGS > "$OUT/trace.log" 2>&1 || exit 1
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT" -o fetch -- \
+  python3 "$R/bench.py" $ARGS > "$OUT/fetch.log" 2>&1 || exit 2
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT" -o write -- \
+  python3 "$R/bench.py" $ARGS > "$OUT/write.log" 2>&1 || exit 3
+python3 "$R/tools/collect_pmc.py" "$OUT/fetch_counter_collection.csv" \
+  "$OUT/write_counter_collection.csv" "$OUT/pmc.json" > /dev/null || exit 4
+echo "profile done: $OUT"
