@@ -103,9 +103,9 @@ def sum_over_ranks(x, world, dev):
     return float(t.item())
 
 
-def make_workload(rank, world, J, B, dev):
-    import torch
-
+def plan_rank(rank, world, J, B):
+    """Key range and push-window bases of one rank (pure host logic; tested with
+    gloo in tests/test_dist.py).  N = 1: cfg 2.  N > 1: cfg 4 weak scaling."""
     from parameter_server_amd import workload
 
     if world == 1:
@@ -121,6 +121,13 @@ def make_workload(rank, world, J, B, dev):
         # every window of this rank's producers is routed to this rank, whole
         assert all(len(routed[r]) == 0 for r in range(world) if r != rank)
         assert len(routed[rank]) == J and all(n == B for _, _, n in routed[rank])
+    return key_space, lo, hi, bases
+
+
+def make_workload(rank, world, J, B, dev):
+    import torch
+
+    key_space, lo, hi, bases = plan_rank(rank, world, J, B)
     batches = []
     for j, b in enumerate(bases):
         keys = torch.arange(int(b), int(b) + B, dtype=torch.int64, device=dev).to(torch.int32)
