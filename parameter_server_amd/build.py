@@ -18,9 +18,11 @@ ARCH = "gfx950"
 
 LIB_SOURCES = ["pskv_kernels.hip", "pskv_shard.cpp"]
 LIB_OUT = os.path.join(PKG, "libpskv.so")
-CPP_TESTS = {  # program -> source (tests/cpp)
-    "hip_storage_test": "hip_storage_test.cpp",
+CPP_TESTS = {  # program -> (source in tests/cpp, links the oracle checker)
+    "hip_storage_test": ("hip_storage_test.cpp", False),
+    "ssp_replay": ("ssp_replay.cpp", True),
 }
+ORACLE_DIR = os.path.join(ROOT, "oracle")
 BIN_DIR = os.path.join(PKG, "bin")
 
 
@@ -51,13 +53,18 @@ def build_cpp_tests(force=False):
     os.makedirs(BIN_DIR, exist_ok=True)
     outs = []
     hdrs = [os.path.join(INCLUDE, "ps", h) for h in os.listdir(os.path.join(INCLUDE, "ps"))]
-    for prog, src in CPP_TESTS.items():
+    for prog, (src, with_oracle) in CPP_TESTS.items():
         s = os.path.join(ROOT, "tests", "cpp", src)
         out = os.path.join(BIN_DIR, prog)
-        if force or _stale(out, [s, LIB_OUT] + hdrs):
+        deps = [s, LIB_OUT] + hdrs
+        extra = []
+        if with_oracle:  # test programs only: the checker is linked beside the product
+            deps.append(os.path.join(ORACLE_DIR, "liboracle.so"))
+            extra = ["-L", ORACLE_DIR, "-loracle", "-Wl,-rpath,$ORIGIN/../../oracle"]
+        if force or _stale(out, deps):
             # host-only C++ against the C ABI: the program never sees HIP types
             _run(["g++", "-O2", "-std=c++11", "-pthread", "-I", INCLUDE, s, "-o", out,
-                  "-L", PKG, "-lpskv", f"-Wl,-rpath,{PKG}", "-Wl,-rpath,$ORIGIN/.."])
+                  "-L", PKG, "-lpskv", "-Wl,-rpath,$ORIGIN/..", *extra])
         outs.append(out)
     return outs
 
@@ -74,8 +81,8 @@ def build_oracle():
 
 def build_all(force=False):
     lib = build_lib(force)
-    progs = build_cpp_tests(force)
     orc = build_oracle()
+    progs = build_cpp_tests(force)
     return {"lib": lib, "cpp": progs, "oracle": orc}
 
 

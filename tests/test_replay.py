@@ -1,0 +1,38 @@
+"""BASELINE config 5 / SURVEY §8f-1: LR-pattern trace through the consistency
+models (include/ps/consistency.hpp) over 8 range shards; every Get reply and
+the final shard contents must be bit-identical between the CPU oracle storage
+and HipStorage<double> (tests/cpp/ssp_replay.cpp)."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "parameter_server_amd", "bin", "ssp_replay")
+
+
+def run(*args):
+    if not os.path.exists(EXE):
+        import __graft_entry__ as g
+
+        g.build()
+    r = subprocess.run(["timeout", "-k", "10", "600", EXE, *args], capture_output=True, text=True)
+    return r.returncode, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("model", ["ssp", "bsp", "asp"])
+def test_replay_cpu_deterministic_and_model_known_answers(model):
+    rc, out = run("--cpu-only", "--known-answers", "--model", model, "--iters", "6")
+    assert rc == 0, out
+    assert "REPLAY OK" in out and "[oracle] model known answers: ok" in out
+    if model == "ssp":
+        assert "ssp_releases=0 " not in out  # the straggler pattern really exercises staleness
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model,staleness", [("ssp", 3), ("ssp", 0), ("bsp", 0), ("asp", 0)])
+def test_replay_hip_vs_cpu(model, staleness):
+    rc, out = run("--known-answers", "--model", model, "--staleness", str(staleness), "--iters", "8",
+                  "--shards", "8", "--workers", "4")
+    assert rc == 0, out
+    assert "REPLAY OK (bit-exact)" in out and "[hip] model known answers: ok" in out
