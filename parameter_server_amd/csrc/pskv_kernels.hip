@@ -533,9 +533,11 @@ __global__ __launch_bounds__(kBlock) void k_general_mark(GroupArgs ga, DenseView
                                                          unsigned long long* owner,
                                                          const uint32_t* cond, uint32_t epoch) {
   if (cond != nullptr && *cond != epoch) return;  // repair launch, sorted path was right
-  __shared__ uint32_t hk[kGeneralSlots];
-  __shared__ uint32_t hidx[MODE == 0 ? kGeneralSlots : 1];
-  __shared__ AT hsum[MODE == 1 ? kGeneralSlots : 1];
+  constexpr int R = kGeneralChunk / kBlock;        // elements per lane per chunk
+  __shared__ uint32_t hk[kGeneralSlots];           // key (EMPTY = 0xFFFFFFFF)
+  __shared__ uint32_t hfirst[kGeneralSlots];       // first chunk index of the key
+  __shared__ uint32_t hidx[MODE == 0 ? kGeneralSlots : 1];  // assign: last chunk index
+  __shared__ AT hsum[MODE == 1 ? kGeneralSlots : 1];        // accumulate: chunk sum
   const int tid = threadIdx.x;
   const uint32_t nvwg = ga.wg_prefix[ga.nb];
   // grid-stride over virtual workgroups (one 2048-key chunk each)
@@ -548,18 +550,24 @@ __global__ __launch_bounds__(kBlock) void k_general_mark(GroupArgs ga, DenseView
     const uint64_t gbase = ga.elem_prefix[j] + base;
     for (int s = tid; s < kGeneralSlots; s += kBlock) {
       hk[s] = kEmpty32;
+      hfirst[s] = kEmpty32;
       if (MODE == 0)
         hidx[s] = 0;
       else
         hsum[s] = AT(0);
     }
     __syncthreads();
-#pragma unroll 2
-    for (int r = 0; r < kGeneralChunk / kBlock; ++r) {
+    uint32_t slot[R];
+    uint32_t key[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
       const int li = r * kBlock + tid;
       const uint64_t i = base + li;
+      slot[r] = kEmpty32;
+      key[r] = 0;
       if (i < n) {
         const uint32_t k = keys[i];
+        key[r] = k;
         if (k == kEmpty32) {  // the LDS sentinel itself: bypass the LDS table
           if (MODE == 0)
             global_stamp(d, o, owner, k, ((unsigned long long)epoch << 32) | (gbase + li));
@@ -572,6 +580,8 @@ __global__ __launch_bounds__(kBlock) void k_general_mark(GroupArgs ga, DenseView
             if (old == kEmpty32 || old == k) break;
             h = (h + 1) & (kGeneralSlots - 1);
           }
+          slot[r] = h;
+          atomicMin(&hfirst[h], (uint32_t)li);
           if (MODE == 0)
             atomicMax(&hidx[h], (uint32_t)li);
           else
@@ -580,13 +590,17 @@ __global__ __launch_bounds__(kBlock) void k_general_mark(GroupArgs ga, DenseView
       }
     }
     __syncthreads();
-    for (int s = tid; s < kGeneralSlots; s += kBlock) {
-      const uint32_t k = hk[s];
-      if (k == kEmpty32) continue;
+    // One global operation per distinct key, issued by the key's FIRST
+    // occurrence in element order: for sorted or dense chunks consecutive lanes
+    // then hit consecutive addresses, so the atomics coalesce.
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t h = slot[r];
+      if (h == kEmpty32 || hfirst[h] != (uint32_t)(r * kBlock + tid)) continue;
       if (MODE == 0)
-        global_stamp(d, o, owner, k, ((unsigned long long)epoch << 32) | (gbase + hidx[s]));
+        global_stamp(d, o, owner, key[r], ((unsigned long long)epoch << 32) | (gbase + hidx[h]));
       else
-        global_accumulate<AT>(d, o, k, hsum[s]);
+        global_accumulate<AT>(d, o, key[r], hsum[h]);
     }
     __syncthreads();  // the table is re-initialised for the next chunk
   }
