@@ -238,7 +238,7 @@ def side_measurements(dev, B):
         sh.set_stream(None)
     add_b, get_b = step_bytes(J * B, u_all, J * B)
     out["zipf"] = {"workload": "cfg 3: Zipf(0.99) over 1e8 keys, 8 x 1M unsorted pushes then pulls, assign "
-                               "(general path: LDS dedup + stamps)",
+                               "(general path K5: LDS dedup + radix buckets)",
                    "GB/s": (add_b + get_b) * reps / dt / 1e9, "ms_per_step": dt / reps * 1e3,
                    "unique_keys_per_batch": uniq, "distinct_keys_per_step": u_all}
     del zb, zo

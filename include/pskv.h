@@ -112,7 +112,8 @@ enum pskv_kernel {
   PSKV_K_ASSIGN_TILES = 2,  /* K2g: grouped sorted scatter, key-tile owner */
   PSKV_K_GENERAL_MARK = 3,  /* K4a: chunk dedup + stamps / accumulate */
   PSKV_K_GENERAL_COMMIT = 4,/* K4b: winner write */
-  PSKV_K_COUNT = 5
+  PSKV_K_RADIX = 5,         /* K5a-d: radix-bucket general Add (timed as one operation) */
+  PSKV_K_COUNT = 6
 };
 
 /* Create a shard owning keys [key_begin, key_end) on `device`.  The dense

@@ -29,13 +29,15 @@ PSKV_K_ASSIGN_SORTED = 1
 PSKV_K_ASSIGN_TILES = 2
 PSKV_K_GENERAL_MARK = 3
 PSKV_K_GENERAL_COMMIT = 4
-PSKV_K_COUNT = 5
+PSKV_K_RADIX = 5
+PSKV_K_COUNT = 6
 KERNEL_NAMES = {
     PSKV_K_GATHER: "k_gather",
     PSKV_K_ASSIGN_SORTED: "k_assign_sorted",
     PSKV_K_ASSIGN_TILES: "k_assign_tiles",
     PSKV_K_GENERAL_MARK: "k_general_mark",
     PSKV_K_GENERAL_COMMIT: "k_general_commit",
+    PSKV_K_RADIX: "k_radix_bucket",
 }
 
 # Every symbol include/pskv.h declares (checked by tests/test_abi.py).

@@ -649,6 +649,377 @@ __global__ __launch_bounds__(kBlock) void k_ovf_rehash(Ovf from, uint64_t from_c
   }
 }
 
+// ------------------------------------------- K5 radix-bucket general path
+// The general (any order) Add without random global atomics.  K4's stamps cost
+// one random agent-scope atomic per distinct key per chunk, and those run at
+// ~20 G/s chip-wide (memory-side atomics, MI355X_MICROARCH.md "Global float
+// atomics": 64 lanes in 64 rows ≈ 17x slower).  K5 instead moves the data to
+// where it can be resolved locally:
+//   K5a k_rb_count    per 4096-key chunk: LDS hash dedup (key -> last index /
+//                     sum), histogram of the distinct keys by key bucket
+//                     (bucket = key offset >> bshift; one extra bucket for
+//                     out-of-range keys) -> cnt[bucket][chunk]
+//   K5b k_rb_scan     one workgroup per bucket: exclusive scan of its row
+//   K5c k_rb_scatter  the same dedup again, each distinct key written as a
+//                     16-byte entry {key, group index, value} to its bucket
+//   K5d k_rb_apply    one workgroup per bucket: an LDS hash resolves the
+//                     bucket's entries (max group index = last write / sum),
+//                     then the winners store (assign) or add (accumulate) into
+//                     the dense array or the overflow table.  A bucket is owned
+//                     by one workgroup, so no cross-workgroup ordering exists.
+// Per-chunk dedup first matters for skew: a Zipf-hot key contributes one
+// entry per chunk, not one per occurrence, so no bucket explodes.
+
+struct RbEntry {
+  uint32_t key;
+  uint32_t gidx;
+  unsigned long long val;  // value bits (assign) or chunk sum bits (accumulate)
+};
+
+constexpr int kRbChunkSlots = 2 * kRbChunk;  // LDS dedup slots (load <= 1/2)
+
+__device__ __forceinline__ uint32_t rb_bucket(const DenseView& d, uint32_t k, uint32_t bshift,
+                                              uint32_t nbd) {
+  const uint32_t off = k - d.key_begin;
+  return (uint64_t)off < d.range ? (off >> bshift) : nbd;  // nbd = the out-of-range bucket
+}
+
+// a + b with two's-complement wrap for int32 (the reference's int values),
+// plain IEEE addition for float/double
+template <typename T>
+__device__ __forceinline__ T add_wrap(T a, T b) {
+  return a + b;
+}
+template <>
+__device__ __forceinline__ int add_wrap<int>(int a, int b) {
+  return (int)((uint32_t)a + (uint32_t)b);
+}
+
+template <typename T>
+__device__ __forceinline__ unsigned long long to_bits(T v) {
+  if (sizeof(T) == 8) return *reinterpret_cast<const unsigned long long*>(&v);
+  return (unsigned long long)*reinterpret_cast<const uint32_t*>(&v);
+}
+template <typename T>
+__device__ __forceinline__ T from_bits(unsigned long long b) {
+  if (sizeof(T) == 8) return *reinterpret_cast<const T*>(&b);
+  const uint32_t lo = (uint32_t)b;
+  return *reinterpret_cast<const T*>(&lo);
+}
+
+// LDS state of the chunk dedup.  The table is cleared ONCE per workgroup;
+// afterwards every chunk leaves it empty again: the thread whose CAS inserted
+// a key ("owner") emits that key and resets its slot (clear-on-emit), so the
+// per-chunk LDS work is O(keys), not O(slots).  Slot kRbChunkSlots belongs to
+// the key 0xFFFFFFFF (equal to the EMPTY marker).
+template <typename AT, int MODE>
+struct RbChunkLds {
+  uint32_t hk[kRbChunkSlots + 1];
+  uint32_t hlast[MODE == 0 ? kRbChunkSlots + 1 : 1];  // assign: last chunk index
+  AT hsum[MODE == 1 ? kRbChunkSlots + 1 : 1];         // accumulate: chunk sum
+  uint32_t sent_owner;                                 // lane index + 1 owning key 0xFFFFFFFF
+};
+
+template <typename AT, int MODE>
+__device__ __forceinline__ void rb_clear_all(RbChunkLds<AT, MODE>& L) {
+  for (int s = threadIdx.x; s <= kRbChunkSlots; s += blockDim.x) {
+    L.hk[s] = kEmpty32;
+    if (MODE == 0)
+      L.hlast[s] = 0;
+    else
+      L.hsum[s] = AT(0);
+  }
+  if (threadIdx.x == 0) L.sent_owner = 0;
+}
+
+// Insert this lane's RB_PER keys of the chunk; returns per key the slot and
+// whether this lane owns (first inserted) it.  Ends with a barrier.
+constexpr int RB_PER = kRbChunk / kBlock;  // 16 keys per lane
+template <typename AT, int MODE>
+__device__ __forceinline__ void rb_insert(const uint32_t* __restrict__ keys,
+                                          const AT* __restrict__ vals, uint64_t base, uint64_t n,
+                                          RbChunkLds<AT, MODE>& L, uint32_t (&slot)[RB_PER],
+                                          uint32_t (&key)[RB_PER], uint32_t& own_mask) {
+  const int tid = threadIdx.x;
+  own_mask = 0;
+  // lane keys: 4 groups of 4 consecutive keys (16-byte loads when the chunk is full)
+  const bool full = base + kRbChunk <= n && ((reinterpret_cast<uintptr_t>(keys) & 15u) == 0);
+#pragma unroll
+  for (int g = 0; g < RB_PER / 4; ++g) {
+    const uint64_t i0 = base + (uint64_t)(g * kBlock + tid) * 4;
+    if (full) {
+      uint32_t k4[4];
+      Vec4<uint32_t>::template load<true>(keys + i0, k4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) key[g * 4 + e] = k4[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) key[g * 4 + e] = i0 + e < n ? keys[i0 + e] : 0u;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < RB_PER; ++q) {
+    const int g = q / 4, e = q % 4;
+    const uint32_t li = (uint32_t)((g * kBlock + tid) * 4 + e);
+    slot[q] = kEmpty32;
+    if (base + li >= n) continue;
+    const uint32_t k = key[q];
+    uint32_t h;
+    bool own = false;
+    if (k == kEmpty32) {
+      h = kRbChunkSlots;
+      own = atomicCAS(&L.sent_owner, 0u, 1u) == 0u;
+    } else {
+      h = fmix32(k) & (kRbChunkSlots - 1);
+      for (;;) {
+        const uint32_t old = atomicCAS(&L.hk[h], kEmpty32, k);
+        if (old == kEmpty32) {
+          own = true;
+          break;
+        }
+        if (old == k) break;
+        h = (h + 1) & (kRbChunkSlots - 1);
+      }
+    }
+    slot[q] = h;
+    own_mask |= own ? (1u << q) : 0u;
+    if (MODE == 0)
+      atomicMax(&L.hlast[h], li);
+    else
+      atomicAdd(&L.hsum[h], vals[base + li]);
+  }
+  __syncthreads();
+}
+
+// Owner lanes read their keys' result and reset the slots.
+template <typename AT, int MODE>
+__device__ __forceinline__ void rb_take(RbChunkLds<AT, MODE>& L, uint32_t h, uint32_t* last,
+                                        AT* sum) {
+  if (MODE == 0) {
+    *last = L.hlast[h];
+    L.hlast[h] = 0;
+  } else {
+    *sum = L.hsum[h];
+    L.hsum[h] = AT(0);
+  }
+  if (h == kRbChunkSlots)
+    L.sent_owner = 0;
+  else
+    L.hk[h] = kEmpty32;
+}
+
+template <typename AT, int MODE>
+__global__ __launch_bounds__(kBlock) void k_rb_count(GroupArgs ga, DenseView d, uint32_t bshift,
+                                                     uint32_t nbd, uint32_t nbk, uint32_t* cnt,
+                                                     uint32_t nchunks) {
+  __shared__ RbChunkLds<AT, MODE> L;
+  __shared__ uint32_t hist[kRbMaxBuckets];
+  const int tid = threadIdx.x;
+  rb_clear_all(L);
+  for (uint32_t b = tid; b < nbk; b += kBlock) hist[b] = 0;
+  __syncthreads();
+  for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int j = batch_of(ga, c);
+    const uint64_t base = (uint64_t)(c - ga.wg_prefix[j]) * kRbChunk;
+    uint32_t slot[RB_PER], key[RB_PER], own;
+    rb_insert<AT, MODE>(ga.b[j].keys, reinterpret_cast<const AT*>(ga.b[j].vals), base, ga.b[j].n,
+                        L, slot, key, own);
+#pragma unroll
+    for (int q = 0; q < RB_PER; ++q) {
+      if (!(own >> q & 1u)) continue;
+      uint32_t last;
+      AT sum;
+      rb_take(L, slot[q], &last, &sum);
+      atomicAdd(&hist[rb_bucket(d, key[q], bshift, nbd)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t b = tid; b < nbk; b += kBlock) {
+      cnt[(uint64_t)b * nchunks + c] = hist[b];
+      hist[b] = 0;
+    }
+    __syncthreads();
+  }
+}
+
+// One workgroup per bucket: exclusive scan of cnt[b][*] in place, total[b].
+// Coalesced: tiles of 256 consecutive entries, wave scans via shuffles.
+__global__ __launch_bounds__(kBlock) void k_rb_scan(uint32_t* cnt, uint32_t nchunks,
+                                                    uint32_t* total) {
+  __shared__ uint32_t wsum[kBlock / 64];
+  uint32_t* row = cnt + (uint64_t)blockIdx.x * nchunks;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  uint32_t carry = 0;
+  for (uint32_t t0 = 0; t0 < nchunks; t0 += kBlock) {
+    const uint32_t i = t0 + tid;
+    const uint32_t x = i < nchunks ? row[i] : 0u;
+    uint32_t v = x;  // inclusive wave scan
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(v, o, 64);
+      if (lane >= o) v += y;
+    }
+    if (lane == 63) wsum[w] = v;
+    __syncthreads();
+    uint32_t before = carry, tile = 0;
+#pragma unroll
+    for (int q = 0; q < kBlock / 64; ++q) {
+      if (q < w) before += wsum[q];
+      tile += wsum[q];
+    }
+    if (i < nchunks) row[i] = before + v - x;
+    carry += tile;
+    __syncthreads();
+  }
+  if (tid == 0) total[blockIdx.x] = carry;
+}
+
+// Exclusive prefix of the bucket totals into LDS (nbk <= kRbMaxBuckets).
+__device__ __forceinline__ void rb_bases(const uint32_t* total, uint32_t nbk, uint32_t* sbase) {
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (uint32_t b = 0; b < nbk; ++b) {
+      sbase[b] = acc;
+      acc += total[b];
+    }
+    sbase[nbk] = acc;
+  }
+  __syncthreads();
+}
+
+template <typename AT, typename VT, int MODE>
+__global__ __launch_bounds__(kBlock) void k_rb_scatter(GroupArgs ga, DenseView d, uint32_t bshift,
+                                                       uint32_t nbd, uint32_t nbk,
+                                                       const uint32_t* cnt, uint32_t nchunks,
+                                                       const uint32_t* total, RbEntry* ent) {
+  __shared__ RbChunkLds<AT, MODE> L;
+  __shared__ uint32_t sbase[kRbMaxBuckets + 1];
+  __shared__ uint32_t cur[kRbMaxBuckets];
+  const int tid = threadIdx.x;
+  rb_clear_all(L);
+  rb_bases(total, nbk, sbase);
+  for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int j = batch_of(ga, c);
+    const uint64_t base = (uint64_t)(c - ga.wg_prefix[j]) * kRbChunk;
+    const uint64_t gbase = ga.elem_prefix[j] + base;
+    for (uint32_t b = tid; b < nbk; b += kBlock) cur[b] = sbase[b] + cnt[(uint64_t)b * nchunks + c];
+    uint32_t slot[RB_PER], key[RB_PER], own;
+    rb_insert<AT, MODE>(ga.b[j].keys, reinterpret_cast<const AT*>(ga.b[j].vals), base, ga.b[j].n,
+                        L, slot, key, own);
+#pragma unroll
+    for (int q = 0; q < RB_PER; ++q) {
+      if (!(own >> q & 1u)) continue;
+      uint32_t last = 0;
+      AT sum = AT(0);
+      rb_take(L, slot[q], &last, &sum);
+      const uint32_t dst = atomicAdd(&cur[rb_bucket(d, key[q], bshift, nbd)], 1u);
+      RbEntry e;
+      e.key = key[q];
+      if (MODE == 0) {
+        e.gidx = (uint32_t)(gbase + last);
+        e.val = to_bits<VT>(reinterpret_cast<const VT*>(ga.b[j].vals)[base + last]);
+      } else {
+        e.gidx = 0;
+        e.val = to_bits<AT>(sum);
+      }
+      ent[dst] = e;
+    }
+    __syncthreads();
+  }
+}
+
+// One 1024-thread workgroup per bucket (LDS: 128 KiB table, one workgroup per
+// CU, 16 waves).  Slot S-1 is reserved for the key 0xFFFFFFFF (probing of other
+// keys wraps before it).  The host sizes buckets for ~8 Ki entries, so one
+// round suffices; rounds split a bucket by key hash only when its entry count
+// could overfill the table (entries >= distinct keys).
+constexpr int kApplyBlock = 1024;
+template <typename AT, typename VT, int MODE>
+__global__ __launch_bounds__(kApplyBlock) void k_rb_apply(DenseView d, Ovf o, uint32_t nbd,
+                                                          uint32_t nbk, const uint32_t* total,
+                                                          const RbEntry* __restrict__ ent) {
+  constexpr int S = (MODE == 1 && sizeof(AT) == 8) ? kRbApplySlots / 2 : kRbApplySlots;
+  __shared__ uint32_t ak[S];
+  __shared__ uint32_t abest[MODE == 0 ? S : 1];  // assign: 1 + max group index (0 = none)
+  __shared__ AT asum[MODE == 1 ? S : 1];
+  __shared__ uint32_t sbase[kRbMaxBuckets + 1];
+  __shared__ uint32_t sent;
+  const int tid = threadIdx.x;
+  rb_bases(total, nbk, sbase);
+  auto probe = [&](uint32_t key, bool insert) -> uint32_t {
+    if (key == kEmpty32) return S - 1;
+    uint32_t h = fmix32(key) % (S - 1);
+    for (;;) {
+      if (insert) {
+        const uint32_t old = atomicCAS(&ak[h], kEmpty32, key);
+        if (old == kEmpty32 || old == key) return h;
+      } else if (ak[h] == key) {
+        return h;
+      }
+      h = h + 1 == S - 1 ? 0 : h + 1;
+    }
+  };
+  for (uint32_t b = blockIdx.x; b < nbk; b += gridDim.x) {
+    const uint32_t e0 = sbase[b], e1 = sbase[b + 1];
+    if (e0 == e1) continue;
+    const uint32_t cap = (uint32_t)(S - 1) / 8 * 7;
+    const uint32_t R = (e1 - e0 + cap - 1) / cap;
+    for (uint32_t round = 0; round < R; ++round) {
+      for (int s = tid; s < S; s += kApplyBlock) {
+        ak[s] = kEmpty32;
+        if (MODE == 0)
+          abest[s] = 0;
+        else
+          asum[s] = AT(0);
+      }
+      if (tid == 0) sent = 0;
+      __syncthreads();
+      for (uint32_t e = e0 + tid; e < e1; e += kApplyBlock) {
+        const RbEntry x = ent[e];
+        if (R > 1 && (fmix32(x.key ^ 0x9E3779B9u) % R) != round) continue;
+        const uint32_t h = probe(x.key, true);
+        if (x.key == kEmpty32) sent = 1;
+        if (MODE == 0)
+          atomicMax(&abest[h], x.gidx + 1u);
+        else
+          atomicAdd(&asum[h], from_bits<AT>(x.val));
+      }
+      __syncthreads();
+      if (MODE == 0) {
+        // the entry holding its key's largest group index is the last write
+        for (uint32_t e = e0 + tid; e < e1; e += kApplyBlock) {
+          const RbEntry x = ent[e];
+          if (R > 1 && (fmix32(x.key ^ 0x9E3779B9u) % R) != round) continue;
+          if (abest[probe(x.key, false)] != x.gidx + 1u) continue;
+          const VT v = from_bits<VT>(x.val);
+          if (b != nbd) {
+            reinterpret_cast<VT*>(d.param)[x.key - d.key_begin] = v;
+          } else {
+            const long long sl = ovf_insert(o, x.key);
+            if (sl >= 0) reinterpret_cast<VT*>(o.vals)[sl] = v;
+          }
+        }
+      } else {
+        // this workgroup owns every key of the bucket: plain read-modify-write
+        for (int s = tid; s < S; s += kApplyBlock) {
+          const bool used = s == S - 1 ? sent != 0 : ak[s] != kEmpty32;
+          if (!used) continue;
+          const uint32_t key = s == S - 1 ? kEmpty32 : ak[s];
+          AT* p;
+          if (b != nbd) {
+            p = reinterpret_cast<AT*>(d.param) + (uint32_t)(key - d.key_begin);
+          } else {
+            const long long sl = ovf_insert(o, key);
+            if (sl < 0) continue;
+            p = reinterpret_cast<AT*>(o.vals) + sl;
+          }
+          *p = add_wrap<AT>(*p, asum[s]);
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
 }  // namespace
 
 // ------------------------------------------------------- launch wrappers
@@ -793,5 +1164,36 @@ hipError_t launch_ovf_rehash(int vb, const Ovf& from, uint64_t from_cap, const O
     k_ovf_rehash<unsigned long long><<<(uint32_t)g, kBlock, 0, st>>>(from, from_cap, to);
   return hipGetLastError();
 }
+
+template <typename AT, typename VT, int MODE>
+static hipError_t rb_launch(const GroupArgs& ga, uint32_t nchunks, const DenseView& d, const Ovf& o,
+                            uint32_t bshift, uint32_t nbd, uint32_t* cnt, uint32_t* total,
+                            void* ent, hipStream_t st) {
+  const uint32_t nbk = nbd + 1;
+  const uint32_t g = nchunks < 1024u ? nchunks : 1024u;  // persistent: LDS cleared once per WG
+  RbEntry* e = reinterpret_cast<RbEntry*>(ent);
+  k_rb_count<AT, MODE><<<g, kBlock, 0, st>>>(ga, d, bshift, nbd, nbk, cnt, nchunks);
+  k_rb_scan<<<nbk, kBlock, 0, st>>>(cnt, nchunks, total);
+  k_rb_scatter<AT, VT, MODE><<<g, kBlock, 0, st>>>(ga, d, bshift, nbd, nbk, cnt, nchunks, total, e);
+  k_rb_apply<AT, VT, MODE><<<nbk, kApplyBlock, 0, st>>>(d, o, nbd, nbk, total, e);
+  return hipGetLastError();
+}
+
+hipError_t launch_rb_add(int dtype, int mode, const GroupArgs& ga, uint32_t nchunks,
+                         const DenseView& d, const Ovf& o, uint32_t bshift, uint32_t nbd,
+                         uint32_t* cnt, uint32_t* total, void* ent, hipStream_t st) {
+  if (nchunks == 0) return hipSuccess;
+  if (nbd + 1 > (uint32_t)kRbMaxBuckets) return hipErrorInvalidValue;
+  if (mode == 0) {
+    if (dtype == 2)
+      return rb_launch<uint32_t, unsigned long long, 0>(ga, nchunks, d, o, bshift, nbd, cnt, total, ent, st);
+    return rb_launch<uint32_t, uint32_t, 0>(ga, nchunks, d, o, bshift, nbd, cnt, total, ent, st);
+  }
+  if (dtype == 0) return rb_launch<int, int, 1>(ga, nchunks, d, o, bshift, nbd, cnt, total, ent, st);
+  if (dtype == 1) return rb_launch<float, float, 1>(ga, nchunks, d, o, bshift, nbd, cnt, total, ent, st);
+  return rb_launch<double, double, 1>(ga, nchunks, d, o, bshift, nbd, cnt, total, ent, st);
+}
+
+size_t rb_entry_bytes() { return sizeof(RbEntry); }
 
 }  // namespace pskv

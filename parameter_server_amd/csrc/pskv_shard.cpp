@@ -110,6 +110,13 @@ struct pskv_shard {
   uint64_t t_elems[PSKV_K_COUNT] = {};
   // stats
   uint64_t n_add = 0, n_get = 0, n_sorted = 0, n_general = 0;
+  // K5 radix-bucket scratch (grown on demand)
+  uint32_t* rb_cnt = nullptr;
+  size_t rb_cnt_bytes = 0;
+  uint32_t* rb_total = nullptr;
+  void* rb_ent = nullptr;
+  size_t rb_ent_bytes = 0;
+  int general_path = 1;  // PSKV_GENERAL: stamps = 0 (K4 always), auto = 1, radix = 2 (K5 always)
   // tuning knobs (environment, read at creation): PSKV_TILE_SHIFT, PSKV_TILE_GRID
   uint32_t tune_tile_shift = 0;
   uint32_t tune_tile_grid = 4096;
@@ -311,10 +318,61 @@ std::vector<std::pair<size_t, size_t>> split_groups(const std::vector<pskv_batch
   return out;
 }
 
+// Grow a device scratch buffer (stream-ordered: queued kernels may still use
+// the old one, so synchronise before freeing it).
+int ensure_scratch(pskv_shard* s, void** p, size_t* have, size_t need) {
+  if (*have >= need) return PSKV_OK;
+  if (*p) {
+    PSKV_HIP(hipStreamSynchronize(s->stream));
+    (void)hipFree(*p);
+  }
+  *p = nullptr;
+  const size_t nb = std::max<size_t>(need + need / 4, 1 << 16);
+  if (hipMalloc(p, nb) != hipSuccess) {
+    *p = nullptr;
+    *have = 0;
+    return fail(PSKV_ENOMEM, "scratch allocation failed");
+  }
+  *have = nb;
+  return PSKV_OK;
+}
+
+// K5: radix-bucket general Add (no random global atomics).
+int radix_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t e) {
+  GroupArgs ga;
+  const uint32_t nchunks = build_group(v, b, e, kRbChunk, &ga);
+  uint64_t elems = 0;
+  for (size_t i = b; i < e; ++i) elems += v[i].n;
+  // bucket = key offset >> bshift, sized for ~8 Ki entries per bucket (one
+  // apply round) and at most 1024 dense buckets
+  uint32_t bits = 0;
+  while (bits < 32 && ((s->range - 1) >> bits) != 0) ++bits;
+  uint32_t tb = 6;
+  while (tb < 10 && (elems >> (13 + tb)) != 0) ++tb;
+  const uint32_t bshift = bits > tb ? bits - tb : 0;
+  const uint32_t nbd = (uint32_t)(((s->range - 1) >> bshift) + 1);
+  const uint32_t nbk = nbd + 1;
+  size_t have_total = s->rb_total ? 4 * (size_t)kRbMaxBuckets : 0;
+  int rc = ensure_scratch(s, reinterpret_cast<void**>(&s->rb_cnt), &s->rb_cnt_bytes,
+                          (size_t)nbk * nchunks * sizeof(uint32_t));
+  if (!rc) rc = ensure_scratch(s, reinterpret_cast<void**>(&s->rb_total), &have_total,
+                               (size_t)kRbMaxBuckets * sizeof(uint32_t));
+  if (!rc) rc = ensure_scratch(s, &s->rb_ent, &s->rb_ent_bytes, elems * rb_entry_bytes());
+  if (rc) return rc;
+  LaunchTimer t(s, PSKV_K_RADIX, elems);
+  PSKV_HIP(launch_rb_add(s->dtype, s->mode, ga, nchunks, s->dview(), s->ovf, bshift, nbd,
+                         s->rb_cnt, s->rb_total, s->rb_ent, s->stream));
+  t.done();
+  s->n_general += 4;
+  return PSKV_OK;
+}
+
 // The general (any order) Add over one launch group.  `cond` non-null makes
-// it a repair that runs only when the sorted path tagged `epoch`.
+// it a repair that runs only when the sorted path tagged `epoch` (K4, whose
+// idle launches are cheap); unconditional general Adds take K5.
 int general_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t e,
-                uint32_t epoch, const uint32_t* cond) {
+                uint32_t epoch, const uint32_t* cond, bool radix = true) {
+  if (!cond && ((radix && s->general_path == 1) || s->general_path == 2)) return radix_add(s, v, b, e);
   if (s->mode == PSKV_ASSIGN && !s->owner) {
     // The stamp array is only needed once the general path can run: allocate it
     // on first use (8 B per owned key).
@@ -459,7 +517,10 @@ int add_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
   for (auto& g : split_groups(v)) {
     const uint32_t epoch = next_epoch(s);
     if (s->mode == PSKV_ACCUMULATE) {
-      rc = general_add(s, v, g.first, g.second, epoch, nullptr);
+      // order-free, so K4a (LDS sums, one atomic add per distinct key per chunk,
+      // coalesced for sorted chunks) is always correct; it measured faster than
+      // K5 for accumulate on cfg 3 (398 vs 480 us per 8M Zipf keys)
+      rc = general_add(s, v, g.first, g.second, epoch, nullptr, /*radix=*/false);
     } else if (!device && host_verified) {
       // the CPU proved the batches sorted and in range while staging them
       rc = sorted_add(s, v, g.first, g.second, vec, epoch, /*repair=*/false);
@@ -579,6 +640,8 @@ int pskv_shard_create_ex(int device, uint32_t key_begin, uint64_t key_end, int d
     const int v = std::atoi(e);
     if (v >= 10 && v <= 20) s->tune_tile_shift = (uint32_t)v;
   }
+  if (const char* e = std::getenv("PSKV_GENERAL"))
+    s->general_path = std::strcmp(e, "stamps") == 0 ? 0 : std::strcmp(e, "radix") == 0 ? 2 : 1;
   if (const char* e = std::getenv("PSKV_UNROLL")) s->tune_unroll = std::atoi(e) == 4 ? 4 : 8;
   if (const char* e = std::getenv("PSKV_NT")) s->tune_nt = std::atoi(e) != 0;
   if (const char* e = std::getenv("PSKV_TILE_GRID")) {
@@ -634,6 +697,9 @@ int pskv_shard_destroy(pskv_shard* s) {
   if (s->flag) (void)hipFree(s->flag);
   free_overflow(&s->ovf);
   if (s->dstage) (void)hipFree(s->dstage);
+  if (s->rb_cnt) (void)hipFree(s->rb_cnt);
+  if (s->rb_total) (void)hipFree(s->rb_total);
+  if (s->rb_ent) (void)hipFree(s->rb_ent);
   if (s->hstage) (void)hipHostFree(s->hstage);
   if (s->hstage_free) (void)hipEventDestroy(s->hstage_free);
   if (s->own_stream) (void)hipStreamDestroy(s->own_stream);

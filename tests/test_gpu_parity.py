@@ -427,3 +427,66 @@ def test_grouped_dense_lookalike_is_repaired(cuda, oracle_mod):
         sh.add_grouped([(tdev(k, cuda), tdev(v, cuda)) for k, v in batches], sorted_hint=True)
         got = sh.get(np.arange(size, dtype=np.uint32))
     assert_bits_equal(got, dense, "lookalike")
+
+
+@pytest.mark.parametrize("mode,dtype", [("assign", np.float32), ("assign", np.float64),
+                                        ("accumulate", np.float64), ("accumulate", np.int32)])
+def test_radix_path_hot_bucket_many_rounds(cuda, oracle_mod, mode, dtype, monkeypatch):
+    """K5: every key in ONE key bucket (and the out-of-range bucket), far more
+    entries than the apply workgroup's LDS table holds -> multi-round apply."""
+    import parameter_server_amd as ps
+
+    monkeypatch.setenv("PSKV_GENERAL", "radix")  # K5 for accumulate too
+
+    rng = np.random.default_rng(55)
+    size = 1 << 25                      # bucket width 64 Ki keys
+    kb = 1000
+    batches = []
+    for j in range(12):
+        n = 60_000 + j
+        k = rng.integers(kb, kb + 65_536, size=n)          # dense bucket 0
+        k[:500] = rng.integers(kb + size, 2**32, size=500)  # out-of-range bucket
+        k = k.astype(np.uint32)
+        if dtype is np.int32:
+            v = rng.integers(-2**31, 2**31 - 1, size=n, dtype=np.int64).astype(np.int32)
+        else:
+            v = rng.standard_normal(n).astype(dtype)
+        batches.append((k, v))
+    q = np.unique(np.concatenate([k for k, _ in batches]))
+    with ps.Shard(kb, kb + size, dtype, mode=mode, overflow_slots=1 << 15) as sh:
+        sh.add_grouped([(tdev(k, cuda), tdev(v, cuda)) for k, v in batches])
+        got = sh.get(q)
+        sh.sync()
+    if mode == "assign":
+        ref = oracle_mod.MapStorageRef(dtype)
+        for k, v in batches:
+            ref.add(k, v)
+        assert_bits_equal(got, ref.get(q), "radix assign")
+    else:
+        acc = {}
+        for k, v in batches:
+            for kk, vv in zip(k.tolist(), v.tolist()):
+                acc[kk] = acc.get(kk, 0) + vv
+        want = np.array([acc[int(x)] for x in q])
+        if dtype is np.int32:
+            assert_bits_equal(got, ((want + 2**31) % 2**32 - 2**31).astype(np.int32), "radix int acc")
+        else:
+            assert np.allclose(got, want, rtol=1e-12, atol=1e-9)
+
+
+def test_general_path_stamps_variant_matches(cuda, oracle_mod, monkeypatch):
+    """The K4 stamp path (kept for repairs) as the unhinted general path."""
+    import parameter_server_amd as ps
+
+    monkeypatch.setenv("PSKV_GENERAL", "stamps")
+    rng = np.random.default_rng(66)
+    ref = oracle_mod.MapStorageRef(np.float32)
+    with ps.Shard(0, 500_000, np.float32, overflow_slots=1 << 14) as sh:
+        for _ in range(4):
+            k = rng.integers(0, 520_000, size=90_000).astype(np.uint32)
+            v = rng.standard_normal(k.size).astype(np.float32)
+            sh.add(tdev(k, cuda), tdev(v, cuda))
+            ref.add(k, v)
+        q = np.arange(0, 520_000, dtype=np.uint32)
+        got = sh.get(q)
+    assert_bits_equal(got, ref.get(q), "stamps path")
