@@ -59,16 +59,26 @@ def parse():
 
 
 def dist_init(args):
+    """One process per GPU (torchrun).  RCCL ("nccl") carries only the barrier and
+    the two scalar reductions.  Rehearsal knobs for a 1-GPU box (never used by the
+    driver): PSKV_BENCH_BACKEND=gloo and PSKV_BENCH_SHARE_GPU=1 put every rank on
+    cuda:0 and synchronise over gloo."""
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("PSKV_BENCH_SHARE_GPU") == "1":
+        local = 0
     if world > 1:
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        backend = os.environ.get("PSKV_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     return rank, world, local
@@ -81,13 +91,19 @@ def barrier(world):
         dist.barrier()
 
 
+def _reduce_device(dev):
+    import torch.distributed as dist
+
+    return dev if dist.get_backend() == "nccl" else "cpu"
+
+
 def max_over_ranks(x, world, dev):
     if world == 1:
         return x
     import torch
     import torch.distributed as dist
 
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    t = torch.tensor([x], dtype=torch.float64, device=_reduce_device(dev))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -98,7 +114,7 @@ def sum_over_ranks(x, world, dev):
     import torch
     import torch.distributed as dist
 
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    t = torch.tensor([x], dtype=torch.float64, device=_reduce_device(dev))
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
 
@@ -193,13 +209,16 @@ def _cpu_model():
     return "unknown"
 
 
-def load_pmc(kernel_substr):
-    """HBM traffic per dispatch from the committed rocprofv3 --pmc summary, if any."""
+def load_pmc(kernel_substr, config):
+    """HBM traffic per dispatch from the committed rocprofv3 --pmc summary, if it
+    was collected on this same bench configuration."""
     path = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if not os.path.exists(path):
         return None, None
     with open(path) as f:
         d = json.load(f)
+    if d.get("config") != config:
+        return None, None
     for name, rec in d.get("kernels", {}).items():
         if kernel_substr in name and rec.get("hbm_bytes_per_dispatch"):
             return rec["hbm_bytes_per_dispatch"], d.get("source", path)
@@ -326,7 +345,7 @@ def main():
     dom = max(ktimes.items(), key=lambda kv: kv[1]["avg_ms"] * kv[1]["launches"])
     launch_bytes = get_b if dom[0] == "k_gather" else add_b  # one launch = one step's Add or Get
     achieved = launch_bytes / (dom[1]["avg_ms"] / 1e3) / 1e9
-    traffic, traffic_src = load_pmc(dom[0])
+    traffic, traffic_src = load_pmc(dom[0], {"n_gpus": world, "batches": J, "batch_keys": B})
     for name, kt in ktimes.items():
         kt["algorithmic_bytes"] = get_b if name == "k_gather" else add_b
         kt["GB/s"] = kt["algorithmic_bytes"] / (kt["avg_ms"] / 1e3) / 1e9
