@@ -9,6 +9,8 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include <vector>
+
 #include "ps/message.hpp"
 
 #ifndef PS_CHECK
@@ -47,6 +49,14 @@ class AbstractStorage {
     reply.AddData<Key>(reply_keys);
     reply.AddData<char>(reply_vals);
     return reply;
+  }
+
+  // Apply several Add messages in order (semantically msgs.size() Add calls).
+  // Source-compatible extension: the default loops; HipStorage overrides it
+  // with one grouped device call (BSP's flush of add_buffer_,
+  // server/consistency/bsp_model.cpp:20-25, is the natural caller).
+  virtual void AddGrouped(std::vector<Message>& msgs) {
+    for (auto& m : msgs) Add(m);
   }
 
   virtual void SubAdd(const third_party::SArray<Key>& typed_keys,

@@ -167,7 +167,13 @@ class BSPModel : public AbstractModel {
       : model_id_(model_id), reply_queue_(reply_queue), storage_(std::move(storage)) {}
   void Clock(Message& msg) override {
     if (tracker_.AdvanceAndGetChangedMinClock(msg.meta.sender) != -1) {
-      for (auto& m : add_buffer_) storage_->Add(m);  // deferred Adds, arrival order
+      // deferred Adds in arrival order (bsp_model.cpp:20-25), as ONE grouped
+      // call: HipStorage turns it into one staged copy and one launch
+      if (grouped_flush_) {
+        if (!add_buffer_.empty()) storage_->AddGrouped(add_buffer_);
+      } else {
+        for (auto& m : add_buffer_) storage_->Add(m);
+      }
       add_buffer_.clear();
       std::vector<Message> gets;
       gets.swap(get_buffer_);
@@ -186,6 +192,7 @@ class BSPModel : public AbstractModel {
     tracker_.Init(detail::tids_of(msg));
     reply_queue_->Push(detail::reset_reply(msg, model_id_));
   }
+  void SetGroupedFlush(bool on) { grouped_flush_ = on; }  // off = the reference's per-message loop
   int GetGetPendingSize() const { return (int)get_buffer_.size(); }
   int GetAddPendingSize() const { return (int)add_buffer_.size(); }
   AbstractStorage* storage() { return storage_.get(); }
@@ -196,6 +203,7 @@ class BSPModel : public AbstractModel {
   std::unique_ptr<AbstractStorage> storage_;
   ProgressTracker tracker_;
   std::vector<Message> add_buffer_, get_buffer_;
+  bool grouped_flush_ = true;
 };
 
 class ASPModel : public AbstractModel {

@@ -20,6 +20,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #include "pskv.h"
 
@@ -78,6 +79,31 @@ class HipStorage : public AbstractStorage {
     pskv_check(pskv_add(shard_, typed_keys.data(), typed_vals.data(), typed_keys.size(), PSKV_HOST),
                "pskv_add");
   }
+
+#ifndef PSKV_IN_REFERENCE_TREE
+  // One staged copy and one grouped launch for a run of Add messages (BSP flush).
+  void AddGrouped(std::vector<Message>& msgs) override {
+    std::vector<pskv_batch> batches;
+    std::vector<third_party::SArray<Key>> keep_k;
+    std::vector<third_party::SArray<Val>> keep_v;
+    batches.reserve(msgs.size());
+    for (auto& m : msgs) {
+      if (m.data.size() != 2) {
+        std::fprintf(stderr, "Check failed: msg.data.size() == 2\n");
+        std::abort();
+      }
+      keep_k.emplace_back(m.data[0]);
+      keep_v.emplace_back(m.data[1]);
+      if (keep_k.back().size() != keep_v.back().size()) {
+        std::fprintf(stderr, "Check failed: typed_keys.size() == typed_vals.size()\n");
+        std::abort();
+      }
+      batches.push_back(pskv_batch{keep_k.back().data(), keep_v.back().data(), keep_k.back().size()});
+    }
+    pskv_check(pskv_add_grouped(shard_, batches.data(), batches.size(), PSKV_HOST),
+               "pskv_add_grouped");
+  }
+#endif
 
   third_party::SArray<char> SubGet(const third_party::SArray<Key>& typed_keys) override {
     third_party::SArray<Val> reply_vals(typed_keys.size());

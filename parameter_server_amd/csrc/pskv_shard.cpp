@@ -19,10 +19,15 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "pskv.h"
@@ -74,6 +79,92 @@ struct TimedLaunch {
   uint64_t elems;
 };
 
+// ---------------------------------------------------------------- host pool
+// A small persistent pool for the host side of the path: copying zmq-buffer
+// inputs into pinned staging (with the sorted/in-range check) and pinned
+// outputs back to the caller.  One parallel section at a time; the caller
+// thread works too.  Size: PSKV_HOST_THREADS (default min(8, cores)).
+class HostPool {
+ public:
+  static HostPool& get() {
+    static HostPool p;
+    return p;
+  }
+  size_t size() const { return workers_.size() + 1; }
+  // Runs fn(0..n-1), blocking until all are done.
+  void run(size_t n, const std::function<void(size_t)>& fn) {
+    if (n == 0) return;
+    if (n == 1 || workers_.empty()) {
+      for (size_t i = 0; i < n; ++i) fn(i);
+      return;
+    }
+    std::lock_guard<std::mutex> section(section_);
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      fn_ = &fn;
+      n_ = n;
+      next_.store(0);
+      left_ = n;
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> lk(m_);
+    done_.wait(lk, [&] { return left_ == 0; });
+    fn_ = nullptr;
+  }
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      stop_ = true;
+      ++gen_;
+    }
+    cv_.notify_all();
+    for (auto& t : workers_) t.join();
+  }
+
+ private:
+  HostPool() {
+    unsigned hw = std::thread::hardware_concurrency();
+    unsigned n = std::min(8u, hw ? hw : 1u);
+    if (const char* e = std::getenv("PSKV_HOST_THREADS")) n = (unsigned)std::max(1, std::atoi(e));
+    for (unsigned i = 1; i < n; ++i) workers_.emplace_back([this] { loop(); });
+  }
+  void work() {
+    for (;;) {
+      const size_t i = next_.fetch_add(1);
+      if (i >= n_) return;
+      (*fn_)(i);
+      std::lock_guard<std::mutex> lk(m_);
+      if (--left_ == 0) done_.notify_all();
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (stop_) return;
+        if (!fn_) continue;
+      }
+      work();
+    }
+  }
+  std::vector<std::thread> workers_;
+  std::mutex section_, m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(size_t)>* fn_ = nullptr;
+  size_t n_ = 0, left_ = 0;
+  std::atomic<size_t> next_{0};
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+constexpr size_t kPieceBytes = 1 << 20;   // one pool task
+constexpr size_t kWindowBytes = 8 << 20;  // one H2D / D2H DMA while the next window is copied
+
 }  // namespace
 
 struct pskv_shard {
@@ -101,6 +192,7 @@ struct pskv_shard {
   bool hstage_pending = false;
   void* dstage = nullptr;
   size_t dstage_bytes = 0;
+  std::vector<hipEvent_t> win_events;  // per-window D2H completion (pull to host)
   // timing
   uint32_t timing_mask = 0;  // bit k: bracket kernel k with events
   std::vector<TimedLaunch> pending;
@@ -435,6 +527,74 @@ int sorted_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t
   return PSKV_OK;
 }
 
+// One contiguous piece of a host->pinned (or pinned->host) copy.
+struct Piece {
+  const char* src;
+  char* dst;
+  size_t bytes;
+  int key_batch;  // >= 0: keys of that batch (checked while copied), -1: values
+  // results of the key check
+  bool sorted;
+  uint32_t first, last;
+  uint64_t outside;
+};
+
+void copy_piece(Piece& p, uint32_t key_begin, uint64_t range) {
+  if (p.key_batch < 0) {
+    std::memcpy(p.dst, p.src, p.bytes);
+    return;
+  }
+  const uint32_t* k = reinterpret_cast<const uint32_t*>(p.src);
+  uint32_t* o = reinterpret_cast<uint32_t*>(p.dst);
+  const size_t n = p.bytes / 4;
+  bool ok = true;
+  uint64_t outside = 0;
+  uint32_t prev = n ? k[0] : 0;
+  for (size_t i = 0; i < n; ++i) {
+    const uint32_t x = k[i];
+    o[i] = x;
+    outside += (uint64_t)(uint32_t)(x - key_begin) >= range;
+    ok &= prev <= x;
+    prev = x;
+  }
+  p.sorted = ok;
+  p.first = n ? k[0] : 0;
+  p.last = n ? k[n - 1] : 0;
+  p.outside = outside;
+}
+
+// Cut [src, src+bytes) into pieces appended to `out`.
+void add_pieces(std::vector<Piece>& out, const void* src, char* dst, size_t bytes, int key_batch) {
+  const char* s = static_cast<const char*>(src);
+  for (size_t off = 0; off < bytes; off += kPieceBytes) {
+    Piece p{};
+    p.src = s + off;
+    p.dst = dst + off;
+    p.bytes = std::min(kPieceBytes, bytes - off);
+    p.key_batch = key_batch;
+    p.sorted = true;
+    out.push_back(p);
+  }
+}
+
+// Copy pieces window by window (pool in parallel) and DMA each window to the
+// device as soon as it is staged, so the copy of window w+1 overlaps the H2D
+// of window w.  Pieces must be in increasing staging order.
+int pipelined_h2d(pskv_shard* s, std::vector<Piece>& pieces, char* h, char* d) {
+  HostPool& pool = HostPool::get();
+  size_t i = 0;
+  while (i < pieces.size()) {
+    size_t j = i, win = 0;
+    while (j < pieces.size() && (win < kWindowBytes || j == i)) win += pieces[j++].bytes;
+    pool.run(j - i, [&](size_t t) { copy_piece(pieces[i + t], s->key_begin, s->range); });
+    char* lo = pieces[i].dst;
+    char* hi = pieces[j - 1].dst + pieces[j - 1].bytes;
+    PSKV_HIP(hipMemcpyAsync(d + (lo - h), lo, (size_t)(hi - lo), hipMemcpyHostToDevice, s->stream));
+    i = j;
+  }
+  return PSKV_OK;
+}
+
 // Stage host batches into one device buffer (keys then values per batch,
 // 16-byte aligned) through pinned memory, checking on the way whether every
 // batch is sorted and inside the dense range.  Returns device batch views.
@@ -449,34 +609,40 @@ int stage_host_batches(pskv_shard* s, const std::vector<pskv_batch>& in,
   if (rc) return rc;
   char* h = static_cast<char*>(s->hstage);
   char* d = static_cast<char*>(s->dstage);
+  std::vector<Piece> pieces;
   size_t off = 0;
-  bool ok = true;
-  uint64_t outside = 0;
   out->clear();
-  for (auto& b : in) {
-    uint32_t* hk = reinterpret_cast<uint32_t*>(h + off);
-    uint32_t prev = 0;
-    for (uint64_t i = 0; i < b.n; ++i) {
-      const uint32_t k = b.keys[i];
-      hk[i] = k;
-      const bool in_range = (uint64_t)(uint32_t)(k - s->key_begin) < s->range;
-      outside += !in_range;
-      ok &= in_range & (i == 0 || prev <= k);
-      prev = k;
-    }
+  for (size_t j = 0; j < in.size(); ++j) {
+    const auto& b = in[j];
     pskv_batch db;
+    add_pieces(pieces, b.keys, h + off, b.n * 4, (int)j);
     db.keys = reinterpret_cast<const uint32_t*>(d + off);
     off += round16(b.n * 4);
-    std::memcpy(h + off, b.vals, b.n * (size_t)s->vb);
+    add_pieces(pieces, b.vals, h + off, b.n * (size_t)s->vb, -1);
     db.vals = d + off;
     db.n = b.n;
     off += round16(b.n * (size_t)s->vb);
     out->push_back(db);
   }
-  PSKV_HIP(hipMemcpyAsync(s->dstage, s->hstage, off, hipMemcpyHostToDevice, s->stream));
+  rc = pipelined_h2d(s, pieces, h, d);
+  if (rc) return rc;
   PSKV_HIP(hipEventRecord(s->hstage_free, s->stream));
   s->hstage_pending = true;
-  *all_sorted_in_range = ok;
+  // combine the per-piece checks: every piece sorted, and each piece's first
+  // key not below the previous piece's last key within the same batch
+  bool ok = true;
+  uint64_t outside = 0;
+  int prev_batch = -1;
+  uint32_t prev_last = 0;
+  for (const auto& p : pieces) {
+    if (p.key_batch < 0) continue;
+    outside += p.outside;
+    ok &= p.sorted;
+    if (p.key_batch == prev_batch) ok &= prev_last <= p.first;
+    prev_batch = p.key_batch;
+    prev_last = p.last;
+  }
+  *all_sorted_in_range = ok && outside == 0;
   *n_outside = outside;
   return PSKV_OK;
 }
@@ -549,7 +715,7 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
   std::vector<pskv_batch> dv = v;
   size_t out_off = 0;
   if (!device) {
-    // keys → pinned → device; outputs land after the keys in the device stage
+    // keys -> pinned -> device (pipelined); outputs land after the keys in the stage
     size_t kbytes = 0, obytes = 0;
     for (auto& b : v) {
       kbytes += round16(b.n * 4);
@@ -561,13 +727,15 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
     if (rc) return rc;
     char* h = static_cast<char*>(s->hstage);
     char* d = static_cast<char*>(s->dstage);
+    std::vector<Piece> pieces;
     size_t off = 0;
     for (size_t i = 0; i < v.size(); ++i) {
-      std::memcpy(h + off, v[i].keys, v[i].n * 4);
+      add_pieces(pieces, v[i].keys, h + off, v[i].n * 4, -1);
       dv[i].keys = reinterpret_cast<const uint32_t*>(d + off);
       off += round16(v[i].n * 4);
     }
-    PSKV_HIP(hipMemcpyAsync(d, h, off, hipMemcpyHostToDevice, s->stream));
+    rc = pipelined_h2d(s, pieces, h, d);
+    if (rc) return rc;
     out_off = off;
     for (size_t i = 0; i < v.size(); ++i) {
       dv[i].vals = d + off;
@@ -587,16 +755,48 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
     t.done();
   }
   if (!device) {
+    // D2H window by window; the pool copies window w out to the caller while
+    // window w+1 is still in flight
     char* h = static_cast<char*>(s->hstage);
     char* d = static_cast<char*>(s->dstage);
-    size_t obytes = 0;
-    for (auto& b : v) obytes += round16(b.n * (size_t)s->vb);
-    PSKV_HIP(hipMemcpyAsync(h + out_off, d + out_off, obytes, hipMemcpyDeviceToHost, s->stream));
-    PSKV_HIP(hipStreamSynchronize(s->stream));
+    std::vector<Piece> pieces;  // pinned -> caller
     size_t off = out_off;
     for (auto& b : v) {
-      std::memcpy(b.vals, h + off, b.n * (size_t)s->vb);
-      off += round16(b.n * (size_t)s->vb);
+      Piece p{};
+      const size_t nb = b.n * (size_t)s->vb;
+      for (size_t o = 0; o < nb; o += kPieceBytes) {
+        p.src = h + off + o;
+        p.dst = static_cast<char*>(b.vals) + o;
+        p.bytes = std::min(kPieceBytes, nb - o);
+        p.key_batch = -1;
+        pieces.push_back(p);
+      }
+      off += round16(nb);
+    }
+    std::vector<std::pair<size_t, size_t>> wins;  // [first piece, end piece)
+    for (size_t i = 0; i < pieces.size();) {
+      size_t j = i, win = 0;
+      while (j < pieces.size() && (win < kWindowBytes || j == i)) win += pieces[j++].bytes;
+      wins.emplace_back(i, j);
+      i = j;
+    }
+    while (s->win_events.size() < wins.size()) {
+      hipEvent_t e = nullptr;
+      PSKV_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      s->win_events.push_back(e);
+    }
+    for (size_t w = 0; w < wins.size(); ++w) {
+      const char* lo = pieces[wins[w].first].src;
+      const char* hi = pieces[wins[w].second - 1].src + pieces[wins[w].second - 1].bytes;
+      PSKV_HIP(hipMemcpyAsync(const_cast<char*>(lo), d + (lo - h), (size_t)(hi - lo),
+                              hipMemcpyDeviceToHost, s->stream));
+      PSKV_HIP(hipEventRecord(s->win_events[w], s->stream));
+    }
+    HostPool& pool = HostPool::get();
+    for (size_t w = 0; w < wins.size(); ++w) {
+      PSKV_HIP(hipEventSynchronize(s->win_events[w]));
+      pool.run(wins[w].second - wins[w].first,
+               [&](size_t t) { copy_piece(pieces[wins[w].first + t], s->key_begin, s->range); });
     }
   }
   return PSKV_OK;
@@ -702,6 +902,7 @@ int pskv_shard_destroy(pskv_shard* s) {
   if (s->rb_ent) (void)hipFree(s->rb_ent);
   if (s->hstage) (void)hipHostFree(s->hstage);
   if (s->hstage_free) (void)hipEventDestroy(s->hstage_free);
+  for (auto e : s->win_events) (void)hipEventDestroy(e);
   if (s->own_stream) (void)hipStreamDestroy(s->own_stream);
   delete s;
   return PSKV_OK;

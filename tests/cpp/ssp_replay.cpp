@@ -104,6 +104,7 @@ struct Config {
   uint32_t n_features = 1000000;
   uint64_t seed = 2026;
   bool cpu_only = false;
+  bool bsp_ungrouped = false;
 };
 
 struct ReplyRecord {
@@ -140,8 +141,11 @@ class Replay {
       storages_.push_back(st.get());
       if (c.model == "ssp")
         models_.emplace_back(new SSPModel(0, std::move(st), c.staleness, &replies_));
-      else if (c.model == "bsp")
-        models_.emplace_back(new BSPModel(0, std::move(st), &replies_));
+      else if (c.model == "bsp") {
+        auto* m = new BSPModel(0, std::move(st), &replies_);
+        m->SetGroupedFlush(!c.bsp_ungrouped);
+        models_.emplace_back(m);
+      }
       else
         models_.emplace_back(new ASPModel(0, std::move(st), &replies_));
     }
@@ -537,6 +541,7 @@ int main(int argc, char** argv) {
     else if (a == "--skew") c.skew = std::stoi(nxt());
     else if (a == "--features") c.n_features = (uint32_t)std::stoul(nxt());
     else if (a == "--cpu-only") c.cpu_only = true;
+    else if (a == "--bsp-ungrouped") c.bsp_ungrouped = true;
     else if (a == "--known-answers") ka = true;
   }
   int fails = 0;
