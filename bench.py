@@ -261,6 +261,29 @@ def side_measurements(dev, B):
                    "GB/s": (add_b + get_b) * reps / dt / 1e9, "ms_per_step": dt / reps * 1e3,
                    "unique_keys_per_batch": uniq, "distinct_keys_per_step": u_all}
     del zb, zo
+    # cfg 2 windows in accumulate mode (the north star's scatter-accumulate):
+    # sorted hint -> K4a, LDS run sums + one coalesced atomic add per key
+    J = 16
+    db = workload.dense_batches(J, space, batch=B, device=dev)
+    with ps.Shard(0, space, np.float32, mode="accumulate") as sh:
+        sh.set_stream(stream.cuda_stream)
+        adds = sh.prepare(db)
+        for _ in range(2):
+            sh.add_grouped(adds, sorted_hint=True)
+        torch.cuda.synchronize()
+        reps = 5
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            sh.add_grouped(adds, sorted_hint=True)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        sh.set_stream(None)
+    # accumulate Add bytes: n*(4+V) input + 2*u*V parameter read-modify-write
+    acc_b = J * B * (4 + V) + 2 * len(set(int(b) for b in workload.dense_bases(J, space, B))) * B * V
+    out["accumulate_dense_add"] = {"workload": f"cfg 2 windows, {J} x 1M contiguous float pushes, accumulate "
+                                               "mode (sorted hint -> K4a)",
+                                   "GB/s": acc_b * reps / dt / 1e9, "ms_per_call": dt / reps * 1e3}
+    del db
     # end-to-end: keys/vals start in pageable host memory (the zmq frames), outputs return to host
     rng = np.random.default_rng(0)
     J = 8

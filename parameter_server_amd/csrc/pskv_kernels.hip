@@ -350,7 +350,7 @@ __device__ __forceinline__ bool apply_segment(const DevBatch& b, uint64_t s, uin
 // once (a 64-lane ballot) and elements test only the few that overlap.
 // Every element verifies k == first_j + i; a batch whose endpoints look dense
 // but whose keys are not is caught there and tagged for the repair.
-template <typename VT, bool VEC, int U, bool NT>
+template <typename VT, bool VEC, int U, bool NT, bool NTP>
 __device__ __forceinline__ bool dense_chunk(const GroupArgs& ga, const DenseView& d, uint32_t c,
                                             const uint32_t* s_first, const uint32_t* s_last) {
   constexpr int CH = kBlock * 4 * U;
@@ -395,7 +395,7 @@ __device__ __forceinline__ bool dense_chunk(const GroupArgs& ga, const DenseView
       bad |= (k[u][0] != k0) | (k[u][1] != k0 + 1u) | (k[u][2] != k0 + 2u) | (k[u][3] != k0 + 3u);
       const uint32_t off0 = k0 - d.key_begin;
       if (later == 0 && (off0 & 3u) == 0u) {
-        Vec4<VT>::store(param + off0, v[u]);
+        Vec4<VT>::template store<NTP>(param + off0, v[u]);
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
@@ -413,7 +413,7 @@ __device__ __forceinline__ bool dense_chunk(const GroupArgs& ga, const DenseView
 }
 
 // Mode B (general sorted batches): key-tile owner, static strided schedule.
-template <typename VT, bool VEC, int U, bool NT>
+template <typename VT, bool VEC, int U, bool NT, bool NTP>
 __global__ __launch_bounds__(kBlock) void k_assign_group(GroupArgs ga, DenseView d,
                                                          uint32_t tile_shift, uint64_t ntiles,
                                                          uint32_t* flag, uint32_t epoch) {
@@ -456,7 +456,7 @@ __global__ __launch_bounds__(kBlock) void k_assign_group(GroupArgs ga, DenseView
   if (s_dense) {
     const uint32_t nchunks = ga.wg_prefix[ga.nb];
     for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x)
-      bad |= dense_chunk<VT, VEC, U, NT>(ga, d, c, s_first, s_last);
+      bad |= dense_chunk<VT, VEC, U, NT, NTP>(ga, d, c, s_first, s_last);
     if (bad) *flag = epoch;
     return;
   }
@@ -1078,38 +1078,48 @@ hipError_t launch_assign_sorted(int vb, bool vec, const uint32_t* keys, const vo
   return hipGetLastError();
 }
 
-template <typename VT, bool VEC>
-static void group_dispatch(int unroll, bool nt, uint32_t grid, const GroupArgs& ga,
-                           const DenseView& d, uint32_t shift, uint64_t ntiles, uint32_t* flag,
-                           uint32_t epoch, hipStream_t st) {
+template <typename VT, bool VEC, bool NTP>
+static void group_dispatch2(int unroll, bool nt, uint32_t grid, const GroupArgs& ga,
+                            const DenseView& d, uint32_t shift, uint64_t ntiles, uint32_t* flag,
+                            uint32_t epoch, hipStream_t st) {
   if (unroll == 8) {
     if (nt)
-      k_assign_group<VT, VEC, 8, true><<<grid, kBlock, 0, st>>>(ga, d, shift, ntiles, flag, epoch);
+      k_assign_group<VT, VEC, 8, true, NTP><<<grid, kBlock, 0, st>>>(ga, d, shift, ntiles, flag, epoch);
     else
-      k_assign_group<VT, VEC, 8, false><<<grid, kBlock, 0, st>>>(ga, d, shift, ntiles, flag, epoch);
+      k_assign_group<VT, VEC, 8, false, NTP><<<grid, kBlock, 0, st>>>(ga, d, shift, ntiles, flag, epoch);
   } else {
     if (nt)
-      k_assign_group<VT, VEC, 4, true><<<grid, kBlock, 0, st>>>(ga, d, shift, ntiles, flag, epoch);
+      k_assign_group<VT, VEC, 4, true, NTP><<<grid, kBlock, 0, st>>>(ga, d, shift, ntiles, flag, epoch);
     else
-      k_assign_group<VT, VEC, 4, false><<<grid, kBlock, 0, st>>>(ga, d, shift, ntiles, flag, epoch);
+      k_assign_group<VT, VEC, 4, false, NTP><<<grid, kBlock, 0, st>>>(ga, d, shift, ntiles, flag, epoch);
   }
 }
 
-hipError_t launch_assign_group(int vb, bool vec, int unroll, bool nt, const GroupArgs& ga,
+template <typename VT, bool VEC>
+static void group_dispatch(int unroll, bool nt, bool ntp, uint32_t grid, const GroupArgs& ga,
+                           const DenseView& d, uint32_t shift, uint64_t ntiles, uint32_t* flag,
+                           uint32_t epoch, hipStream_t st) {
+  if (ntp)
+    group_dispatch2<VT, VEC, true>(unroll, nt, grid, ga, d, shift, ntiles, flag, epoch, st);
+  else
+    group_dispatch2<VT, VEC, false>(unroll, nt, grid, ga, d, shift, ntiles, flag, epoch, st);
+}
+
+hipError_t launch_assign_group(int vb, bool vec, int unroll, bool nt, bool ntp, const GroupArgs& ga,
                                const DenseView& d, uint32_t tile_shift, uint64_t ntiles,
                                uint32_t grid, uint32_t* flag, uint32_t epoch, hipStream_t st) {
   if (grid == 0) return hipSuccess;
   if (vb == 4) {
     if (vec)
-      group_dispatch<uint32_t, true>(unroll, nt, grid, ga, d, tile_shift, ntiles, flag, epoch, st);
+      group_dispatch<uint32_t, true>(unroll, nt, ntp, grid, ga, d, tile_shift, ntiles, flag, epoch, st);
     else
-      group_dispatch<uint32_t, false>(unroll, nt, grid, ga, d, tile_shift, ntiles, flag, epoch, st);
+      group_dispatch<uint32_t, false>(unroll, nt, ntp, grid, ga, d, tile_shift, ntiles, flag, epoch, st);
   } else {
     if (vec)
-      group_dispatch<unsigned long long, true>(unroll, nt, grid, ga, d, tile_shift, ntiles, flag,
+      group_dispatch<unsigned long long, true>(unroll, nt, ntp, grid, ga, d, tile_shift, ntiles, flag,
                                                epoch, st);
     else
-      group_dispatch<unsigned long long, false>(unroll, nt, grid, ga, d, tile_shift, ntiles, flag,
+      group_dispatch<unsigned long long, false>(unroll, nt, ntp, grid, ga, d, tile_shift, ntiles, flag,
                                                 epoch, st);
   }
   return hipGetLastError();

@@ -214,6 +214,7 @@ struct pskv_shard {
   uint32_t tune_tile_grid = 4096;
   int tune_unroll = 8;   // PSKV_UNROLL: 4 or 8 (8: measured +5 % on the dense Add)
   bool tune_nt = true;   // PSKV_NT: non-temporal streams (measured +12-15 % on K1 / K2g)
+  bool tune_ntp = false; // PSKV_NTP: non-temporal parameter stores (dense Add)
 
   DenseView dview() const { return DenseView{dense, key_begin, range}; }
 };
@@ -231,8 +232,10 @@ hipEvent_t take_event(pskv_shard* s) {
     s->event_pool.pop_back();
     return e;
   }
+  // timing-only events: no system-scope release fence (an L2 writeback + invalidate
+  // per record, measured at ~4 us each between the cfg-2 kernels)
   hipEvent_t e = nullptr;
-  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return nullptr;
   return e;
 }
 
@@ -518,7 +521,7 @@ int sorted_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t
     const uint32_t grid =
         (uint32_t)std::min<uint64_t>(std::max<uint64_t>(ntiles, nchunks), s->tune_tile_grid);
     LaunchTimer t(s, PSKV_K_ASSIGN_TILES, elems);
-    PSKV_HIP(launch_assign_group(s->vb, vec, s->tune_unroll, s->tune_nt, ga, s->dview(), shift,
+    PSKV_HIP(launch_assign_group(s->vb, vec, s->tune_unroll, s->tune_nt, s->tune_ntp, ga, s->dview(), shift,
                                  ntiles, grid, s->flag, epoch, s->stream));
     t.done();
   }
@@ -844,6 +847,7 @@ int pskv_shard_create_ex(int device, uint32_t key_begin, uint64_t key_end, int d
     s->general_path = std::strcmp(e, "stamps") == 0 ? 0 : std::strcmp(e, "radix") == 0 ? 2 : 1;
   if (const char* e = std::getenv("PSKV_UNROLL")) s->tune_unroll = std::atoi(e) == 4 ? 4 : 8;
   if (const char* e = std::getenv("PSKV_NT")) s->tune_nt = std::atoi(e) != 0;
+  if (const char* e = std::getenv("PSKV_NTP")) s->tune_ntp = std::atoi(e) != 0;
   if (const char* e = std::getenv("PSKV_TILE_GRID")) {
     const int v = std::atoi(e);
     if (v >= 1 && v <= 65536) s->tune_tile_grid = (uint32_t)v;

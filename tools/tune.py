@@ -60,6 +60,14 @@ def main():
                 continue
             res[name]["step"].append((t1 - t0) / 5 * 1e3)
             res[name]["host"].append((th - t0) / 5 * 1e3)
+            # the same steps without event timing
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            for _ in range(5):
+                sh.add_grouped(adds, sorted_hint=True)
+                sh.get_grouped(gets)
+            torch.cuda.synchronize()
+            res[name].setdefault("step_untimed", []).append((time.perf_counter() - t2) / 5 * 1e3)
             for k, kn in _lib.KERNEL_NAMES.items():
                 t = sh.kernel_time(k)
                 if t["launches"]:
@@ -82,7 +90,7 @@ def main():
             extra = ""
             if k in ("k_gather", "k_assign_tiles"):
                 extra = f" ({J * 1e6 * 12 / (med / 1e3) / 1e9:.0f} GB/s)"
-            if k == "step":
+            if k in ("step", "step_untimed"):
                 extra = f" ({J * 1e6 * 24 / (med / 1e3) / 1e9:.0f} GB/s)"
             line.append(f"{k}={med:.4f}ms{extra}")
         print("  ".join(line), flush=True)
