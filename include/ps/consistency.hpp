@@ -23,6 +23,7 @@
 #include <cstdint>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <queue>
 #include <unordered_map>
 #include <vector>
@@ -31,20 +32,28 @@
 
 namespace csci5570 {
 
-// A FIFO the models push replies into (the reference uses ThreadsafeQueue,
-// base/threadsafe_queue.hpp; the replay is single-threaded).
+// The FIFO models push replies into (the reference uses ThreadsafeQueue,
+// base/threadsafe_queue.hpp): several server threads may push concurrently.
 class ReplyQueue {
  public:
-  void Push(const Message& m) { q_.push(m); }
+  void Push(const Message& m) {
+    std::lock_guard<std::mutex> lk(m_);
+    q_.push(m);
+  }
   bool Pop(Message* m) {
+    std::lock_guard<std::mutex> lk(m_);
     if (q_.empty()) return false;
     *m = q_.front();
     q_.pop();
     return true;
   }
-  size_t Size() const { return q_.size(); }
+  size_t Size() {
+    std::lock_guard<std::mutex> lk(m_);
+    return q_.size();
+  }
 
  private:
+  std::mutex m_;
   std::queue<Message> q_;
 };
 

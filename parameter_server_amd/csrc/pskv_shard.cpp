@@ -99,19 +99,18 @@ class HostPool {
       return;
     }
     std::lock_guard<std::mutex> section(section_);
+    Job job(&fn, n);
     {
       std::lock_guard<std::mutex> lk(m_);
-      fn_ = &fn;
-      n_ = n;
-      next_.store(0);
-      left_ = n;
+      job_ = &job;
       ++gen_;
     }
     cv_.notify_all();
-    work();
+    work(job);
     std::unique_lock<std::mutex> lk(m_);
-    done_.wait(lk, [&] { return left_ == 0; });
-    fn_ = nullptr;
+    // a worker that joined late may still hold the job: wait for it to let go
+    done_.wait(lk, [&] { return job.left == 0 && job.refs == 0; });
+    job_ = nullptr;
   }
   ~HostPool() {
     {
@@ -124,40 +123,53 @@ class HostPool {
   }
 
  private:
+  // One parallel section; lives on the stack of run() until every index is
+  // done and no worker references it.
+  struct Job {
+    Job(const std::function<void(size_t)>* f, size_t count) : fn(f), n(count), left(count) {}
+    const std::function<void(size_t)>* fn;
+    size_t n;
+    std::atomic<size_t> next{0};
+    size_t left;  // guarded by m_
+    int refs = 0;  // workers inside work(*this), guarded by m_
+  };
   HostPool() {
     unsigned hw = std::thread::hardware_concurrency();
     unsigned n = std::min(8u, hw ? hw : 1u);
     if (const char* e = std::getenv("PSKV_HOST_THREADS")) n = (unsigned)std::max(1, std::atoi(e));
     for (unsigned i = 1; i < n; ++i) workers_.emplace_back([this] { loop(); });
   }
-  void work() {
+  void work(Job& j) {
     for (;;) {
-      const size_t i = next_.fetch_add(1);
-      if (i >= n_) return;
-      (*fn_)(i);
+      const size_t i = j.next.fetch_add(1);
+      if (i >= j.n) return;
+      (*j.fn)(i);
       std::lock_guard<std::mutex> lk(m_);
-      if (--left_ == 0) done_.notify_all();
+      if (--j.left == 0) done_.notify_all();
     }
   }
   void loop() {
     uint64_t seen = 0;
     for (;;) {
+      Job* j;
       {
         std::unique_lock<std::mutex> lk(m_);
         cv_.wait(lk, [&] { return gen_ != seen; });
         seen = gen_;
         if (stop_) return;
-        if (!fn_) continue;
+        j = job_;
+        if (!j) continue;
+        ++j->refs;
       }
-      work();
+      work(*j);
+      std::lock_guard<std::mutex> lk(m_);
+      if (--j->refs == 0 && j->left == 0) done_.notify_all();
     }
   }
   std::vector<std::thread> workers_;
   std::mutex section_, m_;
   std::condition_variable cv_, done_;
-  const std::function<void(size_t)>* fn_ = nullptr;
-  size_t n_ = 0, left_ = 0;
-  std::atomic<size_t> next_{0};
+  Job* job_ = nullptr;
   uint64_t gen_ = 0;
   bool stop_ = false;
 };

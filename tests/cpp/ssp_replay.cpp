@@ -21,6 +21,9 @@
 // usage: ssp_replay [--model ssp|bsp|asp] [--workers W] [--shards S] [--iters I]
 //                   [--batch B] [--staleness T] [--skew K] [--cpu-only] [--known-answers]
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <mutex>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -35,6 +38,7 @@
 #include "ps/consistency.hpp"
 #include "ps/hip_storage.hpp"
 #include "ps/range_partition_manager.hpp"
+#include "ps/server_thread.hpp"
 
 using namespace csci5570;
 
@@ -105,6 +109,7 @@ struct Config {
   uint64_t seed = 2026;
   bool cpu_only = false;
   bool bsp_ungrouped = false;
+  bool threads = false;  // one ServerThread per shard (concurrent HipStorage use)
 };
 
 struct ReplyRecord {
@@ -139,17 +144,29 @@ class Replay {
       else
         st.reset(new OracleStorage<double>());
       storages_.push_back(st.get());
-      if (c.model == "ssp")
-        models_.emplace_back(new SSPModel(0, std::move(st), c.staleness, &replies_));
-      else if (c.model == "bsp") {
+      std::unique_ptr<AbstractModel> md;
+      if (c.model == "ssp") {
+        md.reset(new SSPModel(0, std::move(st), c.staleness, &replies_));
+      } else if (c.model == "bsp") {
         auto* m = new BSPModel(0, std::move(st), &replies_);
         m->SetGroupedFlush(!c.bsp_ungrouped);
-        models_.emplace_back(m);
+        md.reset(m);
+      } else {
+        md.reset(new ASPModel(0, std::move(st), &replies_));
       }
-      else
-        models_.emplace_back(new ASPModel(0, std::move(st), &replies_));
+      if (c.threads) {  // server_thread.cpp: the model lives in its server's thread
+        threads_.emplace_back(new ServerThread((uint32_t)s));
+        threads_.back()->RegisterModel(0, std::move(md));
+        threads_.back()->SetOnProcessed([this] {
+          std::lock_guard<std::mutex> lk(qm_);
+          if (--inflight_ == 0) quiet_.notify_all();
+        });
+      } else {
+        models_.push_back(std::move(md));
+      }
     }
     server_q_.resize(c.shards);
+    for (auto& t : threads_) t->Start();
     // samples: feature popularity is skewed (idx ~ n * u^3) so workers collide on keys
     for (int w = 0; w < c.workers; ++w) {
       Rng r(c.seed * 1000003ull + (uint64_t)w);
@@ -188,6 +205,7 @@ class Replay {
       m.meta.flag = Flag::kResetWorkerInModel;
       m.meta.sender = 9999;
       m.meta.recver = s;
+      m.meta.model_id = 0;
       m.AddData(third_party::SArray<uint32_t>(tids));
       deliver(m);
     }
@@ -210,6 +228,7 @@ class Replay {
       if (all_done) break;
       if (!progressed) throw std::runtime_error("replay deadlock: every worker waits on a reply");
     }
+    for (auto& t : threads_) t->Stop();  // kExit; the storages stay alive in their models
     // final contents of every shard, read through the plugin interface
     for (int s = 0; s < c_.shards; ++s) {
       std::vector<uint32_t> ks;
@@ -237,11 +256,44 @@ class Replay {
 
   void deliver(const Message& m) {
     ++out_.msgs;
-    server_q_[m.meta.recver].push(m);
+    if (c_.threads) {
+      {
+        std::lock_guard<std::mutex> lk(qm_);
+        ++inflight_;
+      }
+      threads_[m.meta.recver]->GetWorkQueue()->Push(m);
+    } else {
+      server_q_[m.meta.recver].push(m);
+    }
+  }
+
+  // Threaded mode: wait until every server thread is idle, then route the
+  // replies of that window ordered by server (each server's replies keep
+  // their FIFO order), so the run is deterministic.
+  void pump_threads() {
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(qm_);
+        quiet_.wait(lk, [&] { return inflight_ == 0; });
+      }
+      std::vector<Message> window;
+      Message r;
+      while (replies_.Pop(&r)) window.push_back(r);
+      if (window.empty()) return;
+      std::stable_sort(window.begin(), window.end(), [](const Message& a, const Message& b) {
+        const int sa = a.data.size() == 1 ? a.meta.recver : a.meta.sender;
+        const int sb = b.data.size() == 1 ? b.meta.recver : b.meta.sender;
+        return sa < sb;
+      });
+      // route the window itself: echoes delivered now are served concurrently
+      // and their replies land in the NEXT window
+      for (auto& m : window) route_one(m);
+    }
   }
 
   // Process every queued server message and route every reply, until quiet.
   void pump() {
+    if (c_.threads) return pump_threads();
     for (;;) {
       bool any = false;
       for (int s = 0; s < c_.shards; ++s) {
@@ -266,22 +318,24 @@ class Replay {
 
   void route() {
     Message r;
-    while (replies_.Pop(&r)) {
-      if (r.meta.flag == Flag::kGet && r.data.size() == 1) {  // SSP-released request: back to its server
-        ++out_.echoes;
-        deliver(r);
-        continue;
-      }
-      if (r.meta.flag != Flag::kGet) continue;  // reset acknowledgements
-      Worker& w = workers_[r.meta.recver - 100];
-      auto k = third_party::SArray<Key>(r.data[0]);
-      auto v = third_party::SArray<double>(r.data[1]);
-      ReplyRecord rec{r.meta.sender, r.meta.recver, std::vector<uint32_t>(k.begin(), k.end()),
-                      std::vector<double>(v.begin(), v.end())};
-      out_.log.push_back(rec);
-      for (size_t i = 0; i < k.size(); ++i) w.reply.insert(std::make_pair(k[i], v[i]));
-      if (--w.outstanding == 0) finish_get(w);
+    while (replies_.Pop(&r)) route_one(r);
+  }
+
+  void route_one(const Message& r) {
+    if (r.meta.flag == Flag::kGet && r.data.size() == 1) {  // SSP-released request: back to its server
+      ++out_.echoes;
+      deliver(r);
+      return;
     }
+    if (r.meta.flag != Flag::kGet) return;  // reset acknowledgements
+    Worker& w = workers_[r.meta.recver - 100];
+    auto k = third_party::SArray<Key>(r.data[0]);
+    auto v = third_party::SArray<double>(r.data[1]);
+    ReplyRecord rec{r.meta.sender, r.meta.recver, std::vector<uint32_t>(k.begin(), k.end()),
+                    std::vector<double>(v.begin(), v.end())};
+    out_.log.push_back(rec);
+    for (size_t i = 0; i < k.size(); ++i) w.reply.insert(std::make_pair(k[i], v[i]));
+    if (--w.outstanding == 0) finish_get(w);
   }
 
   void send_get(Worker& w, const std::vector<Key>& keys) {  // kv_client_table.hpp:107-139
@@ -399,6 +453,10 @@ class Replay {
   std::unique_ptr<RangeShardMap> map_;
   std::vector<AbstractStorage*> storages_;
   std::vector<std::unique_ptr<AbstractModel>> models_;
+  std::vector<std::unique_ptr<ServerThread>> threads_;
+  std::mutex qm_;
+  std::condition_variable quiet_;
+  int64_t inflight_ = 0;
   std::vector<std::queue<Message>> server_q_;
   ReplyQueue replies_;
   std::vector<std::vector<Sample>> pools_;
@@ -542,6 +600,7 @@ int main(int argc, char** argv) {
     else if (a == "--features") c.n_features = (uint32_t)std::stoul(nxt());
     else if (a == "--cpu-only") c.cpu_only = true;
     else if (a == "--bsp-ungrouped") c.bsp_ungrouped = true;
+    else if (a == "--threads") c.threads = true;
     else if (a == "--known-answers") ka = true;
   }
   int fails = 0;

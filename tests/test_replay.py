@@ -36,3 +36,24 @@ def test_replay_hip_vs_cpu(model, staleness):
                   "--shards", "8", "--workers", "4")
     assert rc == 0, out
     assert "REPLAY OK (bit-exact)" in out and "[hip] model known answers: ok" in out
+
+
+@pytest.mark.parametrize("model", ["ssp", "bsp", "asp"])
+def test_replay_threaded_cpu_deterministic(model):
+    """One ServerThread per shard (server/server_thread.cpp:20-50): the replies
+    of each quiescence window are routed in server order, so two threaded runs
+    agree bit for bit."""
+    rc, out = run("--cpu-only", "--threads", "--model", model, "--iters", "6", "--workers", "6",
+                  "--skew", "2")
+    assert rc == 0, out
+    assert "REPLAY OK" in out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model", ["ssp", "bsp"])
+def test_replay_threaded_hip_vs_cpu(model):
+    """8 server threads drive 8 HipStorage shards concurrently (pskv.h threading
+    contract: distinct handles on distinct threads)."""
+    rc, out = run("--threads", "--model", model, "--iters", "8", "--shards", "8", "--workers", "4")
+    assert rc == 0, out
+    assert "REPLAY OK (bit-exact)" in out
