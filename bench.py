@@ -231,7 +231,7 @@ def side_measurements(dev, B):
     import torch
 
     import parameter_server_amd as ps
-    from parameter_server_amd import workload
+    from parameter_server_amd import _lib, workload
 
     out = {}
     stream = torch.cuda.current_stream()
@@ -260,10 +260,27 @@ def side_measurements(dev, B):
                                "(general path K5: LDS dedup + radix buckets)",
                    "GB/s": (add_b + get_b) * reps / dt / 1e9, "ms_per_step": dt / reps * 1e3,
                    "unique_keys_per_batch": uniq, "distinct_keys_per_step": u_all}
+    # cfg 3 in accumulate mode (the north star's LDS segmented-sum path): K4a,
+    # per-chunk LDS sums then one atomic add per distinct key per chunk
+    with ps.Shard(0, space, np.float32, mode="accumulate") as sh:
+        sh.set_stream(stream.cuda_stream)
+        for _ in range(2):
+            sh.add_grouped(zb)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            sh.add_grouped(zb)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        sh.set_stream(None)
+    acc_b = J * B * (4 + V) + 2 * u_all * V
+    out["zipf_accumulate_add"] = {"workload": "cfg 3 pushes (8 x 1M Zipf(0.99), unsorted), accumulate mode "
+                                              "(K4a: LDS chunk sums + one atomic add per distinct key per chunk)",
+                                  "GB/s": acc_b * reps / dt / 1e9, "ms_per_call": dt / reps * 1e3}
     del zb, zo
     # cfg 2 windows in accumulate mode (the north star's scatter-accumulate):
-    # sorted hint -> K4a, LDS run sums + one coalesced atomic add per key
-    J = 16
+    # sorted hint -> K6 density proof + K7 one RMW per key (sums in call order)
+    J = 64
     db = workload.dense_batches(J, space, batch=B, device=dev)
     with ps.Shard(0, space, np.float32, mode="accumulate") as sh:
         sh.set_stream(stream.cuda_stream)
@@ -271,18 +288,30 @@ def side_measurements(dev, B):
         for _ in range(2):
             sh.add_grouped(adds, sorted_hint=True)
         torch.cuda.synchronize()
-        reps = 5
+        reps = 10
         t0 = time.perf_counter()
         for _ in range(reps):
             sh.add_grouped(adds, sorted_hint=True)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        sh.set_timing(True, kernels=[_lib.PSKV_K_DENSE_CHECK, _lib.PSKV_K_ACC_DENSE])
+        for _ in range(reps):
+            sh.add_grouped(adds, sorted_hint=True)
+        torch.cuda.synchronize()
+        kt = {_lib.KERNEL_NAMES[k]: sh.kernel_time(k) for k in (_lib.PSKV_K_DENSE_CHECK, _lib.PSKV_K_ACC_DENSE)}
+        sh.set_timing(False)
         sh.set_stream(None)
     # accumulate Add bytes: n*(4+V) input + 2*u*V parameter read-modify-write
-    acc_b = J * B * (4 + V) + 2 * len(set(int(b) for b in workload.dense_bases(J, space, B))) * B * V
-    out["accumulate_dense_add"] = {"workload": f"cfg 2 windows, {J} x 1M contiguous float pushes, accumulate "
-                                               "mode (sorted hint -> K4a)",
-                                   "GB/s": acc_b * reps / dt / 1e9, "ms_per_call": dt / reps * 1e3}
+    u_acc = len(set(int(b) for b in workload.dense_bases(J, space, B))) * B
+    acc_b = J * B * (4 + V) + 2 * u_acc * V
+    k_ms = {n: t["total_ms"] / max(1, t["launches"]) for n, t in kt.items()}
+    out["accumulate_dense_add"] = {
+        "workload": f"cfg 2 windows, {J} x 1M contiguous float pushes, accumulate mode "
+                    "(sorted hint -> K6 density proof + K7 one RMW per key, no atomics)",
+        "GB/s": acc_b * reps / dt / 1e9, "ms_per_call": dt / reps * 1e3,
+        "kernels_avg_ms": k_ms,
+        "k_acc_dense_GB/s": (J * B * V + 2 * u_acc * V) / (k_ms["k_acc_dense"] * 1e-3) / 1e9,
+        "k_dense_check_GB/s": (J * B * 4) / (k_ms["k_dense_check"] * 1e-3) / 1e9}
     del db
     # end-to-end: keys/vals start in pageable host memory (the zmq frames), outputs return to host
     rng = np.random.default_rng(0)

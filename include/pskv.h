@@ -113,7 +113,9 @@ enum pskv_kernel {
   PSKV_K_GENERAL_MARK = 3,  /* K4a: chunk dedup + stamps / accumulate */
   PSKV_K_GENERAL_COMMIT = 4,/* K4b: winner write */
   PSKV_K_RADIX = 5,         /* K5a-d: radix-bucket general Add (timed as one operation) */
-  PSKV_K_COUNT = 6
+  PSKV_K_DENSE_CHECK = 6,   /* K6: accumulate, prove the batches dense windows */
+  PSKV_K_ACC_DENSE = 7,     /* K7: accumulate dense windows, one RMW per key */
+  PSKV_K_COUNT = 8
 };
 
 /* Create a shard owning keys [key_begin, key_end) on `device`.  The dense

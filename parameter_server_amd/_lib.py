@@ -30,7 +30,9 @@ PSKV_K_ASSIGN_TILES = 2
 PSKV_K_GENERAL_MARK = 3
 PSKV_K_GENERAL_COMMIT = 4
 PSKV_K_RADIX = 5
-PSKV_K_COUNT = 6
+PSKV_K_DENSE_CHECK = 6
+PSKV_K_ACC_DENSE = 7
+PSKV_K_COUNT = 8
 KERNEL_NAMES = {
     PSKV_K_GATHER: "k_gather",
     PSKV_K_ASSIGN_SORTED: "k_assign_sorted",
@@ -38,6 +40,8 @@ KERNEL_NAMES = {
     PSKV_K_GENERAL_MARK: "k_general_mark",
     PSKV_K_GENERAL_COMMIT: "k_general_commit",
     PSKV_K_RADIX: "k_radix_bucket",
+    PSKV_K_DENSE_CHECK: "k_dense_check",
+    PSKV_K_ACC_DENSE: "k_acc_dense",
 }
 
 # Every symbol include/pskv.h declares (checked by tests/test_abi.py).

@@ -88,6 +88,13 @@ hipError_t launch_ovf_rehash(int vb, const Ovf& from, uint64_t from_cap, const O
 hipError_t launch_rb_add(int dtype, int mode, const GroupArgs& ga, uint32_t nchunks,
                          const DenseView& d, const Ovf& o, uint32_t bshift, uint32_t nbd,
                          uint32_t* cnt, uint32_t* total, void* ent, hipStream_t st);
+// K6: tag `flag` with `epoch` unless every batch is a dense in-range window
+// (chunk = kBlock * 4 * 8 keys per workgroup).
+hipError_t launch_dense_check(const GroupArgs& ga, uint32_t nchunks, const DenseView& d,
+                              uint32_t* flag, uint32_t epoch, hipStream_t st);
+// K7: accumulate dense windows (skips when flag == epoch); chunk as K6.
+hipError_t launch_acc_dense(int dtype, const GroupArgs& ga, uint32_t grid, const DenseView& d,
+                            const uint32_t* flag, uint32_t epoch, hipStream_t st);
 size_t rb_entry_bytes();
 
 }  // namespace pskv

@@ -17,6 +17,10 @@
 //                         (assign) u64 last-writer stamps / (accumulate) one
 //                         atomic add per distinct key per workgroup
 //   K4b k_general_commit  Add, any order: the stamped winner of each key stores
+//   K5  k_rb_*            Add, any order, assign: radix buckets, no global atomics
+//   K6  k_dense_check     accumulate: prove every batch a dense in-range window
+//   K7  k_acc_dense       accumulate over dense windows: one RMW per key, sums in
+//                         call order, no atomics
 //
 // Semantics restated from the reference: last write wins within a call (index
 // order) and across calls (stream order) — map_storage.hpp:22-23 assigns in a
@@ -1020,6 +1024,157 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_apply(DenseView d, Ovf o, ui
   }
 }
 
+
+// ------------------------------------------- K6/K7 dense accumulate
+// Accumulate for grouped batches that are each one contiguous key window
+// (first_j .. first_j + n_j - 1): no atomics and no duplicates to resolve.
+// Every key gets exactly ONE read-modify-write, by the element of the
+// EARLIEST batch that covers it, which adds that batch's value and then the
+// values of every later covering batch in call order — so the result is the
+// sequential sum p + v_0 + v_1 + ... bit for bit.  Because the RMW cannot be
+// undone, density is proven BEFORE it runs:
+//   K6 k_dense_check  reads the keys only; tags `flag` with the call's epoch
+//                     unless every batch is exactly dense and in range
+//   K7 k_acc_dense    skips when tagged; K4a accumulate (conditional on the
+//                     tag) takes the group instead
+// Host-staged batches are proven dense on the CPU while copied, so K6 and the
+// K4a fallback are not launched for them.
+
+template <int U>
+__global__ __launch_bounds__(kBlock) void k_dense_check(GroupArgs ga, DenseView d, uint32_t* flag,
+                                                        uint32_t epoch) {
+  constexpr int CH = kBlock * 4 * U;
+  const uint32_t wg = blockIdx.x;
+  const int j = batch_of(ga, wg);
+  const uint32_t* __restrict__ keys = ga.b[j].keys;
+  const uint64_t n = ga.b[j].n;
+  const uint64_t base = (uint64_t)(wg - ga.wg_prefix[j]) * CH;
+  const int tid = threadIdx.x;
+  const uint32_t first = keys[0];
+  const uint64_t off = (uint32_t)(first - d.key_begin);
+  bool bad = off >= d.range || off + n > d.range;
+  if (base + CH <= n && (reinterpret_cast<uintptr_t>(keys) & 15u) == 0) {
+    uint32_t k[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      Vec4<uint32_t>::load<true>(keys + base + (uint64_t)(u * kBlock + tid) * 4, k[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t k0 = first + (uint32_t)(base + (uint64_t)(u * kBlock + tid) * 4);
+      bad |= (k[u][0] != k0) | (k[u][1] != k0 + 1u) | (k[u][2] != k0 + 2u) | (k[u][3] != k0 + 3u);
+    }
+  } else {
+    const uint64_t end = n < base + CH ? n : base + CH;
+    for (uint64_t i = base + tid; i < end; i += kBlock) bad |= keys[i] != first + (uint32_t)i;
+  }
+  if (__any(bad) && (tid & 63) == 0) *flag = epoch;
+}
+
+template <typename AT>
+struct Bits;
+template <>
+struct Bits<int> {
+  using T = uint32_t;
+};
+template <>
+struct Bits<float> {
+  using T = uint32_t;
+};
+template <>
+struct Bits<double> {
+  using T = unsigned long long;
+};
+
+template <typename AT, int U, bool NT>
+__global__ __launch_bounds__(kBlock) void k_acc_dense(GroupArgs ga, DenseView d,
+                                                      const uint32_t* flag, uint32_t epoch) {
+  using BT = typename Bits<AT>::T;
+  constexpr int CH = kBlock * 4 * U;
+  if (*flag == epoch) return;  // K6 found a batch that is not a dense window
+  __shared__ uint32_t s_first[kMaxBatches];
+  __shared__ uint32_t s_last[kMaxBatches];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  if (tid < 64) {
+    uint32_t f = 0, l = 0;
+    if (lane < ga.nb) {
+      f = ga.b[lane].keys[0];
+      l = f + (uint32_t)(ga.b[lane].n - 1);
+    }
+    s_first[lane] = f;
+    s_last[lane] = l;
+  }
+  __syncthreads();
+  AT* __restrict__ param = reinterpret_cast<AT*>(d.param);
+  const uint32_t nchunks = ga.wg_prefix[ga.nb];
+  for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int j = batch_of(ga, c);
+    const AT* __restrict__ vals = reinterpret_cast<const AT*>(ga.b[j].vals);
+    const uint64_t n = ga.b[j].n;
+    const uint64_t base = (uint64_t)(c - ga.wg_prefix[j]) * CH;
+    const uint64_t end = n < base + CH ? n : base + CH;
+    const uint32_t first = s_first[j];
+    const uint32_t c_lo = first + (uint32_t)base, c_hi = first + (uint32_t)(end - 1);
+    const bool meets = lane < ga.nb && lane != j && s_first[lane] <= c_hi && s_last[lane] >= c_lo;
+    const unsigned long long earlier = __ballot(meets && lane < j);
+    const unsigned long long later = __ballot(meets && lane > j);
+    // the single RMW of key k, issued by batch j's element when j is the
+    // earliest batch covering k
+    auto rmw = [&](uint32_t k, AT v) {
+      unsigned long long m = earlier;
+      bool owned_earlier = false;
+      while (m) {
+        const int q = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        owned_earlier |= (k >= s_first[q]) & (k <= s_last[q]);
+      }
+      if (owned_earlier) return;
+      const uint32_t off = k - d.key_begin;
+      AT acc = add_wrap<AT>(param[off], v);
+      m = later;
+      while (m) {  // ascending batch index = call order
+        const int q = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        if ((k >= s_first[q]) & (k <= s_last[q]))
+          acc = add_wrap<AT>(acc, reinterpret_cast<const AT*>(ga.b[q].vals)[k - s_first[q]]);
+      }
+      param[off] = acc;
+    };
+    const bool vec_ok = ((reinterpret_cast<uintptr_t>(vals) & 15u) == 0) && end - base == CH;
+    if (vec_ok) {
+      BT v[U][4];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        Vec4<BT>::template load<NT>(reinterpret_cast<const BT*>(vals) + base +
+                                        (uint64_t)(u * kBlock + tid) * 4,
+                                    v[u]);
+      if ((earlier | later) == 0 && ((first - d.key_begin) & 3u) == 0) {
+        // the common case: no other batch meets this chunk, aligned: 16-B RMW
+        BT p[U][4];
+        BT* pb = reinterpret_cast<BT*>(param) + (first - d.key_begin) + base;
+#pragma unroll
+        for (int u = 0; u < U; ++u) Vec4<BT>::load(pb + (uint64_t)(u * kBlock + tid) * 4, p[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            p[u][e] = to_bits<AT>(add_wrap<AT>(from_bits<AT>(p[u][e]), from_bits<AT>(v[u][e])));
+          Vec4<BT>::store(pb + (uint64_t)(u * kBlock + tid) * 4, p[u]);
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t k0 = first + (uint32_t)(base + (uint64_t)(u * kBlock + tid) * 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) rmw(k0 + e, from_bits<AT>(v[u][e]));
+        }
+      }
+    } else {
+      for (uint64_t i = base + tid; i < end; i += kBlock) rmw(first + (uint32_t)i, vals[i]);
+    }
+  }
+}
+
 }  // namespace
 
 // ------------------------------------------------------- launch wrappers
@@ -1202,6 +1357,25 @@ hipError_t launch_rb_add(int dtype, int mode, const GroupArgs& ga, uint32_t nchu
   if (dtype == 0) return rb_launch<int, int, 1>(ga, nchunks, d, o, bshift, nbd, cnt, total, ent, st);
   if (dtype == 1) return rb_launch<float, float, 1>(ga, nchunks, d, o, bshift, nbd, cnt, total, ent, st);
   return rb_launch<double, double, 1>(ga, nchunks, d, o, bshift, nbd, cnt, total, ent, st);
+}
+
+hipError_t launch_dense_check(const GroupArgs& ga, uint32_t nchunks, const DenseView& d,
+                              uint32_t* flag, uint32_t epoch, hipStream_t st) {
+  if (nchunks == 0) return hipSuccess;
+  k_dense_check<8><<<nchunks, kBlock, 0, st>>>(ga, d, flag, epoch);
+  return hipGetLastError();
+}
+
+hipError_t launch_acc_dense(int dtype, const GroupArgs& ga, uint32_t grid, const DenseView& d,
+                            const uint32_t* flag, uint32_t epoch, hipStream_t st) {
+  if (grid == 0) return hipSuccess;
+  if (dtype == 0)
+    k_acc_dense<int, 8, true><<<grid, kBlock, 0, st>>>(ga, d, flag, epoch);
+  else if (dtype == 1)
+    k_acc_dense<float, 8, true><<<grid, kBlock, 0, st>>>(ga, d, flag, epoch);
+  else
+    k_acc_dense<double, 8, true><<<grid, kBlock, 0, st>>>(ga, d, flag, epoch);
+  return hipGetLastError();
 }
 
 size_t rb_entry_bytes() { return sizeof(RbEntry); }

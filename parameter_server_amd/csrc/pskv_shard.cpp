@@ -542,6 +542,32 @@ int sorted_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t
   return PSKV_OK;
 }
 
+// Accumulate over dense windows (K7), one launch group.  `verify`: device
+// inputs under PSKV_SORTED_HINT are first proven dense by K6; if not, K7 skips
+// and the conditional K4a accumulate takes the group.  Host inputs come
+// proven by the CPU check (verify = false).
+int dense_accumulate(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t e,
+                     uint32_t epoch, bool verify) {
+  uint64_t elems = 0;
+  for (size_t i = b; i < e; ++i) elems += v[i].n;
+  GroupArgs ga;
+  const uint32_t nchunks = build_group(v, b, e, stream_chunk(8), &ga);
+  if (verify) {
+    LaunchTimer t(s, PSKV_K_DENSE_CHECK, elems);
+    PSKV_HIP(launch_dense_check(ga, nchunks, s->dview(), s->flag, epoch, s->stream));
+    t.done();
+  }
+  {
+    const uint32_t grid = std::min<uint32_t>(nchunks, s->tune_tile_grid);
+    LaunchTimer t(s, PSKV_K_ACC_DENSE, elems);
+    PSKV_HIP(launch_acc_dense(s->dtype, ga, grid, s->dview(), s->flag, epoch, s->stream));
+    t.done();
+  }
+  s->n_sorted++;
+  if (verify) return general_add(s, v, b, e, epoch, s->flag, /*radix=*/false);
+  return PSKV_OK;
+}
+
 // One contiguous piece of a host->pinned (or pinned->host) copy.
 struct Piece {
   const char* src;
@@ -550,6 +576,7 @@ struct Piece {
   int key_batch;  // >= 0: keys of that batch (checked while copied), -1: values
   // results of the key check
   bool sorted;
+  bool dense;  // every key is its predecessor + 1
   uint32_t first, last;
   uint64_t outside;
 };
@@ -562,7 +589,7 @@ void copy_piece(Piece& p, uint32_t key_begin, uint64_t range) {
   const uint32_t* k = reinterpret_cast<const uint32_t*>(p.src);
   uint32_t* o = reinterpret_cast<uint32_t*>(p.dst);
   const size_t n = p.bytes / 4;
-  bool ok = true;
+  bool ok = true, dense = true;
   uint64_t outside = 0;
   uint32_t prev = n ? k[0] : 0;
   for (size_t i = 0; i < n; ++i) {
@@ -570,9 +597,11 @@ void copy_piece(Piece& p, uint32_t key_begin, uint64_t range) {
     o[i] = x;
     outside += (uint64_t)(uint32_t)(x - key_begin) >= range;
     ok &= prev <= x;
+    dense &= i == 0 || x == prev + 1u;
     prev = x;
   }
   p.sorted = ok;
+  p.dense = dense;
   p.first = n ? k[0] : 0;
   p.last = n ? k[n - 1] : 0;
   p.outside = outside;
@@ -588,6 +617,7 @@ void add_pieces(std::vector<Piece>& out, const void* src, char* dst, size_t byte
     p.bytes = std::min(kPieceBytes, bytes - off);
     p.key_batch = key_batch;
     p.sorted = true;
+    p.dense = true;
     out.push_back(p);
   }
 }
@@ -615,7 +645,7 @@ int pipelined_h2d(pskv_shard* s, std::vector<Piece>& pieces, char* h, char* d) {
 // batch is sorted and inside the dense range.  Returns device batch views.
 int stage_host_batches(pskv_shard* s, const std::vector<pskv_batch>& in,
                        std::vector<pskv_batch>* out, bool* all_sorted_in_range,
-                       uint64_t* n_outside) {
+                       uint64_t* n_outside, bool* all_dense_in_range = nullptr) {
   size_t bytes = 0;
   for (auto& b : in) bytes += round16(b.n * 4) + round16(b.n * (size_t)s->vb);
   int rc = ensure_hstage(s, bytes);
@@ -645,7 +675,7 @@ int stage_host_batches(pskv_shard* s, const std::vector<pskv_batch>& in,
   s->hstage_pending = true;
   // combine the per-piece checks: every piece sorted, and each piece's first
   // key not below the previous piece's last key within the same batch
-  bool ok = true;
+  bool ok = true, dense = true;
   uint64_t outside = 0;
   int prev_batch = -1;
   uint32_t prev_last = 0;
@@ -653,11 +683,16 @@ int stage_host_batches(pskv_shard* s, const std::vector<pskv_batch>& in,
     if (p.key_batch < 0) continue;
     outside += p.outside;
     ok &= p.sorted;
-    if (p.key_batch == prev_batch) ok &= prev_last <= p.first;
+    dense &= p.dense;
+    if (p.key_batch == prev_batch) {
+      ok &= prev_last <= p.first;
+      dense &= p.first == prev_last + 1u;
+    }
     prev_batch = p.key_batch;
     prev_last = p.last;
   }
   *all_sorted_in_range = ok && outside == 0;
+  if (all_dense_in_range) *all_dense_in_range = dense && outside == 0;
   *n_outside = outside;
   return PSKV_OK;
 }
@@ -674,11 +709,11 @@ int add_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
   int rc = use_device(s);
   if (rc) return rc;
   const bool device = (flags & PSKV_DEVICE) != 0;
-  bool host_verified = false;
+  bool host_verified = false, host_dense = false;
   if (!device) {
     std::vector<pskv_batch> staged;
     uint64_t outside = 0;
-    rc = stage_host_batches(s, v, &staged, &host_verified, &outside);
+    rc = stage_host_batches(s, v, &staged, &host_verified, &outside, &host_dense);
     if (rc) return rc;
     if (outside) {
       // exact bound on new overflow keys: grow before the kernels can fill the table
@@ -698,10 +733,17 @@ int add_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
   for (auto& g : split_groups(v)) {
     const uint32_t epoch = next_epoch(s);
     if (s->mode == PSKV_ACCUMULATE) {
-      // order-free, so K4a (LDS sums, one atomic add per distinct key per chunk,
-      // coalesced for sorted chunks) is always correct; it measured faster than
-      // K5 for accumulate on cfg 3 (398 vs 480 us per 8M Zipf keys)
-      rc = general_add(s, v, g.first, g.second, epoch, nullptr, /*radix=*/false);
+      if (!device && host_dense) {
+        // the CPU proved every batch a dense in-range window while staging it
+        rc = dense_accumulate(s, v, g.first, g.second, epoch, /*verify=*/false);
+      } else if (device && (flags & PSKV_SORTED_HINT)) {
+        rc = dense_accumulate(s, v, g.first, g.second, epoch, /*verify=*/true);
+      } else {
+        // order-free, so K4a (LDS sums, one atomic add per distinct key per chunk,
+        // coalesced for sorted chunks) is always correct; it measured faster than
+        // K5 for accumulate on cfg 3 (398 vs 480 us per 8M Zipf keys)
+        rc = general_add(s, v, g.first, g.second, epoch, nullptr, /*radix=*/false);
+      }
     } else if (!device && host_verified) {
       // the CPU proved the batches sorted and in range while staging them
       rc = sorted_add(s, v, g.first, g.second, vec, epoch, /*repair=*/false);

@@ -264,6 +264,90 @@ def test_accumulate_mode(cuda, dt):
         assert np.all(err <= tol), f"max err/tol {np.max(err / np.maximum(tol, 1e-300))}"
 
 
+def _dense_windows(rng, kb, size, n_windows):
+    """Overlapping contiguous key windows inside [kb, kb+size): long ones (many
+    8 Ki-key chunks), short ones, odd lengths and unaligned starts."""
+    out = []
+    for w in range(n_windows):
+        n = int(rng.choice([1, 3, 1000, 8191, 8192, 20_001, 70_000]))
+        first = int(rng.integers(kb, kb + size - n + 1))
+        if w % 3 == 0:
+            first -= (first - kb) % 4  # 4-aligned offset: the 16-byte RMW path
+        out.append(np.arange(first, first + n, dtype=np.uint32))
+    return out
+
+
+@pytest.mark.parametrize("dt", [np.int32, np.float32, np.float64])
+@pytest.mark.parametrize("path", ["host", "device_hint", "device_hint_unaligned"])
+def test_accumulate_dense_windows_sequential_bits(cuda, dt, path):
+    """K7 (dense accumulate): every key gets one RMW summing the covering
+    windows in call order, so the result equals sequential accumulation in the
+    value dtype BIT FOR BIT (np.add.at is sequential, in dtype arithmetic)."""
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(5)
+    kb, size = 1000, 200_000
+    want = np.zeros(size, dt)
+    with ps.Shard(kb, kb + size, dt, mode="accumulate") as sh:
+        sh.set_timing(True)
+        for call in range(4):
+            wins = _dense_windows(rng, kb, size, 9 if call % 2 else 1)
+            vals = [(rng.integers(-2**31, 2**31 - 1, size=k.size, dtype=np.int64).astype(np.int32)
+                     if dt is np.int32 else rng.standard_normal(k.size).astype(dt)) for k in wins]
+            if path == "host":
+                sh.add_grouped(list(zip(wins, vals)))
+            else:
+                off = 1 if path.endswith("unaligned") else 0
+                sh.add_grouped([(tdev(k, cuda), tdev(v, cuda, off)) for k, v in zip(wins, vals)],
+                               sorted_hint=True)
+            for k, v in zip(wins, vals):
+                np.add.at(want, k.astype(np.int64) - kb, v)
+        got = sh.get(np.arange(kb, kb + size, dtype=np.uint32))
+        assert sh.kernel_time(_lib_k("ACC_DENSE"))["launches"] > 0, "dense accumulate kernel did not run"
+        if path != "host":
+            assert sh.kernel_time(_lib_k("DENSE_CHECK"))["launches"] > 0
+    assert_bits_equal(got, want, f"dense accumulate {path}")
+
+
+def _lib_k(name):
+    from parameter_server_amd import _lib
+
+    return getattr(_lib, "PSKV_K_" + name)
+
+
+@pytest.mark.parametrize("dt", [np.int32, np.float32])
+def test_accumulate_dense_lookalike_falls_back(cuda, dt):
+    """A hinted window whose endpoints look dense but whose inside is not (two
+    keys swapped, one key repeated): K6 must reject the group before any RMW,
+    and the K4a accumulate applies it instead (order-free: int32 exact, float
+    within the stated bound)."""
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(9)
+    kb, size = 0, 100_000
+    wins = _dense_windows(rng, kb, size, 6)
+    big = [i for i, k in enumerate(wins) if k.size >= 1000][0]
+    k = wins[big].copy()
+    k[10], k[11] = k[11], k[10]
+    k[500] = k[499]
+    wins[big] = k
+    vals = [(rng.integers(-1000, 1000, size=w.size).astype(np.int32) if dt is np.int32
+             else rng.standard_normal(w.size).astype(dt)) for w in wins]
+    p64, a64, cnt = np.zeros(size), np.zeros(size), np.zeros(size, np.int64)
+    with ps.Shard(kb, kb + size, dt, mode="accumulate") as sh:
+        sh.add_grouped([(tdev(w, cuda), tdev(v, cuda)) for w, v in zip(wins, vals)], sorted_hint=True)
+        got = sh.get(np.arange(kb, kb + size, dtype=np.uint32))
+    for w, v in zip(wins, vals):
+        np.add.at(p64, w.astype(np.int64) - kb, v.astype(np.float64))
+        np.add.at(a64, w.astype(np.int64) - kb, np.abs(v.astype(np.float64)))
+        np.add.at(cnt, w.astype(np.int64) - kb, 1)
+    if dt is np.int32:
+        assert_bits_equal(got, p64.astype(np.int32), "int32 fallback")
+    else:
+        tol = 1.01 * (cnt + 1) * 2.0**-24 * a64
+        assert np.all(np.abs(got.astype(np.float64) - p64) <= tol)
+
+
 def test_baseline_size_dense_roundtrip(cuda):
     """cfg 2 at full size: 1e8-float shard, 1M-key contiguous windows at seed-42
     bases; grouped sorted Add then grouped Get returns the last write of every
