@@ -22,8 +22,8 @@ inline int stream_chunk(int unroll) { return kBlock * 4 * unroll; }  // keys per
 constexpr int kSortedChunk = kBlock * 4 * kSortedUnroll;          // 2048 keys / workgroup
 constexpr int kGeneralChunk = 2048;  // keys per workgroup in the dedup path
 constexpr int kGeneralSlots = 4096;  // LDS hash slots (load factor <= 1/2)
-constexpr int kRbChunk = 2048;       // keys per chunk in the radix-bucket path (K5)
-constexpr int kRbMaxBuckets = 1040;  // key buckets incl. the out-of-range bucket (>= 1025)
+constexpr int kRbChunk = 2048;       // keys per dedup sub-chunk in the radix-bucket path (K5)
+constexpr int kRbMaxBuckets = 2064;  // key buckets incl. the out-of-range bucket (>= 2049)
 constexpr int kRbApplySlots = 16384; // LDS hash slots of a K5 apply workgroup
 constexpr unsigned long long kEmpty64 = ~0ull;
 constexpr uint32_t kEmpty32 = 0xFFFFFFFFu;
@@ -82,12 +82,17 @@ hipError_t launch_general_commit(int vb, const GroupArgs& ga, uint32_t nwg, cons
                                  const uint32_t* cond, uint32_t epoch, hipStream_t st);
 hipError_t launch_ovf_rehash(int vb, const Ovf& from, uint64_t from_cap, const Ovf& to,
                              hipStream_t st);
-// K5 radix-bucket general Add (4 launches).  `ga` chunked by kRbChunk; buckets
-// are key offset >> bshift (nbd dense buckets) plus one out-of-range bucket;
-// cnt: (nbd+1) * nchunks u32, total: nbd+1 u32, ent: one entry per element.
-hipError_t launch_rb_add(int dtype, int mode, const GroupArgs& ga, uint32_t nchunks,
+// K5 radix-bucket general Add (4 launches).  `ga` chunked by
+// rb_superchunk(vb) keys (nsc super-chunks); buckets are key offset >> bshift
+// (nbd dense buckets) plus one out-of-range bucket.  Scratch: cnt, off:
+// nsc * (nbd+1) u32 each; nsub: nsc * 4 u32; total: nbd+1 u32; tmp: nsc *
+// rb_superchunk(vb) entries; ent: one entry per element (rb_entry_bytes(vb) each).
+hipError_t launch_rb_add(int dtype, int mode, const GroupArgs& ga, uint32_t nsc,
                          const DenseView& d, const Ovf& o, uint32_t bshift, uint32_t nbd,
-                         uint32_t* cnt, uint32_t* total, void* ent, hipStream_t st);
+                         uint32_t* cnt, uint32_t* off, uint32_t* nsub, uint32_t* total, void* tmp,
+                         void* ent, hipStream_t st);
+uint32_t rb_superchunk(int vb);
+size_t rb_entry_bytes(int vb);
 // K6: tag `flag` with `epoch` unless every batch is a dense in-range window
 // (chunk = kBlock * 4 * 8 keys per workgroup).
 hipError_t launch_dense_check(const GroupArgs& ga, uint32_t nchunks, const DenseView& d,
@@ -95,6 +100,5 @@ hipError_t launch_dense_check(const GroupArgs& ga, uint32_t nchunks, const Dense
 // K7: accumulate dense windows (skips when flag == epoch); chunk as K6.
 hipError_t launch_acc_dense(int dtype, const GroupArgs& ga, uint32_t grid, const DenseView& d,
                             const uint32_t* flag, uint32_t epoch, hipStream_t st);
-size_t rb_entry_bytes();
 
 }  // namespace pskv

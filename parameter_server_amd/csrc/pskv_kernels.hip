@@ -658,29 +658,47 @@ __global__ __launch_bounds__(kBlock) void k_ovf_rehash(Ovf from, uint64_t from_c
 // one random agent-scope atomic per distinct key per chunk, and those run at
 // ~20 G/s chip-wide (memory-side atomics, MI355X_MICROARCH.md "Global float
 // atomics": 64 lanes in 64 rows ≈ 17x slower).  K5 instead moves the data to
-// where it can be resolved locally:
-//   K5a k_rb_count    per 4096-key chunk: LDS hash dedup (key -> last index /
-//                     sum), histogram of the distinct keys by key bucket
+// where it can be resolved locally.  Work unit: a SUPER-CHUNK of NSUB x 2048
+// keys of one batch; each 2048-key sub-chunk is deduplicated in an LDS hash
+// (clear-on-emit), so a Zipf-hot key yields one entry per sub-chunk.
+//   K5a k_rb_count    per super-chunk: dedup (loads issued one sub-chunk
+//                     ahead), entries {key, value bits} appended to the
+//                     super-chunk's scratch region (one LDS atomic per wave),
+//                     histogram by key bucket -> cnt[sc][bucket]
 //                     (bucket = key offset >> bshift; one extra bucket for
-//                     out-of-range keys) -> cnt[bucket][chunk]
-//   K5b k_rb_scan     one workgroup per bucket: exclusive scan of its row
-//   K5c k_rb_scatter  the same dedup again, each distinct key written as a
-//                     16-byte entry {key, group index, value} to its bucket
+//                     out-of-range keys)
+//   K5b k_rb_scan     exclusive scan over super-chunks per bucket -> off, total
+//   K5c k_rb_move     per super-chunk: counting sort of its entries by bucket
+//                     in LDS, then each bucket's run written to the bucket's
+//                     region (consecutive lanes -> consecutive slots)
 //   K5d k_rb_apply    one workgroup per bucket: an LDS hash resolves the
-//                     bucket's entries (max group index = last write / sum),
-//                     then the winners store (assign) or add (accumulate) into
-//                     the dense array or the overflow table.  A bucket is owned
-//                     by one workgroup, so no cross-workgroup ordering exists.
-// Per-chunk dedup first matters for skew: a Zipf-hot key contributes one
-// entry per chunk, not one per occurrence, so no bucket explodes.
+//                     bucket's entries — an entry's position in its bucket IS
+//                     call order (super-chunks in order, sub-chunks in order),
+//                     so the largest position wins (assign) / values add
+//                     (accumulate) — then the winners store into the dense
+//                     array or the overflow table.  A bucket is owned by one
+//                     workgroup: no cross-workgroup ordering, no global atomics.
 
-struct RbEntry {
+template <int VB>
+struct RbEnt;
+template <>
+struct RbEnt<4> {
   uint32_t key;
-  uint32_t gidx;
-  unsigned long long val;  // value bits (assign) or chunk sum bits (accumulate)
+  uint32_t val;
+};
+template <>
+struct RbEnt<8> {
+  uint32_t key;
+  uint32_t pad;
+  unsigned long long val;
 };
 
 constexpr int kRbChunkSlots = 2 * kRbChunk;  // LDS dedup slots (load <= 1/2)
+constexpr int kRbMoveBlock = 512;             // 8 waves per CU for the LDS counting sort
+template <int VB>
+constexpr int rb_nsub() {
+  return VB == 8 ? 2 : 4;  // sub-chunks per super-chunk (LDS staging budget)
+}
 
 __device__ __forceinline__ uint32_t rb_bucket(const DenseView& d, uint32_t k, uint32_t bshift,
                                               uint32_t nbd) {
@@ -711,17 +729,63 @@ __device__ __forceinline__ T from_bits(unsigned long long b) {
   return *reinterpret_cast<const T*>(&lo);
 }
 
-// LDS state of the chunk dedup.  The table is cleared ONCE per workgroup;
-// afterwards every chunk leaves it empty again: the thread whose CAS inserted
-// a key ("owner") emits that key and resets its slot (clear-on-emit), so the
-// per-chunk LDS work is O(keys), not O(slots).  Slot kRbChunkSlots belongs to
-// the key 0xFFFFFFFF (equal to the EMPTY marker).
+// Block-wide exclusive scan of a[0..n) in LDS, in place (n <= kRbMaxBuckets + 1).
+// Returns the total.  Every thread of the block must call it.
+template <int BLOCK>
+__device__ __forceinline__ uint32_t block_exscan(uint32_t* a, uint32_t n, uint32_t* wtmp) {
+  constexpr int PER = (kRbMaxBuckets + 1 + BLOCK - 1) / BLOCK;
+  constexpr int NW = BLOCK / 64;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t b0 = (uint32_t)tid * PER;
+  uint32_t x[PER];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    x[i] = b0 + i < n ? a[b0 + i] : 0u;
+    sum += x[i];
+  }
+  uint32_t v = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(v, o, 64);
+    if (lane >= o) v += y;
+  }
+  if (lane == 63) wtmp[w] = v;
+  __syncthreads();
+  uint32_t before = 0, tot = 0;
+#pragma unroll
+  for (int q = 0; q < NW; ++q) {
+    if (q < w) before += wtmp[q];
+    tot += wtmp[q];
+  }
+  uint32_t run = before + v - sum;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    if (b0 + i < n) a[b0 + i] = run;
+    run += x[i];
+  }
+  __syncthreads();
+  return tot;
+}
+
+// sbase[b] = exclusive prefix of total[] over buckets, sbase[nbk] = all entries.
+template <int BLOCK>
+__device__ __forceinline__ void rb_bases(const uint32_t* total, uint32_t nbk, uint32_t* sbase,
+                                         uint32_t* wtmp) {
+  for (uint32_t b = threadIdx.x; b <= nbk; b += BLOCK) sbase[b] = b < nbk ? total[b] : 0u;
+  __syncthreads();
+  block_exscan<BLOCK>(sbase, nbk + 1, wtmp);
+}
+
+// LDS state of the sub-chunk dedup.  Cleared ONCE per workgroup; afterwards
+// every sub-chunk leaves it empty again (the emitting lane resets its slot).
+// Slot kRbChunkSlots belongs to the key 0xFFFFFFFF (equal to the EMPTY marker).
 template <typename AT, int MODE>
 struct RbChunkLds {
   uint32_t hk[kRbChunkSlots + 1];
-  uint32_t hlast[MODE == 0 ? kRbChunkSlots + 1 : 1];  // assign: last chunk index
-  AT hsum[MODE == 1 ? kRbChunkSlots + 1 : 1];         // accumulate: chunk sum
-  uint32_t sent_owner;                                 // lane index + 1 owning key 0xFFFFFFFF
+  uint32_t hlast[MODE == 0 ? kRbChunkSlots + 1 : 1];  // assign: last sub-chunk index
+  AT hsum[MODE == 1 ? kRbChunkSlots + 1 : 1];         // accumulate: sub-chunk sum
+  uint32_t sent_owner;                                 // key 0xFFFFFFFF inserted
 };
 
 template <typename AT, int MODE>
@@ -736,38 +800,69 @@ __device__ __forceinline__ void rb_clear_all(RbChunkLds<AT, MODE>& L) {
   if (threadIdx.x == 0) L.sent_owner = 0;
 }
 
-// Insert this lane's RB_PER keys of the chunk; returns per key the slot and
-// whether this lane owns (first inserted) it.  Ends with a barrier.
-constexpr int RB_PER = kRbChunk / kBlock;  // 16 keys per lane
-template <typename AT, int MODE>
-__device__ __forceinline__ void rb_insert(const uint32_t* __restrict__ keys,
-                                          const AT* __restrict__ vals, uint64_t base, uint64_t n,
-                                          RbChunkLds<AT, MODE>& L, uint32_t (&slot)[RB_PER],
-                                          uint32_t (&key)[RB_PER], uint32_t& own_mask) {
+// One lane's share of a sub-chunk: PER/4 groups of 4 consecutive elements.
+template <typename BT, int BLOCK>
+struct RbRegs {
+  static constexpr int PER = kRbChunk / BLOCK;  // keys per lane per sub-chunk
+  uint32_t key[PER];
+  BT val[PER];
+};
+
+// Issue the loads of sub-chunk [base, base + 2048) of a batch (16-byte loads
+// when the sub-chunk is full and aligned).  Elements past n read key 0.
+// NEEDV = false: keys only (the count pass).
+template <typename BT, int BLOCK, bool NEEDV>
+__device__ __forceinline__ void rb_load(const uint32_t* __restrict__ keys,
+                                        const BT* __restrict__ vals, uint64_t base, uint64_t n,
+                                        RbRegs<BT, BLOCK>& r) {
+  constexpr int PER = RbRegs<BT, BLOCK>::PER;
   const int tid = threadIdx.x;
-  own_mask = 0;
-  // lane keys: 4 groups of 4 consecutive keys (16-byte loads when the chunk is full)
-  const bool full = base + kRbChunk <= n && ((reinterpret_cast<uintptr_t>(keys) & 15u) == 0);
+  const bool full = base + kRbChunk <= n && ((reinterpret_cast<uintptr_t>(keys) & 15u) == 0) &&
+                    (!NEEDV || (reinterpret_cast<uintptr_t>(vals) & 15u) == 0);
 #pragma unroll
-  for (int g = 0; g < RB_PER / 4; ++g) {
-    const uint64_t i0 = base + (uint64_t)(g * kBlock + tid) * 4;
+  for (int g = 0; g < PER / 4; ++g) {
+    const uint64_t i0 = base + (uint64_t)(g * BLOCK + tid) * 4;
     if (full) {
       uint32_t k4[4];
       Vec4<uint32_t>::template load<true>(keys + i0, k4);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) key[g * 4 + e] = k4[e];
+      for (int e = 0; e < 4; ++e) r.key[g * 4 + e] = k4[e];
+      if (NEEDV) {
+        BT v4[4];
+        Vec4<BT>::template load<true>(vals + i0, v4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) r.val[g * 4 + e] = v4[e];
+      }
     } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) key[g * 4 + e] = i0 + e < n ? keys[i0 + e] : 0u;
+      for (int e = 0; e < 4; ++e) {
+        const bool in = i0 + e < n;
+        r.key[g * 4 + e] = in ? keys[i0 + e] : 0u;
+        if (NEEDV) r.val[g * 4 + e] = in ? vals[i0 + e] : BT(0);
+      }
     }
   }
+}
+
+// Dedup one sub-chunk held in registers and call emit(key, value bits) once
+// per distinct key: assign — the LAST occurrence emits its own value;
+// accumulate — the first inserter emits the sub-chunk sum; COUNT — the first
+// inserter emits (no values).  Starts and ends with the LDS table empty;
+// contains the barriers it needs (and one at the end).
+template <typename AT, typename BT, int MODE, int BLOCK, bool COUNT, typename Emit>
+__device__ __forceinline__ void rb_dedup(const RbRegs<BT, BLOCK>& r, uint32_t nvalid,
+                                         RbChunkLds<AT, MODE>& L, Emit&& emit) {
+  constexpr int PER = RbRegs<BT, BLOCK>::PER;
+  const int tid = threadIdx.x;
+  uint32_t slot[PER];
+  uint32_t own_mask = 0;
 #pragma unroll
-  for (int q = 0; q < RB_PER; ++q) {
+  for (int q = 0; q < PER; ++q) {
     const int g = q / 4, e = q % 4;
-    const uint32_t li = (uint32_t)((g * kBlock + tid) * 4 + e);
+    const uint32_t li = (uint32_t)((g * BLOCK + tid) * 4 + e);
     slot[q] = kEmpty32;
-    if (base + li >= n) continue;
-    const uint32_t k = key[q];
+    if (li >= nvalid) continue;
+    const uint32_t k = r.key[q];
     uint32_t h;
     bool own = false;
     if (k == kEmpty32) {
@@ -787,168 +882,282 @@ __device__ __forceinline__ void rb_insert(const uint32_t* __restrict__ keys,
     }
     slot[q] = h;
     own_mask |= own ? (1u << q) : 0u;
+    if (COUNT) continue;
     if (MODE == 0)
       atomicMax(&L.hlast[h], li);
     else
-      atomicAdd(&L.hsum[h], vals[base + li]);
+      atomicAdd(&L.hsum[h], from_bits<AT>(to_bits<BT>(r.val[q])));
+  }
+  __syncthreads();
+  if (MODE == 0 && !COUNT) {
+    uint32_t last_mask = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const uint32_t li = (uint32_t)(((q / 4) * BLOCK + tid) * 4 + (q % 4));
+      if (slot[q] != kEmpty32 && L.hlast[slot[q]] == li) last_mask |= 1u << q;
+    }
+    __syncthreads();  // every lane has read hlast before the emitters reset it
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      if (!(last_mask >> q & 1u)) continue;
+      const uint32_t h = slot[q];
+      L.hlast[h] = 0;
+      if (h == kRbChunkSlots)
+        L.sent_owner = 0;
+      else
+        L.hk[h] = kEmpty32;
+      emit(r.key[q], to_bits<BT>(r.val[q]));
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      if (!(own_mask >> q & 1u)) continue;
+      const uint32_t h = slot[q];
+      unsigned long long vb = 0;
+      if (!COUNT && MODE == 1) {
+        vb = to_bits<AT>(L.hsum[h]);
+        L.hsum[h] = AT(0);
+      }
+      if (h == kRbChunkSlots)
+        L.sent_owner = 0;
+      else
+        L.hk[h] = kEmpty32;
+      emit(r.key[q], vb);
+    }
   }
   __syncthreads();
 }
 
-// Owner lanes read their keys' result and reset the slots.
-template <typename AT, int MODE>
-__device__ __forceinline__ void rb_take(RbChunkLds<AT, MODE>& L, uint32_t h, uint32_t* last,
-                                        AT* sum) {
-  if (MODE == 0) {
-    *last = L.hlast[h];
-    L.hlast[h] = 0;
-  } else {
-    *sum = L.hsum[h];
-    L.hsum[h] = AT(0);
-  }
-  if (h == kRbChunkSlots)
-    L.sent_owner = 0;
-  else
-    L.hk[h] = kEmpty32;
+// Sub-chunk schedule of a workgroup: super-chunks blockIdx.x, +gridDim.x, ...,
+// each NSUB sub-chunks (those past the end of the batch are skipped).
+struct RbTask {
+  uint32_t sc;
+  uint32_t s;
+  int j;
+  uint64_t base;  // first element of the sub-chunk in batch j
+  uint32_t nvalid;
+};
+
+template <int NSUB>
+__device__ __forceinline__ bool rb_task(const GroupArgs& ga, uint32_t nsc, uint32_t sc, uint32_t s,
+                                        RbTask& t) {
+  if (sc >= nsc) return false;
+  t.sc = sc;
+  t.s = s;
+  t.j = batch_of(ga, sc);
+  t.base = (uint64_t)(sc - ga.wg_prefix[t.j]) * (kRbChunk * NSUB) + (uint64_t)s * kRbChunk;
+  const uint64_t n = ga.b[t.j].n;
+  t.nvalid = t.base >= n ? 0u : (uint32_t)(n - t.base < kRbChunk ? n - t.base : kRbChunk);
+  return true;
 }
 
-template <typename AT, int MODE>
+// Allocate one slot per calling lane from an LDS counter with one atomic per
+// wave (call from divergent code: the active lanes get consecutive slots).
+__device__ __forceinline__ uint32_t wave_alloc(uint32_t* counter) {
+  const unsigned long long m = __ballot(1);
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((long long)m) - 1;
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+  base = __shfl(base, leader, 64);
+  return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+}
+
+// K5a: per super-chunk, dedup each sub-chunk and append its entries to the
+// super-chunk's region of `tmp` (arrival order, coalesced by wave); histogram
+// of the entries by bucket -> cnt[sc][b]; entries after sub-chunk s -> nsub[sc][s].
+template <typename AT, typename BT, int MODE>
 __global__ __launch_bounds__(kBlock) void k_rb_count(GroupArgs ga, DenseView d, uint32_t bshift,
                                                      uint32_t nbd, uint32_t nbk, uint32_t* cnt,
-                                                     uint32_t nchunks) {
+                                                     uint32_t* nsub, uint32_t nsc,
+                                                     RbEnt<sizeof(BT)>* __restrict__ tmp) {
+  constexpr int NSUB = rb_nsub<sizeof(BT)>();
+  constexpr int SC = NSUB * kRbChunk;
   __shared__ RbChunkLds<AT, MODE> L;
   __shared__ uint32_t hist[kRbMaxBuckets];
+  __shared__ uint32_t nent;
   const int tid = threadIdx.x;
   rb_clear_all(L);
   for (uint32_t b = tid; b < nbk; b += kBlock) hist[b] = 0;
+  if (tid == 0) nent = 0;
   __syncthreads();
-  for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-    const int j = batch_of(ga, c);
-    const uint64_t base = (uint64_t)(c - ga.wg_prefix[j]) * kRbChunk;
-    uint32_t slot[RB_PER], key[RB_PER], own;
-    rb_insert<AT, MODE>(ga.b[j].keys, reinterpret_cast<const AT*>(ga.b[j].vals), base, ga.b[j].n,
-                        L, slot, key, own);
-#pragma unroll
-    for (int q = 0; q < RB_PER; ++q) {
-      if (!(own >> q & 1u)) continue;
-      uint32_t last;
-      AT sum;
-      rb_take(L, slot[q], &last, &sum);
-      atomicAdd(&hist[rb_bucket(d, key[q], bshift, nbd)], 1u);
+  RbTask cur, nxt;
+  RbRegs<BT, kBlock> rc, rn;
+  bool have = rb_task<NSUB>(ga, nsc, blockIdx.x, 0, cur);
+  if (have)
+    rb_load<BT, kBlock, true>(ga.b[cur.j].keys, reinterpret_cast<const BT*>(ga.b[cur.j].vals),
+                              cur.base, ga.b[cur.j].n, rc);
+  while (have) {
+    // next sub-chunk of this super-chunk, else the first of the next one
+    bool hn = cur.s + 1 < NSUB && rb_task<NSUB>(ga, nsc, cur.sc, cur.s + 1, nxt) && nxt.nvalid > 0;
+    if (!hn) hn = rb_task<NSUB>(ga, nsc, cur.sc + gridDim.x, 0, nxt);
+    if (hn)
+      rb_load<BT, kBlock, true>(ga.b[nxt.j].keys, reinterpret_cast<const BT*>(ga.b[nxt.j].vals),
+                                nxt.base, ga.b[nxt.j].n, rn);
+    RbEnt<sizeof(BT)>* out = tmp + (uint64_t)cur.sc * SC;
+    rb_dedup<AT, BT, MODE, kBlock, false>(rc, cur.nvalid, L, [&](uint32_t k, unsigned long long vb) {
+      atomicAdd(&hist[rb_bucket(d, k, bshift, nbd)], 1u);
+      RbEnt<sizeof(BT)> e;
+      e.key = k;
+      if (sizeof(BT) == 8) reinterpret_cast<uint32_t*>(&e)[1] = 0;
+      e.val = (BT)vb;
+      out[wave_alloc(&nent)] = e;
+    });
+    const bool last = !hn || nxt.sc != cur.sc;
+    if (tid == 0) {
+      // sub-chunks never reached (past the batch end) repeat the final count
+      for (uint32_t s = cur.s; s < (last ? (uint32_t)NSUB : cur.s + 1); ++s)
+        nsub[(uint64_t)cur.sc * NSUB + s] = nent;
     }
-    __syncthreads();
-    for (uint32_t b = tid; b < nbk; b += kBlock) {
-      cnt[(uint64_t)b * nchunks + c] = hist[b];
-      hist[b] = 0;
-    }
-    __syncthreads();
-  }
-}
-
-// One workgroup per bucket: exclusive scan of cnt[b][*] in place, total[b].
-// Coalesced: tiles of 256 consecutive entries, wave scans via shuffles.
-__global__ __launch_bounds__(kBlock) void k_rb_scan(uint32_t* cnt, uint32_t nchunks,
-                                                    uint32_t* total) {
-  __shared__ uint32_t wsum[kBlock / 64];
-  uint32_t* row = cnt + (uint64_t)blockIdx.x * nchunks;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  uint32_t carry = 0;
-  for (uint32_t t0 = 0; t0 < nchunks; t0 += kBlock) {
-    const uint32_t i = t0 + tid;
-    const uint32_t x = i < nchunks ? row[i] : 0u;
-    uint32_t v = x;  // inclusive wave scan
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(v, o, 64);
-      if (lane >= o) v += y;
-    }
-    if (lane == 63) wsum[w] = v;
-    __syncthreads();
-    uint32_t before = carry, tile = 0;
-#pragma unroll
-    for (int q = 0; q < kBlock / 64; ++q) {
-      if (q < w) before += wsum[q];
-      tile += wsum[q];
-    }
-    if (i < nchunks) row[i] = before + v - x;
-    carry += tile;
-    __syncthreads();
-  }
-  if (tid == 0) total[blockIdx.x] = carry;
-}
-
-// Exclusive prefix of the bucket totals into LDS (nbk <= kRbMaxBuckets).
-__device__ __forceinline__ void rb_bases(const uint32_t* total, uint32_t nbk, uint32_t* sbase) {
-  if (threadIdx.x == 0) {
-    uint32_t acc = 0;
-    for (uint32_t b = 0; b < nbk; ++b) {
-      sbase[b] = acc;
-      acc += total[b];
-    }
-    sbase[nbk] = acc;
-  }
-  __syncthreads();
-}
-
-template <typename AT, typename VT, int MODE>
-__global__ __launch_bounds__(kBlock) void k_rb_scatter(GroupArgs ga, DenseView d, uint32_t bshift,
-                                                       uint32_t nbd, uint32_t nbk,
-                                                       const uint32_t* cnt, uint32_t nchunks,
-                                                       const uint32_t* total, RbEntry* ent) {
-  __shared__ RbChunkLds<AT, MODE> L;
-  __shared__ uint32_t sbase[kRbMaxBuckets + 1];
-  __shared__ uint32_t cur[kRbMaxBuckets];
-  const int tid = threadIdx.x;
-  rb_clear_all(L);
-  rb_bases(total, nbk, sbase);
-  for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-    const int j = batch_of(ga, c);
-    const uint64_t base = (uint64_t)(c - ga.wg_prefix[j]) * kRbChunk;
-    const uint64_t gbase = ga.elem_prefix[j] + base;
-    for (uint32_t b = tid; b < nbk; b += kBlock) cur[b] = sbase[b] + cnt[(uint64_t)b * nchunks + c];
-    uint32_t slot[RB_PER], key[RB_PER], own;
-    rb_insert<AT, MODE>(ga.b[j].keys, reinterpret_cast<const AT*>(ga.b[j].vals), base, ga.b[j].n,
-                        L, slot, key, own);
-#pragma unroll
-    for (int q = 0; q < RB_PER; ++q) {
-      if (!(own >> q & 1u)) continue;
-      uint32_t last = 0;
-      AT sum = AT(0);
-      rb_take(L, slot[q], &last, &sum);
-      const uint32_t dst = atomicAdd(&cur[rb_bucket(d, key[q], bshift, nbd)], 1u);
-      RbEntry e;
-      e.key = key[q];
-      if (MODE == 0) {
-        e.gidx = (uint32_t)(gbase + last);
-        e.val = to_bits<VT>(reinterpret_cast<const VT*>(ga.b[j].vals)[base + last]);
-      } else {
-        e.gidx = 0;
-        e.val = to_bits<AT>(sum);
+    if (last) {  // super-chunk done: publish its histogram (a contiguous row)
+      for (uint32_t b = tid; b < nbk; b += kBlock) {
+        cnt[(uint64_t)cur.sc * nbk + b] = hist[b];
+        hist[b] = 0;
       }
-      ent[dst] = e;
+      __syncthreads();
+      if (tid == 0) nent = 0;
+      __syncthreads();
+    }
+    have = hn;
+    cur = nxt;
+    rc = rn;
+  }
+}
+
+// K5b: per block of 64 buckets (one lane each), exclusive scan over the
+// super-chunks: off[sc][b] = sum of cnt[s][b] for s < sc; total[b].  16 waves
+// split the super-chunk range; rows are read 256 B at a time (coalesced).
+constexpr int kScanBlock = 1024;
+__global__ __launch_bounds__(kScanBlock) void k_rb_scan(const uint32_t* __restrict__ cnt,
+                                                        uint32_t* __restrict__ off, uint32_t nsc,
+                                                        uint32_t nbk, uint32_t* total) {
+  constexpr int NW = kScanBlock / 64;
+  __shared__ uint32_t part[NW][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t b = blockIdx.x * 64 + lane;
+  const uint32_t seg = (nsc + NW - 1) / NW;
+  const uint32_t s0 = w * seg < nsc ? w * seg : nsc;
+  const uint32_t s1 = s0 + seg < nsc ? s0 + seg : nsc;
+  uint32_t sum = 0;
+  if (b < nbk) {
+#pragma unroll 8
+    for (uint32_t s = s0; s < s1; ++s) sum += cnt[(uint64_t)s * nbk + b];
+  }
+  part[w][lane] = sum;
+  __syncthreads();
+  uint32_t run = 0, tot = 0;
+#pragma unroll
+  for (int q = 0; q < NW; ++q) {
+    if (q < w) run += part[q][lane];
+    tot += part[q][lane];
+  }
+  if (b < nbk) {
+#pragma unroll 8
+    for (uint32_t s = s0; s < s1; ++s) {
+      const uint32_t x = cnt[(uint64_t)s * nbk + b];
+      off[(uint64_t)s * nbk + b] = run;
+      run += x;
+    }
+    if (w == 0) total[b] = tot;
+  }
+}
+
+// K5c: per super-chunk, counting-sort its entries by bucket in LDS and write
+// each bucket's run to the bucket's region: consecutive lanes write
+// consecutive slots.  Sub-chunks are ranked one after another (barrier), so in
+// a bucket the entries of sub-chunk s precede those of s+1 (call order).
+template <typename BT, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_rb_move(DenseView d, uint32_t bshift, uint32_t nbd,
+                                                   uint32_t nbk, const uint32_t* __restrict__ cnt,
+                                                   const uint32_t* __restrict__ off,
+                                                   const uint32_t* __restrict__ nsub, uint32_t nsc,
+                                                   const uint32_t* total,
+                                                   const RbEnt<sizeof(BT)>* __restrict__ tmp,
+                                                   RbEnt<sizeof(BT)>* __restrict__ ent) {
+  constexpr int NSUB = rb_nsub<sizeof(BT)>();
+  constexpr int SC = NSUB * kRbChunk;
+  constexpr int EPT = SC / BLOCK;
+  using Ent = RbEnt<sizeof(BT)>;
+  __shared__ uint32_t sbase[kRbMaxBuckets + 1];
+  __shared__ uint32_t loff[kRbMaxBuckets + 1];
+  __shared__ uint32_t lcur[kRbMaxBuckets];
+  __shared__ uint32_t goff[kRbMaxBuckets];
+  __shared__ uint32_t skey[SC];
+  __shared__ BT sval[SC];
+  __shared__ uint32_t wtmp[BLOCK / 64];
+  const int tid = threadIdx.x;
+  rb_bases<BLOCK>(total, nbk, sbase, wtmp);
+  for (uint32_t sc = blockIdx.x; sc < nsc; sc += gridDim.x) {
+    uint32_t ends[NSUB];
+#pragma unroll
+    for (int s = 0; s < NSUB; ++s) ends[s] = nsub[(uint64_t)sc * NSUB + s];
+    const uint32_t n = ends[NSUB - 1];
+    // all loads up front: the super-chunk's entries, this lane's EPT of them
+    Ent x[EPT];
+    const Ent* src = tmp + (uint64_t)sc * SC;
+#pragma unroll
+    for (int q = 0; q < EPT; ++q) {
+      const uint32_t i = (uint32_t)(q * BLOCK + tid);
+      if (i < n) x[q] = src[i];
+    }
+    for (uint32_t b = tid; b < nbk; b += BLOCK) {
+      loff[b] = cnt[(uint64_t)sc * nbk + b];
+      goff[b] = sbase[b] + off[(uint64_t)sc * nbk + b];
+    }
+    __syncthreads();
+    block_exscan<BLOCK>(loff, nbk, wtmp);
+    for (uint32_t b = tid; b < nbk; b += BLOCK) lcur[b] = loff[b];
+    __syncthreads();
+    uint32_t lo = 0;
+#pragma unroll
+    for (int s = 0; s < NSUB; ++s) {
+      const uint32_t hi = ends[s];
+#pragma unroll
+      for (int q = 0; q < EPT; ++q) {
+        const uint32_t i = (uint32_t)(q * BLOCK + tid);
+        if (i < lo || i >= hi) continue;
+        const uint32_t p = atomicAdd(&lcur[rb_bucket(d, x[q].key, bshift, nbd)], 1u);
+        skey[p] = x[q].key;
+        sval[p] = (BT)x[q].val;
+      }
+      __syncthreads();
+      lo = hi;
+    }
+    for (uint32_t t = tid; t < n; t += BLOCK) {
+      const uint32_t k = skey[t];
+      const uint32_t b = rb_bucket(d, k, bshift, nbd);
+      Ent e;
+      e.key = k;
+      if (sizeof(BT) == 8) reinterpret_cast<uint32_t*>(&e)[1] = 0;
+      e.val = sval[t];
+      ent[goff[b] + (t - loff[b])] = e;
     }
     __syncthreads();
   }
 }
 
-// One 1024-thread workgroup per bucket (LDS: 128 KiB table, one workgroup per
-// CU, 16 waves).  Slot S-1 is reserved for the key 0xFFFFFFFF (probing of other
-// keys wraps before it).  The host sizes buckets for ~8 Ki entries, so one
-// round suffices; rounds split a bucket by key hash only when its entry count
-// could overfill the table (entries >= distinct keys).
+// K5d: one 1024-thread workgroup per bucket (LDS: 128 KiB table, one workgroup
+// per CU, 16 waves).  Slot S-1 is reserved for the key 0xFFFFFFFF (probing of
+// other keys wraps before it).  A bucket whose entries fit the table (the host
+// sizes buckets for that) is resolved from registers in one pass, the next
+// bucket's entries loading meanwhile; otherwise rounds split it by key hash.
 constexpr int kApplyBlock = 1024;
-template <typename AT, typename VT, int MODE>
+template <typename AT, typename BT, int MODE>
 __global__ __launch_bounds__(kApplyBlock) void k_rb_apply(DenseView d, Ovf o, uint32_t nbd,
                                                           uint32_t nbk, const uint32_t* total,
-                                                          const RbEntry* __restrict__ ent) {
+                                                          const RbEnt<sizeof(BT)>* __restrict__ ent) {
   constexpr int S = (MODE == 1 && sizeof(AT) == 8) ? kRbApplySlots / 2 : kRbApplySlots;
+  constexpr uint32_t CAP = (uint32_t)(S - 1) / 8 * 7;  // entries per round (load <= 7/8)
+  constexpr int EPT = (int)((CAP + kApplyBlock - 1) / kApplyBlock);
+  using Ent = RbEnt<sizeof(BT)>;
   __shared__ uint32_t ak[S];
-  __shared__ uint32_t abest[MODE == 0 ? S : 1];  // assign: 1 + max group index (0 = none)
+  __shared__ uint32_t abest[MODE == 0 ? S : 1];  // assign: 1 + max position (0 = none)
   __shared__ AT asum[MODE == 1 ? S : 1];
   __shared__ uint32_t sbase[kRbMaxBuckets + 1];
+  __shared__ uint32_t wtmp[kApplyBlock / 64];
   __shared__ uint32_t sent;
   const int tid = threadIdx.x;
-  rb_bases(total, nbk, sbase);
+  rb_bases<kApplyBlock>(total, nbk, sbase, wtmp);
   auto probe = [&](uint32_t key, bool insert) -> uint32_t {
     if (key == kEmpty32) return S - 1;
     uint32_t h = fmix32(key) % (S - 1);
@@ -962,65 +1171,118 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_apply(DenseView d, Ovf o, ui
       h = h + 1 == S - 1 ? 0 : h + 1;
     }
   };
-  for (uint32_t b = blockIdx.x; b < nbk; b += gridDim.x) {
-    const uint32_t e0 = sbase[b], e1 = sbase[b + 1];
-    if (e0 == e1) continue;
-    const uint32_t cap = (uint32_t)(S - 1) / 8 * 7;
-    const uint32_t R = (e1 - e0 + cap - 1) / cap;
-    for (uint32_t round = 0; round < R; ++round) {
-      for (int s = tid; s < S; s += kApplyBlock) {
-        ak[s] = kEmpty32;
-        if (MODE == 0)
-          abest[s] = 0;
-        else
-          asum[s] = AT(0);
+  auto store_winner = [&](uint32_t b, uint32_t key, BT vbits) {
+    const AT v = from_bits<AT>(to_bits<BT>(vbits));
+    if (b != nbd) {
+      reinterpret_cast<AT*>(d.param)[key - d.key_begin] = v;
+    } else {
+      const long long sl = ovf_insert(o, key);
+      if (sl >= 0) reinterpret_cast<AT*>(o.vals)[sl] = v;
+    }
+  };
+  auto accumulate_all = [&](uint32_t b) {
+    // this workgroup owns every key of the bucket: plain read-modify-write
+    for (int s = tid; s < S; s += kApplyBlock) {
+      const bool used = s == S - 1 ? sent != 0 : ak[s] != kEmpty32;
+      if (!used) continue;
+      const uint32_t key = s == S - 1 ? kEmpty32 : ak[s];
+      AT* p;
+      if (b != nbd) {
+        p = reinterpret_cast<AT*>(d.param) + (uint32_t)(key - d.key_begin);
+      } else {
+        const long long sl = ovf_insert(o, key);
+        if (sl < 0) continue;
+        p = reinterpret_cast<AT*>(o.vals) + sl;
       }
-      if (tid == 0) sent = 0;
+      *p = add_wrap<AT>(*p, asum[s]);
+    }
+  };
+  auto clear_table = [&]() {
+    for (int s = tid; s < S; s += kApplyBlock) {
+      ak[s] = kEmpty32;
+      if (MODE == 0)
+        abest[s] = 0;
+      else
+        asum[s] = AT(0);
+    }
+    if (tid == 0) sent = 0;
+  };
+  // entries of bucket b held in registers: x[q] = entry q * kApplyBlock + tid
+  auto load_bucket = [&](uint32_t b, Ent (&x)[EPT]) {
+    const uint32_t e0 = sbase[b], ne = sbase[b + 1] - e0;
+    if (ne > CAP) return;
+#pragma unroll
+    for (int q = 0; q < EPT; ++q) {
+      const uint32_t p = (uint32_t)(q * kApplyBlock + tid);
+      if (p < ne) x[q] = ent[e0 + p];
+    }
+  };
+  Ent xc[EPT], xn[EPT];
+  uint32_t b = blockIdx.x;
+  if (b < nbk) load_bucket(b, xc);
+  for (; b < nbk; b += gridDim.x) {
+    const uint32_t e0 = sbase[b], e1 = sbase[b + 1];
+    const uint32_t ne = e1 - e0;
+    const uint32_t bn = b + gridDim.x;
+    if (bn < nbk) load_bucket(bn, xn);  // in flight while this bucket resolves
+    if (ne == 0) {
+    } else if (ne <= CAP) {
+      clear_table();
       __syncthreads();
-      for (uint32_t e = e0 + tid; e < e1; e += kApplyBlock) {
-        const RbEntry x = ent[e];
-        if (R > 1 && (fmix32(x.key ^ 0x9E3779B9u) % R) != round) continue;
-        const uint32_t h = probe(x.key, true);
-        if (x.key == kEmpty32) sent = 1;
+      uint32_t slot[EPT];
+#pragma unroll
+      for (int q = 0; q < EPT; ++q) {
+        const uint32_t p = (uint32_t)(q * kApplyBlock + tid);
+        if (p >= ne) continue;
+        slot[q] = probe(xc[q].key, true);
+        if (xc[q].key == kEmpty32) sent = 1;
         if (MODE == 0)
-          atomicMax(&abest[h], x.gidx + 1u);
+          atomicMax(&abest[slot[q]], p + 1u);
         else
-          atomicAdd(&asum[h], from_bits<AT>(x.val));
+          atomicAdd(&asum[slot[q]], from_bits<AT>(to_bits<BT>((BT)xc[q].val)));
       }
       __syncthreads();
       if (MODE == 0) {
-        // the entry holding its key's largest group index is the last write
-        for (uint32_t e = e0 + tid; e < e1; e += kApplyBlock) {
-          const RbEntry x = ent[e];
-          if (R > 1 && (fmix32(x.key ^ 0x9E3779B9u) % R) != round) continue;
-          if (abest[probe(x.key, false)] != x.gidx + 1u) continue;
-          const VT v = from_bits<VT>(x.val);
-          if (b != nbd) {
-            reinterpret_cast<VT*>(d.param)[x.key - d.key_begin] = v;
-          } else {
-            const long long sl = ovf_insert(o, x.key);
-            if (sl >= 0) reinterpret_cast<VT*>(o.vals)[sl] = v;
-          }
+#pragma unroll
+        for (int q = 0; q < EPT; ++q) {
+          const uint32_t p = (uint32_t)(q * kApplyBlock + tid);
+          if (p < ne && abest[slot[q]] == p + 1u) store_winner(b, xc[q].key, (BT)xc[q].val);
         }
       } else {
-        // this workgroup owns every key of the bucket: plain read-modify-write
-        for (int s = tid; s < S; s += kApplyBlock) {
-          const bool used = s == S - 1 ? sent != 0 : ak[s] != kEmpty32;
-          if (!used) continue;
-          const uint32_t key = s == S - 1 ? kEmpty32 : ak[s];
-          AT* p;
-          if (b != nbd) {
-            p = reinterpret_cast<AT*>(d.param) + (uint32_t)(key - d.key_begin);
-          } else {
-            const long long sl = ovf_insert(o, key);
-            if (sl < 0) continue;
-            p = reinterpret_cast<AT*>(o.vals) + sl;
-          }
-          *p = add_wrap<AT>(*p, asum[s]);
-        }
+        accumulate_all(b);
       }
       __syncthreads();
+    } else {
+      const uint32_t R = (ne + CAP - 1) / CAP;
+      for (uint32_t round = 0; round < R; ++round) {
+        clear_table();
+        __syncthreads();
+        for (uint32_t p = tid; p < ne; p += kApplyBlock) {
+          const Ent x = ent[e0 + p];
+          if ((fmix32(x.key ^ 0x9E3779B9u) % R) != round) continue;
+          const uint32_t h = probe(x.key, true);
+          if (x.key == kEmpty32) sent = 1;
+          if (MODE == 0)
+            atomicMax(&abest[h], p + 1u);
+          else
+            atomicAdd(&asum[h], from_bits<AT>(to_bits<BT>((BT)x.val)));
+        }
+        __syncthreads();
+        if (MODE == 0) {
+          // the entry holding its key's largest position is the last write
+          for (uint32_t p = tid; p < ne; p += kApplyBlock) {
+            const Ent x = ent[e0 + p];
+            if ((fmix32(x.key ^ 0x9E3779B9u) % R) != round) continue;
+            if (abest[probe(x.key, false)] == p + 1u) store_winner(b, x.key, (BT)x.val);
+          }
+        } else {
+          accumulate_all(b);
+        }
+        __syncthreads();
+      }
     }
+#pragma unroll
+    for (int q = 0; q < EPT; ++q) xc[q] = xn[q];
   }
 }
 
@@ -1118,6 +1380,8 @@ __global__ __launch_bounds__(kBlock) void k_acc_dense(GroupArgs ga, DenseView d,
     const bool meets = lane < ga.nb && lane != j && s_first[lane] <= c_hi && s_last[lane] >= c_lo;
     const unsigned long long earlier = __ballot(meets && lane < j);
     const unsigned long long later = __ballot(meets && lane > j);
+    // an earlier batch covering the whole chunk owns every key: nothing to load
+    if (__ballot(meets && lane < j && s_first[lane] <= c_lo && s_last[lane] >= c_hi)) continue;
     // the single RMW of key k, issued by batch j's element when j is the
     // earliest batch covering k
     auto rmw = [&](uint32_t k, AT v) {
@@ -1148,8 +1412,9 @@ __global__ __launch_bounds__(kBlock) void k_acc_dense(GroupArgs ga, DenseView d,
         Vec4<BT>::template load<NT>(reinterpret_cast<const BT*>(vals) + base +
                                         (uint64_t)(u * kBlock + tid) * 4,
                                     v[u]);
-      if ((earlier | later) == 0 && ((first - d.key_begin) & 3u) == 0) {
-        // the common case: no other batch meets this chunk, aligned: 16-B RMW
+      if (earlier == 0 && ((first - d.key_begin) & 3u) == 0) {
+        // no earlier batch meets this chunk (the common case), aligned: 16-B
+        // RMW; later batches meeting it add their values in call order
         BT p[U][4];
         BT* pb = reinterpret_cast<BT*>(param) + (first - d.key_begin) + base;
 #pragma unroll
@@ -1159,8 +1424,32 @@ __global__ __launch_bounds__(kBlock) void k_acc_dense(GroupArgs ga, DenseView d,
 #pragma unroll
           for (int e = 0; e < 4; ++e)
             p[u][e] = to_bits<AT>(add_wrap<AT>(from_bits<AT>(p[u][e]), from_bits<AT>(v[u][e])));
-          Vec4<BT>::store(pb + (uint64_t)(u * kBlock + tid) * 4, p[u]);
         }
+        unsigned long long m = later;
+        while (m) {
+          const int q = __ffsll((long long)m) - 1;
+          m &= m - 1;
+          const uint32_t fq = s_first[q], lq = s_last[q];
+          const BT* __restrict__ vq = reinterpret_cast<const BT*>(ga.b[q].vals);
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const uint32_t k0 = first + (uint32_t)(base + (uint64_t)(u * kBlock + tid) * 4);
+            BT w[4];
+            if (k0 >= fq && k0 + 3u <= lq && (((k0 - fq) & 3u) | (reinterpret_cast<uintptr_t>(vq) & 15u)) == 0) {
+              Vec4<BT>::template load<NT>(vq + (k0 - fq), w);
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                p[u][e] = to_bits<AT>(add_wrap<AT>(from_bits<AT>(p[u][e]), from_bits<AT>(w[e])));
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                if (k0 + e >= fq && k0 + e <= lq)
+                  p[u][e] = to_bits<AT>(add_wrap<AT>(from_bits<AT>(p[u][e]), from_bits<AT>(vq[k0 + e - fq])));
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) Vec4<BT>::store(pb + (uint64_t)(u * kBlock + tid) * 4, p[u]);
       } else {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -1330,33 +1619,40 @@ hipError_t launch_ovf_rehash(int vb, const Ovf& from, uint64_t from_cap, const O
   return hipGetLastError();
 }
 
-template <typename AT, typename VT, int MODE>
-static hipError_t rb_launch(const GroupArgs& ga, uint32_t nchunks, const DenseView& d, const Ovf& o,
-                            uint32_t bshift, uint32_t nbd, uint32_t* cnt, uint32_t* total,
-                            void* ent, hipStream_t st) {
+template <typename AT, typename BT, int MODE>
+static hipError_t rb_launch(const GroupArgs& ga, uint32_t nsc, const DenseView& d, const Ovf& o,
+                            uint32_t bshift, uint32_t nbd, uint32_t* cnt, uint32_t* off,
+                            uint32_t* nsub, uint32_t* total, void* tmp, void* ent, hipStream_t st) {
   const uint32_t nbk = nbd + 1;
-  const uint32_t g = nchunks < 1024u ? nchunks : 1024u;  // persistent: LDS cleared once per WG
-  RbEntry* e = reinterpret_cast<RbEntry*>(ent);
-  k_rb_count<AT, MODE><<<g, kBlock, 0, st>>>(ga, d, bshift, nbd, nbk, cnt, nchunks);
-  k_rb_scan<<<nbk, kBlock, 0, st>>>(cnt, nchunks, total);
-  k_rb_scatter<AT, VT, MODE><<<g, kBlock, 0, st>>>(ga, d, bshift, nbd, nbk, cnt, nchunks, total, e);
-  k_rb_apply<AT, VT, MODE><<<nbk, kApplyBlock, 0, st>>>(d, o, nbd, nbk, total, e);
+  // persistent grids: the dedup LDS is cleared once per workgroup
+  const uint32_t gc = nsc < 768u ? nsc : 768u;   // ~41 KiB LDS: 3 workgroups per CU
+  const uint32_t gm = nsc < 512u ? nsc : 512u;   // ~90 KiB LDS
+  auto* t = reinterpret_cast<RbEnt<sizeof(BT)>*>(tmp);
+  auto* e = reinterpret_cast<RbEnt<sizeof(BT)>*>(ent);
+  k_rb_count<AT, BT, MODE><<<gc, kBlock, 0, st>>>(ga, d, bshift, nbd, nbk, cnt, nsub, nsc, t);
+  k_rb_scan<<<(nbk + 63) / 64, kScanBlock, 0, st>>>(cnt, off, nsc, nbk, total);
+  k_rb_move<BT, kRbMoveBlock><<<gm, kRbMoveBlock, 0, st>>>(d, bshift, nbd, nbk, cnt, off, nsub, nsc,
+                                                           total, t, e);
+  k_rb_apply<AT, BT, MODE><<<nbk < 256u ? nbk : 256u, kApplyBlock, 0, st>>>(d, o, nbd, nbk, total, e);
   return hipGetLastError();
 }
 
-hipError_t launch_rb_add(int dtype, int mode, const GroupArgs& ga, uint32_t nchunks,
+hipError_t launch_rb_add(int dtype, int mode, const GroupArgs& ga, uint32_t nsc,
                          const DenseView& d, const Ovf& o, uint32_t bshift, uint32_t nbd,
-                         uint32_t* cnt, uint32_t* total, void* ent, hipStream_t st) {
-  if (nchunks == 0) return hipSuccess;
+                         uint32_t* cnt, uint32_t* off, uint32_t* nsub, uint32_t* total, void* tmp,
+                         void* ent, hipStream_t st) {
+  if (nsc == 0) return hipSuccess;
   if (nbd + 1 > (uint32_t)kRbMaxBuckets) return hipErrorInvalidValue;
+#define PSKV_RB(AT, BT, M) rb_launch<AT, BT, M>(ga, nsc, d, o, bshift, nbd, cnt, off, nsub, total, tmp, ent, st)
   if (mode == 0) {
-    if (dtype == 2)
-      return rb_launch<uint32_t, unsigned long long, 0>(ga, nchunks, d, o, bshift, nbd, cnt, total, ent, st);
-    return rb_launch<uint32_t, uint32_t, 0>(ga, nchunks, d, o, bshift, nbd, cnt, total, ent, st);
+    if (dtype == 0) return PSKV_RB(int, uint32_t, 0);
+    if (dtype == 1) return PSKV_RB(float, uint32_t, 0);
+    return PSKV_RB(double, unsigned long long, 0);
   }
-  if (dtype == 0) return rb_launch<int, int, 1>(ga, nchunks, d, o, bshift, nbd, cnt, total, ent, st);
-  if (dtype == 1) return rb_launch<float, float, 1>(ga, nchunks, d, o, bshift, nbd, cnt, total, ent, st);
-  return rb_launch<double, double, 1>(ga, nchunks, d, o, bshift, nbd, cnt, total, ent, st);
+  if (dtype == 0) return PSKV_RB(int, uint32_t, 1);
+  if (dtype == 1) return PSKV_RB(float, uint32_t, 1);
+  return PSKV_RB(double, unsigned long long, 1);
+#undef PSKV_RB
 }
 
 hipError_t launch_dense_check(const GroupArgs& ga, uint32_t nchunks, const DenseView& d,
@@ -1378,6 +1674,9 @@ hipError_t launch_acc_dense(int dtype, const GroupArgs& ga, uint32_t grid, const
   return hipGetLastError();
 }
 
-size_t rb_entry_bytes() { return sizeof(RbEntry); }
+// Super-chunk size (keys) and entry size of the K5 path for a value size.
+uint32_t rb_superchunk(int vb) { return vb == 8 ? 2 * kRbChunk : 4 * kRbChunk; }
+size_t rb_entry_bytes(int vb) { return vb == 8 ? sizeof(RbEnt<8>) : sizeof(RbEnt<4>); }
+
 
 }  // namespace pskv

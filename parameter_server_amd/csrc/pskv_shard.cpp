@@ -227,6 +227,7 @@ struct pskv_shard {
   int tune_unroll = 8;   // PSKV_UNROLL: 4 or 8 (8: measured +5 % on the dense Add)
   bool tune_nt = true;   // PSKV_NT: non-temporal streams (measured +12-15 % on K1 / K2g)
   bool tune_ntp = false; // PSKV_NTP: non-temporal parameter stores (dense Add)
+  uint32_t tune_rb_tb = 0; // PSKV_RB_TB: K5 bucket bits (0 = by element count)
 
   DenseView dview() const { return DenseView{dense, key_begin, range}; }
 };
@@ -447,28 +448,36 @@ int ensure_scratch(pskv_shard* s, void** p, size_t* have, size_t need) {
 // K5: radix-bucket general Add (no random global atomics).
 int radix_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t e) {
   GroupArgs ga;
-  const uint32_t nchunks = build_group(v, b, e, kRbChunk, &ga);
+  const uint32_t nsc = build_group(v, b, e, rb_superchunk(s->vb), &ga);
   uint64_t elems = 0;
   for (size_t i = b; i < e; ++i) elems += v[i].n;
-  // bucket = key offset >> bshift, sized for ~8 Ki entries per bucket (one
-  // apply round) and at most 1024 dense buckets
+  // bucket = key offset >> bshift: about one bucket per 4 Ki pushed keys (an
+  // apply workgroup resolves up to ~14 Ki entries in one register-resident
+  // pass), at most 2048 dense buckets
   uint32_t bits = 0;
   while (bits < 32 && ((s->range - 1) >> bits) != 0) ++bits;
   uint32_t tb = 6;
-  while (tb < 10 && (elems >> (13 + tb)) != 0) ++tb;
+  while (tb < 11 && (elems >> (12 + tb)) != 0) ++tb;
+  if (s->tune_rb_tb) tb = s->tune_rb_tb;
   const uint32_t bshift = bits > tb ? bits - tb : 0;
   const uint32_t nbd = (uint32_t)(((s->range - 1) >> bshift) + 1);
   const uint32_t nbk = nbd + 1;
+  if (nbk > (uint32_t)kRbMaxBuckets) return fail(PSKV_EINVAL, "radix path: too many buckets");
   size_t have_total = s->rb_total ? 4 * (size_t)kRbMaxBuckets : 0;
+  const size_t eb = rb_entry_bytes(s->vb);
+  const size_t nb2 = (size_t)nbk * nsc;
   int rc = ensure_scratch(s, reinterpret_cast<void**>(&s->rb_cnt), &s->rb_cnt_bytes,
-                          (size_t)nbk * nchunks * sizeof(uint32_t));
+                          (2 * nb2 + 4 * (size_t)nsc) * sizeof(uint32_t));
   if (!rc) rc = ensure_scratch(s, reinterpret_cast<void**>(&s->rb_total), &have_total,
                                (size_t)kRbMaxBuckets * sizeof(uint32_t));
-  if (!rc) rc = ensure_scratch(s, &s->rb_ent, &s->rb_ent_bytes, elems * rb_entry_bytes());
+  if (!rc) rc = ensure_scratch(s, &s->rb_ent, &s->rb_ent_bytes,
+                               (elems + (size_t)nsc * rb_superchunk(s->vb)) * eb);
   if (rc) return rc;
+  char* ent = static_cast<char*>(s->rb_ent);
   LaunchTimer t(s, PSKV_K_RADIX, elems);
-  PSKV_HIP(launch_rb_add(s->dtype, s->mode, ga, nchunks, s->dview(), s->ovf, bshift, nbd,
-                         s->rb_cnt, s->rb_total, s->rb_ent, s->stream));
+  PSKV_HIP(launch_rb_add(s->dtype, s->mode, ga, nsc, s->dview(), s->ovf, bshift, nbd, s->rb_cnt,
+                         s->rb_cnt + nb2, s->rb_cnt + 2 * nb2, s->rb_total,
+                         ent + elems * eb, ent, s->stream));
   t.done();
   s->n_general += 4;
   return PSKV_OK;
@@ -739,10 +748,10 @@ int add_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
       } else if (device && (flags & PSKV_SORTED_HINT)) {
         rc = dense_accumulate(s, v, g.first, g.second, epoch, /*verify=*/true);
       } else {
-        // order-free, so K4a (LDS sums, one atomic add per distinct key per chunk,
-        // coalesced for sorted chunks) is always correct; it measured faster than
-        // K5 for accumulate on cfg 3 (398 vs 480 us per 8M Zipf keys)
-        rc = general_add(s, v, g.first, g.second, epoch, nullptr, /*radix=*/false);
+        // K5 (no global atomics) measured faster than K4a (LDS sums + one
+        // atomic add per distinct key per chunk) on cfg 3: 322 vs 380 us per
+        // 8M Zipf keys; PSKV_GENERAL=stamps selects K4a
+        rc = general_add(s, v, g.first, g.second, epoch, nullptr);
       }
     } else if (!device && host_verified) {
       // the CPU proved the batches sorted and in range while staging them
@@ -905,6 +914,10 @@ int pskv_shard_create_ex(int device, uint32_t key_begin, uint64_t key_end, int d
   if (const char* e = std::getenv("PSKV_TILE_GRID")) {
     const int v = std::atoi(e);
     if (v >= 1 && v <= 65536) s->tune_tile_grid = (uint32_t)v;
+  }
+  if (const char* e = std::getenv("PSKV_RB_TB")) {
+    const int v = std::atoi(e);
+    if (v >= 1 && v <= 11) s->tune_rb_tb = (uint32_t)v;
   }
   auto bail = [&](int rc) {
     pskv_shard_destroy(s);

@@ -574,3 +574,30 @@ def test_general_path_stamps_variant_matches(cuda, oracle_mod, monkeypatch):
         q = np.arange(0, 520_000, dtype=np.uint32)
         got = sh.get(q)
     assert_bits_equal(got, ref.get(q), "stamps path")
+
+
+@pytest.mark.parametrize("dtype", [np.int32, np.float32])
+def test_accumulate_stamps_variant_k4a(cuda, monkeypatch, dtype):
+    """K4a accumulate (LDS chunk sums + one atomic add per distinct key per
+    chunk), selected by PSKV_GENERAL=stamps: int32 exact, float within bound."""
+    import parameter_server_amd as ps
+
+    monkeypatch.setenv("PSKV_GENERAL", "stamps")
+    rng = np.random.default_rng(67)
+    size = 300_000
+    p64, a64, cnt = np.zeros(size), np.zeros(size), np.zeros(size, np.int64)
+    with ps.Shard(0, size, dtype, mode="accumulate") as sh:
+        for _ in range(3):
+            k = (rng.zipf(1.3, size=120_000) % size).astype(np.uint32)
+            v = (rng.integers(-1000, 1000, size=k.size).astype(np.int32) if dtype is np.int32
+                 else rng.standard_normal(k.size).astype(dtype))
+            sh.add(tdev(k, cuda), tdev(v, cuda))
+            np.add.at(p64, k.astype(np.int64), v.astype(np.float64))
+            np.add.at(a64, k.astype(np.int64), np.abs(v.astype(np.float64)))
+            np.add.at(cnt, k.astype(np.int64), 1)
+        got = sh.get(np.arange(size, dtype=np.uint32))
+    if dtype is np.int32:
+        assert_bits_equal(got, p64.astype(np.int32), "k4a int32")
+    else:
+        tol = 1.01 * (cnt + 1) * 2.0**-24 * a64
+        assert np.all(np.abs(got.astype(np.float64) - p64) <= tol)
