@@ -844,86 +844,122 @@ __device__ __forceinline__ void rb_load(const uint32_t* __restrict__ keys,
   }
 }
 
-// Dedup one sub-chunk held in registers and call emit(key, value bits) once
-// per distinct key: assign — the LAST occurrence emits its own value;
-// accumulate — the first inserter emits the sub-chunk sum; COUNT — the first
-// inserter emits (no values).  Starts and ends with the LDS table empty;
-// contains the barriers it needs (and one at the end).
-template <typename AT, typename BT, int MODE, int BLOCK, bool COUNT, typename Emit>
-__device__ __forceinline__ void rb_dedup(const RbRegs<BT, BLOCK>& r, uint32_t nvalid,
-                                         RbChunkLds<AT, MODE>& L, Emit&& emit) {
-  constexpr int PER = RbRegs<BT, BLOCK>::PER;
-  const int tid = threadIdx.x;
-  uint32_t slot[PER];
-  uint32_t own_mask = 0;
+// Insert this lane's keys into an LDS open-addressing table (linear probing,
+// SLOTS a power of two; the key 0xFFFFFFFF uses the side word *sent).  The
+// first probe of every key is issued back to back (independent LDS atomics in
+// flight); only keys that met another key probe further.  slot[q] = EMPTY for
+// invalid keys; own bit q = this lane inserted the key.
+template <int PER, int SLOTS>
+__device__ __forceinline__ uint32_t lds_insert(uint32_t* hk, uint32_t* sent,
+                                               const uint32_t (&key)[PER], uint32_t valid_mask,
+                                               uint32_t (&slot)[PER]) {
+  uint32_t old[PER];
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
-    const int g = q / 4, e = q % 4;
-    const uint32_t li = (uint32_t)((g * BLOCK + tid) * 4 + e);
     slot[q] = kEmpty32;
-    if (li >= nvalid) continue;
-    const uint32_t k = r.key[q];
-    uint32_t h;
-    bool own = false;
-    if (k == kEmpty32) {
-      h = kRbChunkSlots;
-      own = atomicCAS(&L.sent_owner, 0u, 1u) == 0u;
+    old[q] = 0;
+    if (!(valid_mask >> q & 1u)) continue;
+    if (key[q] == kEmpty32) {
+      slot[q] = SLOTS;
+      old[q] = atomicCAS(sent, 0u, 1u) == 0u ? kEmpty32 : key[q];
     } else {
-      h = fmix32(k) & (kRbChunkSlots - 1);
-      for (;;) {
-        const uint32_t old = atomicCAS(&L.hk[h], kEmpty32, k);
-        if (old == kEmpty32) {
-          own = true;
-          break;
-        }
-        if (old == k) break;
-        h = (h + 1) & (kRbChunkSlots - 1);
-      }
+      slot[q] = fmix32(key[q]) & (SLOTS - 1);
+      old[q] = atomicCAS(&hk[slot[q]], kEmpty32, key[q]);
+    }
+  }
+  uint32_t own = 0;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    if (!(valid_mask >> q & 1u)) continue;
+    uint32_t o = old[q], h = slot[q];
+    while (o != kEmpty32 && o != key[q]) {  // collision: probe on
+      h = (h + 1) & (SLOTS - 1);
+      o = atomicCAS(&hk[h], kEmpty32, key[q]);
     }
     slot[q] = h;
-    own_mask |= own ? (1u << q) : 0u;
-    if (COUNT) continue;
+    own |= o == kEmpty32 ? (1u << q) : 0u;
+  }
+  return own;
+}
+
+// Wave-wide exclusive prefix of a per-lane count; *total = the wave's sum.
+__device__ __forceinline__ uint32_t wave_exscan(uint32_t x, uint32_t* total) {
+  const int lane = threadIdx.x & 63;
+  uint32_t v = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(v, o, 64);
+    if (lane >= o) v += y;
+  }
+  *total = __shfl(v, 63, 64);
+  return v - x;
+}
+
+// Dedup one sub-chunk held in registers and append one entry per distinct key
+// to out[] (slots from the LDS counter *nent, one atomic per wave) and to the
+// bucket histogram: assign — the LAST occurrence supplies its own value;
+// accumulate — the first inserter supplies the sub-chunk sum.  Starts and ends
+// with the LDS table empty; contains the barriers it needs (one at the end).
+template <typename AT, typename BT, int MODE, int BLOCK>
+__device__ __forceinline__ void rb_dedup(const RbRegs<BT, BLOCK>& r, uint32_t nvalid,
+                                         RbChunkLds<AT, MODE>& L, uint32_t* hist, uint32_t* nent,
+                                         RbEnt<sizeof(BT)>* __restrict__ out, const DenseView& d,
+                                         uint32_t bshift, uint32_t nbd) {
+  constexpr int PER = RbRegs<BT, BLOCK>::PER;
+  const int tid = threadIdx.x;
+  auto li_of = [&](int q) { return (uint32_t)(((q / 4) * BLOCK + tid) * 4 + (q % 4)); };
+  uint32_t valid = 0;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) valid |= li_of(q) < nvalid ? (1u << q) : 0u;
+  uint32_t slot[PER];
+  const uint32_t own = lds_insert<PER, kRbChunkSlots>(L.hk, &L.sent_owner, r.key, valid, slot);
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    if (!(valid >> q & 1u)) continue;
     if (MODE == 0)
-      atomicMax(&L.hlast[h], li);
+      atomicMax(&L.hlast[slot[q]], li_of(q));
     else
-      atomicAdd(&L.hsum[h], from_bits<AT>(to_bits<BT>(r.val[q])));
+      atomicAdd(&L.hsum[slot[q]], from_bits<AT>(to_bits<BT>(r.val[q])));
   }
   __syncthreads();
-  if (MODE == 0 && !COUNT) {
-    uint32_t last_mask = 0;
+  uint32_t emask = own;
+  unsigned long long vb[PER];
+  if (MODE == 0) {
+    emask = 0;
 #pragma unroll
-    for (int q = 0; q < PER; ++q) {
-      const uint32_t li = (uint32_t)(((q / 4) * BLOCK + tid) * 4 + (q % 4));
-      if (slot[q] != kEmpty32 && L.hlast[slot[q]] == li) last_mask |= 1u << q;
-    }
-    __syncthreads();  // every lane has read hlast before the emitters reset it
+    for (int q = 0; q < PER; ++q)
+      if ((valid >> q & 1u) && L.hlast[slot[q]] == li_of(q)) emask |= 1u << q;
 #pragma unroll
-    for (int q = 0; q < PER; ++q) {
-      if (!(last_mask >> q & 1u)) continue;
-      const uint32_t h = slot[q];
-      L.hlast[h] = 0;
-      if (h == kRbChunkSlots)
-        L.sent_owner = 0;
-      else
-        L.hk[h] = kEmpty32;
-      emit(r.key[q], to_bits<BT>(r.val[q]));
-    }
+    for (int q = 0; q < PER; ++q) vb[q] = to_bits<BT>(r.val[q]);
   } else {
 #pragma unroll
-    for (int q = 0; q < PER; ++q) {
-      if (!(own_mask >> q & 1u)) continue;
-      const uint32_t h = slot[q];
-      unsigned long long vb = 0;
-      if (!COUNT && MODE == 1) {
-        vb = to_bits<AT>(L.hsum[h]);
-        L.hsum[h] = AT(0);
-      }
-      if (h == kRbChunkSlots)
-        L.sent_owner = 0;
-      else
-        L.hk[h] = kEmpty32;
-      emit(r.key[q], vb);
-    }
+    for (int q = 0; q < PER; ++q) vb[q] = (own >> q & 1u) ? to_bits<AT>(L.hsum[slot[q]]) : 0ull;
+  }
+  __syncthreads();  // every lane has read the table before the slots are reset
+  // one allocation per wave for all of its entries
+  uint32_t wtot;
+  const uint32_t mine = wave_exscan((uint32_t)__popc(emask), &wtot);
+  uint32_t base = 0;
+  if ((tid & 63) == 63 && wtot) base = atomicAdd(nent, wtot);
+  base = __shfl(base, 63, 64) + mine;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    if (!(emask >> q & 1u)) continue;
+    const uint32_t h = slot[q];
+    if (MODE == 0)
+      L.hlast[h] = 0;
+    else
+      L.hsum[h] = AT(0);
+    if (h == kRbChunkSlots)
+      L.sent_owner = 0;
+    else
+      L.hk[h] = kEmpty32;
+    atomicAdd(&hist[rb_bucket(d, r.key[q], bshift, nbd)], 1u);
+    RbEnt<sizeof(BT)> e;
+    e.key = r.key[q];
+    if (sizeof(BT) == 8) reinterpret_cast<uint32_t*>(&e)[1] = 0;
+    e.val = (BT)vb[q];
+    out[base++] = e;
   }
   __syncthreads();
 }
@@ -967,14 +1003,14 @@ __device__ __forceinline__ uint32_t wave_alloc(uint32_t* counter) {
 // super-chunk's region of `tmp` (arrival order, coalesced by wave); histogram
 // of the entries by bucket -> cnt[sc][b]; entries after sub-chunk s -> nsub[sc][s].
 template <typename AT, typename BT, int MODE>
-__global__ __launch_bounds__(kBlock) void k_rb_count(GroupArgs ga, DenseView d, uint32_t bshift,
-                                                     uint32_t nbd, uint32_t nbk, uint32_t* cnt,
-                                                     uint32_t* nsub, uint32_t nsc,
-                                                     RbEnt<sizeof(BT)>* __restrict__ tmp) {
+__global__ __launch_bounds__(kBlock, 4) void k_rb_count(GroupArgs ga, DenseView d, uint32_t bshift,
+                                                        uint32_t nbd, uint32_t nbk, uint32_t* cnt,
+                                                        uint32_t* nsub, uint32_t nsc,
+                                                        RbEnt<sizeof(BT)>* __restrict__ tmp) {
   constexpr int NSUB = rb_nsub<sizeof(BT)>();
   constexpr int SC = NSUB * kRbChunk;
   __shared__ RbChunkLds<AT, MODE> L;
-  __shared__ uint32_t hist[kRbMaxBuckets];
+  extern __shared__ uint32_t hist[];  // nbk words (dynamic: 4 workgroups per CU fit)
   __shared__ uint32_t nent;
   const int tid = threadIdx.x;
   rb_clear_all(L);
@@ -994,15 +1030,8 @@ __global__ __launch_bounds__(kBlock) void k_rb_count(GroupArgs ga, DenseView d, 
     if (hn)
       rb_load<BT, kBlock, true>(ga.b[nxt.j].keys, reinterpret_cast<const BT*>(ga.b[nxt.j].vals),
                                 nxt.base, ga.b[nxt.j].n, rn);
-    RbEnt<sizeof(BT)>* out = tmp + (uint64_t)cur.sc * SC;
-    rb_dedup<AT, BT, MODE, kBlock, false>(rc, cur.nvalid, L, [&](uint32_t k, unsigned long long vb) {
-      atomicAdd(&hist[rb_bucket(d, k, bshift, nbd)], 1u);
-      RbEnt<sizeof(BT)> e;
-      e.key = k;
-      if (sizeof(BT) == 8) reinterpret_cast<uint32_t*>(&e)[1] = 0;
-      e.val = (BT)vb;
-      out[wave_alloc(&nent)] = e;
-    });
+    rb_dedup<AT, BT, MODE, kBlock>(rc, cur.nvalid, L, hist, &nent, tmp + (uint64_t)cur.sc * SC, d,
+                                   bshift, nbd);
     const bool last = !hn || nxt.sc != cur.sc;
     if (tid == 0) {
       // sub-chunks never reached (past the batch end) repeat the final count
@@ -1137,39 +1166,32 @@ __global__ __launch_bounds__(BLOCK) void k_rb_move(DenseView d, uint32_t bshift,
 }
 
 // K5d: one 1024-thread workgroup per bucket (LDS: 128 KiB table, one workgroup
-// per CU, 16 waves).  Slot S-1 is reserved for the key 0xFFFFFFFF (probing of
-// other keys wraps before it).  A bucket whose entries fit the table (the host
-// sizes buckets for that) is resolved from registers in one pass, the next
-// bucket's entries loading meanwhile; otherwise rounds split it by key hash.
+// per CU, 16 waves).  Slot SLOTS belongs to the key 0xFFFFFFFF.  A bucket whose
+// entries fit the table (the host sizes buckets for that) is resolved from
+// registers in one pass, the next bucket's entries loading meanwhile;
+// otherwise rounds split it by key hash.
 constexpr int kApplyBlock = 1024;
 template <typename AT, typename BT, int MODE>
 __global__ __launch_bounds__(kApplyBlock) void k_rb_apply(DenseView d, Ovf o, uint32_t nbd,
                                                           uint32_t nbk, const uint32_t* total,
                                                           const RbEnt<sizeof(BT)>* __restrict__ ent) {
-  constexpr int S = (MODE == 1 && sizeof(AT) == 8) ? kRbApplySlots / 2 : kRbApplySlots;
-  constexpr uint32_t CAP = (uint32_t)(S - 1) / 8 * 7;  // entries per round (load <= 7/8)
+  constexpr int SLOTS = (MODE == 1 && sizeof(AT) == 8) ? kRbApplySlots / 2 : kRbApplySlots;
+  constexpr uint32_t CAP = (uint32_t)SLOTS / 8 * 7;  // entries per round (load <= 7/8)
   constexpr int EPT = (int)((CAP + kApplyBlock - 1) / kApplyBlock);
   using Ent = RbEnt<sizeof(BT)>;
-  __shared__ uint32_t ak[S];
-  __shared__ uint32_t abest[MODE == 0 ? S : 1];  // assign: 1 + max position (0 = none)
-  __shared__ AT asum[MODE == 1 ? S : 1];
+  __shared__ uint32_t ak[SLOTS + 1];
+  __shared__ uint32_t abest[MODE == 0 ? SLOTS + 1 : 1];  // assign: 1 + max position (0 = none)
+  __shared__ AT asum[MODE == 1 ? SLOTS + 1 : 1];
   __shared__ uint32_t sbase[kRbMaxBuckets + 1];
   __shared__ uint32_t wtmp[kApplyBlock / 64];
   __shared__ uint32_t sent;
   const int tid = threadIdx.x;
   rb_bases<kApplyBlock>(total, nbk, sbase, wtmp);
-  auto probe = [&](uint32_t key, bool insert) -> uint32_t {
-    if (key == kEmpty32) return S - 1;
-    uint32_t h = fmix32(key) % (S - 1);
-    for (;;) {
-      if (insert) {
-        const uint32_t old = atomicCAS(&ak[h], kEmpty32, key);
-        if (old == kEmpty32 || old == key) return h;
-      } else if (ak[h] == key) {
-        return h;
-      }
-      h = h + 1 == S - 1 ? 0 : h + 1;
-    }
+  auto find = [&](uint32_t key) -> uint32_t {
+    if (key == kEmpty32) return SLOTS;
+    uint32_t h = fmix32(key) & (SLOTS - 1);
+    while (ak[h] != key) h = (h + 1) & (SLOTS - 1);
+    return h;
   };
   auto store_winner = [&](uint32_t b, uint32_t key, BT vbits) {
     const AT v = from_bits<AT>(to_bits<BT>(vbits));
@@ -1182,10 +1204,10 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_apply(DenseView d, Ovf o, ui
   };
   auto accumulate_all = [&](uint32_t b) {
     // this workgroup owns every key of the bucket: plain read-modify-write
-    for (int s = tid; s < S; s += kApplyBlock) {
-      const bool used = s == S - 1 ? sent != 0 : ak[s] != kEmpty32;
+    for (int s = tid; s <= SLOTS; s += kApplyBlock) {
+      const bool used = s == SLOTS ? sent != 0 : ak[s] != kEmpty32;
       if (!used) continue;
-      const uint32_t key = s == S - 1 ? kEmpty32 : ak[s];
+      const uint32_t key = s == SLOTS ? kEmpty32 : ak[s];
       AT* p;
       if (b != nbd) {
         p = reinterpret_cast<AT*>(d.param) + (uint32_t)(key - d.key_begin);
@@ -1198,7 +1220,7 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_apply(DenseView d, Ovf o, ui
     }
   };
   auto clear_table = [&]() {
-    for (int s = tid; s < S; s += kApplyBlock) {
+    for (int s = tid; s <= SLOTS; s += kApplyBlock) {
       ak[s] = kEmpty32;
       if (MODE == 0)
         abest[s] = 0;
@@ -1229,15 +1251,18 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_apply(DenseView d, Ovf o, ui
     } else if (ne <= CAP) {
       clear_table();
       __syncthreads();
-      uint32_t slot[EPT];
+      uint32_t key[EPT], slot[EPT], valid = 0;
 #pragma unroll
       for (int q = 0; q < EPT; ++q) {
-        const uint32_t p = (uint32_t)(q * kApplyBlock + tid);
-        if (p >= ne) continue;
-        slot[q] = probe(xc[q].key, true);
-        if (xc[q].key == kEmpty32) sent = 1;
+        key[q] = xc[q].key;
+        valid |= (uint32_t)(q * kApplyBlock + tid) < ne ? (1u << q) : 0u;
+      }
+      lds_insert<EPT, SLOTS>(ak, &sent, key, valid, slot);
+#pragma unroll
+      for (int q = 0; q < EPT; ++q) {
+        if (!(valid >> q & 1u)) continue;
         if (MODE == 0)
-          atomicMax(&abest[slot[q]], p + 1u);
+          atomicMax(&abest[slot[q]], (uint32_t)(q * kApplyBlock + tid) + 1u);
         else
           atomicAdd(&asum[slot[q]], from_bits<AT>(to_bits<BT>((BT)xc[q].val)));
       }
@@ -1246,7 +1271,7 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_apply(DenseView d, Ovf o, ui
 #pragma unroll
         for (int q = 0; q < EPT; ++q) {
           const uint32_t p = (uint32_t)(q * kApplyBlock + tid);
-          if (p < ne && abest[slot[q]] == p + 1u) store_winner(b, xc[q].key, (BT)xc[q].val);
+          if ((valid >> q & 1u) && abest[slot[q]] == p + 1u) store_winner(b, key[q], (BT)xc[q].val);
         }
       } else {
         accumulate_all(b);
@@ -1260,12 +1285,12 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_apply(DenseView d, Ovf o, ui
         for (uint32_t p = tid; p < ne; p += kApplyBlock) {
           const Ent x = ent[e0 + p];
           if ((fmix32(x.key ^ 0x9E3779B9u) % R) != round) continue;
-          const uint32_t h = probe(x.key, true);
-          if (x.key == kEmpty32) sent = 1;
+          uint32_t k1[1] = {x.key}, s1[1];
+          lds_insert<1, SLOTS>(ak, &sent, k1, 1u, s1);
           if (MODE == 0)
-            atomicMax(&abest[h], p + 1u);
+            atomicMax(&abest[s1[0]], p + 1u);
           else
-            atomicAdd(&asum[h], from_bits<AT>(to_bits<BT>((BT)x.val)));
+            atomicAdd(&asum[s1[0]], from_bits<AT>(to_bits<BT>((BT)x.val)));
         }
         __syncthreads();
         if (MODE == 0) {
@@ -1273,7 +1298,7 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_apply(DenseView d, Ovf o, ui
           for (uint32_t p = tid; p < ne; p += kApplyBlock) {
             const Ent x = ent[e0 + p];
             if ((fmix32(x.key ^ 0x9E3779B9u) % R) != round) continue;
-            if (abest[probe(x.key, false)] == p + 1u) store_winner(b, x.key, (BT)x.val);
+            if (abest[find(x.key)] == p + 1u) store_winner(b, x.key, (BT)x.val);
           }
         } else {
           accumulate_all(b);
@@ -1285,7 +1310,6 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_apply(DenseView d, Ovf o, ui
     for (int q = 0; q < EPT; ++q) xc[q] = xn[q];
   }
 }
-
 
 // ------------------------------------------- K6/K7 dense accumulate
 // Accumulate for grouped batches that are each one contiguous key window
@@ -1625,11 +1649,11 @@ static hipError_t rb_launch(const GroupArgs& ga, uint32_t nsc, const DenseView& 
                             uint32_t* nsub, uint32_t* total, void* tmp, void* ent, hipStream_t st) {
   const uint32_t nbk = nbd + 1;
   // persistent grids: the dedup LDS is cleared once per workgroup
-  const uint32_t gc = nsc < 768u ? nsc : 768u;   // ~41 KiB LDS: 3 workgroups per CU
+  const uint32_t gc = nsc < 1024u ? nsc : 1024u;  // <= 40 KiB LDS, <= 128 VGPRs: 4 per CU
   const uint32_t gm = nsc < 512u ? nsc : 512u;   // ~90 KiB LDS
   auto* t = reinterpret_cast<RbEnt<sizeof(BT)>*>(tmp);
   auto* e = reinterpret_cast<RbEnt<sizeof(BT)>*>(ent);
-  k_rb_count<AT, BT, MODE><<<gc, kBlock, 0, st>>>(ga, d, bshift, nbd, nbk, cnt, nsub, nsc, t);
+  k_rb_count<AT, BT, MODE><<<gc, kBlock, nbk * sizeof(uint32_t), st>>>(ga, d, bshift, nbd, nbk, cnt, nsub, nsc, t);
   k_rb_scan<<<(nbk + 63) / 64, kScanBlock, 0, st>>>(cnt, off, nsc, nbk, total);
   k_rb_move<BT, kRbMoveBlock><<<gm, kRbMoveBlock, 0, st>>>(d, bshift, nbd, nbk, cnt, off, nsub, nsc,
                                                            total, t, e);
