@@ -335,6 +335,24 @@ def side_measurements(dev, B):
     out["e2e_host_buffers"] = {"workload": "8 x 1M contiguous float keys from pageable host memory, Add then Get "
                                            "(H2D + kernels + D2H, host sortedness check included)",
                                "GB/s": (add_b + get_b) * reps / dt / 1e9}
+    # the same from page-locked buffers (zmq frames received into pinned memory,
+    # SURVEY §8f-3): direct DMA, no staging copy
+    def pin(a):
+        t = torch.from_numpy(a.view(np.int32) if a.dtype == np.uint32 else a).pin_memory()
+        return t.numpy().view(a.dtype)
+    pk, pv, po = [pin(k) for k in hk], [pin(v) for v in hv], [pin(o) for o in ho]
+    with ps.Shard(0, space, np.float32) as sh:
+        sh.add_grouped(list(zip(pk, pv)))
+        sh.get_grouped(list(zip(pk, po)))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            sh.add_grouped(list(zip(pk, pv)))
+            sh.get_grouped(list(zip(pk, po)))
+        sh.sync()
+        dt = time.perf_counter() - t0
+    assert all(np.array_equal(o, hv[last[int(k[0])]]) for o, k in zip(po, hk))
+    out["e2e_pinned_buffers"] = {"workload": "as e2e_host_buffers, from page-locked host memory (direct DMA)",
+                                 "GB/s": (add_b + get_b) * reps / dt / 1e9}
     return out
 
 

@@ -202,6 +202,7 @@ struct pskv_shard {
   size_t hstage_bytes = 0;
   hipEvent_t hstage_free = nullptr;
   bool hstage_pending = false;
+  hipEvent_t h2d_done = nullptr;  // pinned caller buffers: their DMA has completed
   void* dstage = nullptr;
   size_t dstage_bytes = 0;
   std::vector<hipEvent_t> win_events;  // per-window D2H completion (pull to host)
@@ -601,14 +602,20 @@ void copy_piece(Piece& p, uint32_t key_begin, uint64_t range) {
   bool ok = true, dense = true;
   uint64_t outside = 0;
   uint32_t prev = n ? k[0] : 0;
-  for (size_t i = 0; i < n; ++i) {
-    const uint32_t x = k[i];
-    o[i] = x;
-    outside += (uint64_t)(uint32_t)(x - key_begin) >= range;
-    ok &= prev <= x;
-    dense &= i == 0 || x == prev + 1u;
-    prev = x;
-  }
+  auto scan = [&](auto store) {
+    for (size_t i = 0; i < n; ++i) {
+      const uint32_t x = k[i];
+      store(i, x);
+      outside += (uint64_t)(uint32_t)(x - key_begin) >= range;
+      ok &= prev <= x;
+      dense &= i == 0 || x == prev + 1u;
+      prev = x;
+    }
+  };
+  if (o)
+    scan([&](size_t i, uint32_t x) { o[i] = x; });
+  else
+    scan([](size_t, uint32_t) {});  // pinned caller buffer: check only, the DMA reads it
   p.sorted = ok;
   p.dense = dense;
   p.first = n ? k[0] : 0;
@@ -622,7 +629,7 @@ void add_pieces(std::vector<Piece>& out, const void* src, char* dst, size_t byte
   for (size_t off = 0; off < bytes; off += kPieceBytes) {
     Piece p{};
     p.src = s + off;
-    p.dst = dst + off;
+    p.dst = dst ? dst + off : nullptr;
     p.bytes = std::min(kPieceBytes, bytes - off);
     p.key_batch = key_batch;
     p.sorted = true;
@@ -649,6 +656,17 @@ int pipelined_h2d(pskv_shard* s, std::vector<Piece>& pieces, char* h, char* d) {
   return PSKV_OK;
 }
 
+// Page-locked (hipHostMalloc'd / registered) host memory: the DMA engine can
+// read or write it directly, so no staging copy is needed.
+bool is_pinned(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
 // Stage host batches into one device buffer (keys then values per batch,
 // 16-byte aligned) through pinned memory, checking on the way whether every
 // batch is sorted and inside the dense range.  Returns device batch views.
@@ -657,7 +675,9 @@ int stage_host_batches(pskv_shard* s, const std::vector<pskv_batch>& in,
                        uint64_t* n_outside, bool* all_dense_in_range = nullptr) {
   size_t bytes = 0;
   for (auto& b : in) bytes += round16(b.n * 4) + round16(b.n * (size_t)s->vb);
-  int rc = ensure_hstage(s, bytes);
+  bool pinned = true;
+  for (const auto& b : in) pinned = pinned && is_pinned(b.keys) && is_pinned(b.vals);
+  int rc = pinned ? PSKV_OK : ensure_hstage(s, bytes);
   if (rc) return rc;
   rc = ensure_dstage(s, bytes);
   if (rc) return rc;
@@ -669,19 +689,36 @@ int stage_host_batches(pskv_shard* s, const std::vector<pskv_batch>& in,
   for (size_t j = 0; j < in.size(); ++j) {
     const auto& b = in[j];
     pskv_batch db;
-    add_pieces(pieces, b.keys, h + off, b.n * 4, (int)j);
+    if (pinned) {
+      // DMA straight from the caller's page-locked buffers; the CPU only checks
+      PSKV_HIP(hipMemcpyAsync(d + off, b.keys, b.n * 4, hipMemcpyHostToDevice, s->stream));
+      add_pieces(pieces, b.keys, nullptr, b.n * 4, (int)j);
+    } else {
+      add_pieces(pieces, b.keys, h + off, b.n * 4, (int)j);
+    }
     db.keys = reinterpret_cast<const uint32_t*>(d + off);
     off += round16(b.n * 4);
-    add_pieces(pieces, b.vals, h + off, b.n * (size_t)s->vb, -1);
+    if (pinned)
+      PSKV_HIP(hipMemcpyAsync(d + off, b.vals, b.n * (size_t)s->vb, hipMemcpyHostToDevice, s->stream));
+    else
+      add_pieces(pieces, b.vals, h + off, b.n * (size_t)s->vb, -1);
     db.vals = d + off;
     db.n = b.n;
     off += round16(b.n * (size_t)s->vb);
     out->push_back(db);
   }
-  rc = pipelined_h2d(s, pieces, h, d);
-  if (rc) return rc;
-  PSKV_HIP(hipEventRecord(s->hstage_free, s->stream));
-  s->hstage_pending = true;
+  if (pinned) {
+    PSKV_HIP(hipEventRecord(s->h2d_done, s->stream));
+    HostPool::get().run(pieces.size(),
+                        [&](size_t t) { copy_piece(pieces[t], s->key_begin, s->range); });
+    // the caller may reuse its buffers once this returns
+    PSKV_HIP(hipEventSynchronize(s->h2d_done));
+  } else {
+    rc = pipelined_h2d(s, pieces, h, d);
+    if (rc) return rc;
+    PSKV_HIP(hipEventRecord(s->hstage_free, s->stream));
+    s->hstage_pending = true;
+  }
   // combine the per-piece checks: every piece sorted, and each piece's first
   // key not below the previous piece's last key within the same batch
   bool ok = true, dense = true;
@@ -780,7 +817,24 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
   const bool device = (flags & PSKV_DEVICE) != 0;
   std::vector<pskv_batch> dv = v;
   size_t out_off = 0;
-  if (!device) {
+  bool pinned = !device;
+  for (const auto& b : v) pinned = pinned && is_pinned(b.keys) && is_pinned(b.vals);
+  if (pinned) {
+    // page-locked caller buffers: keys DMA'd in directly, values DMA'd out directly
+    size_t bytes = 0;
+    for (auto& b : v) bytes += round16(b.n * 4) + round16(b.n * (size_t)s->vb);
+    rc = ensure_dstage(s, bytes);
+    if (rc) return rc;
+    char* d = static_cast<char*>(s->dstage);
+    size_t off = 0;
+    for (size_t i = 0; i < v.size(); ++i) {
+      PSKV_HIP(hipMemcpyAsync(d + off, v[i].keys, v[i].n * 4, hipMemcpyHostToDevice, s->stream));
+      dv[i].keys = reinterpret_cast<const uint32_t*>(d + off);
+      off += round16(v[i].n * 4);
+      dv[i].vals = d + off;
+      off += round16(v[i].n * (size_t)s->vb);
+    }
+  } else if (!device) {
     // keys -> pinned -> device (pipelined); outputs land after the keys in the stage
     size_t kbytes = 0, obytes = 0;
     for (auto& b : v) {
@@ -820,7 +874,12 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
                            s->stream));
     t.done();
   }
-  if (!device) {
+  if (pinned) {
+    for (size_t i = 0; i < v.size(); ++i)
+      PSKV_HIP(hipMemcpyAsync(v[i].vals, dv[i].vals, v[i].n * (size_t)s->vb, hipMemcpyDeviceToHost,
+                              s->stream));
+    PSKV_HIP(hipStreamSynchronize(s->stream));
+  } else if (!device) {
     // D2H window by window; the pool copies window w out to the caller while
     // window w+1 is still in flight
     char* h = static_cast<char*>(s->hstage);
@@ -930,7 +989,9 @@ int pskv_shard_create_ex(int device, uint32_t key_begin, uint64_t key_end, int d
   if (hipStreamCreateWithFlags(&s->own_stream, hipStreamDefault) != hipSuccess)
     return bail(fail(PSKV_EHIP, "hipStreamCreate failed"));
   s->stream = s->own_stream;
-  if (hipEventCreateWithFlags(&s->hstage_free, hipEventDisableTiming) != hipSuccess)
+  if (hipEventCreateWithFlags(&s->hstage_free, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&s->h2d_done, hipEventDisableTiming | hipEventDisableSystemFence) !=
+          hipSuccess)
     return bail(fail(PSKV_EHIP, "hipEventCreate failed"));
   if (hipMalloc(&s->dense, s->range * (size_t)vb) != hipSuccess)
     return bail(fail(PSKV_ENOMEM, "dense parameter allocation failed"));
@@ -973,6 +1034,7 @@ int pskv_shard_destroy(pskv_shard* s) {
   if (s->rb_ent) (void)hipFree(s->rb_ent);
   if (s->hstage) (void)hipHostFree(s->hstage);
   if (s->hstage_free) (void)hipEventDestroy(s->hstage_free);
+  if (s->h2d_done) (void)hipEventDestroy(s->h2d_done);
   for (auto e : s->win_events) (void)hipEventDestroy(e);
   if (s->own_stream) (void)hipStreamDestroy(s->own_stream);
   delete s;

@@ -601,3 +601,55 @@ def test_accumulate_stamps_variant_k4a(cuda, monkeypatch, dtype):
     else:
         tol = 1.01 * (cnt + 1) * 2.0**-24 * a64
         assert np.all(np.abs(got.astype(np.float64) - p64) <= tol)
+
+
+def _pinned(a):
+    """numpy view of a page-locked copy of a (torch pinned host memory)."""
+    import torch
+
+    a = np.ascontiguousarray(a)
+    t = torch.from_numpy(a.view(np.int32) if a.dtype == np.uint32 else a).pin_memory()
+    out = t.numpy()
+    return out.view(np.uint32) if a.dtype == np.uint32 else out
+
+
+@pytest.mark.parametrize("mode", ["assign", "accumulate"])
+def test_pinned_host_buffers_direct_dma(cuda, oracle_mod, mode):
+    """Page-locked caller buffers (the zmq frames after the SURVEY §8f-3 mailbox
+    change) are DMA'd directly, without the staging copy: same results as
+    pageable buffers, for sorted, dense and unsorted batches, Add and Get."""
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(71)
+    kb, size = 10, 400_000
+    batches = []
+    for j in range(6):
+        if j % 3 == 0:
+            f = int(rng.integers(kb, kb + size - 50_000))
+            k = np.arange(f, f + 50_000, dtype=np.uint32)                       # dense window
+        elif j % 3 == 1:
+            k = np.sort(rng.integers(kb, kb + size, size=30_000)).astype(np.uint32)  # sorted
+        else:
+            k = rng.integers(0, kb + size + 1000, size=30_000).astype(np.uint32)    # unsorted, overflow
+        v = rng.integers(-500, 500, size=k.size).astype(np.float64)
+        batches.append((k, v))
+    q = np.arange(0, kb + size + 1000, dtype=np.uint32)
+    outs = {}
+    for kind in ("pageable", "pinned"):
+        with ps.Shard(kb, kb + size, np.float64, mode=mode, overflow_slots=1 << 14) as sh:
+            bb = batches if kind == "pageable" else [(_pinned(k), _pinned(v)) for k, v in batches]
+            sh.add_grouped(bb[:3])
+            for k, v in bb[3:]:
+                sh.add(k, v)
+            qq = q if kind == "pageable" else _pinned(q)
+            o = np.zeros(q.size, np.float64) if kind == "pageable" else _pinned(np.zeros(q.size, np.float64))
+            sh.get_grouped([(qq, o)])
+            outs[kind] = o.copy()
+            outs[kind + "_single"] = sh.get(qq)
+    assert_bits_equal(outs["pinned"], outs["pageable"], "pinned vs pageable")
+    assert_bits_equal(outs["pinned_single"], outs["pageable"], "pinned single get")
+    if mode == "assign":
+        ref = oracle_mod.MapStorageRef(np.float64)
+        for k, v in batches:
+            ref.add(k, v)
+        assert_bits_equal(outs["pinned"], ref.get(q), "pinned vs oracle")
