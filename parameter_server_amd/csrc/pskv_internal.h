@@ -24,7 +24,6 @@ constexpr int kGeneralChunk = 2048;  // keys per workgroup in the dedup path
 constexpr int kGeneralSlots = 4096;  // LDS hash slots (load factor <= 1/2)
 constexpr int kRbChunk = 2048;       // keys per dedup sub-chunk in the radix-bucket path (K5)
 constexpr int kRbMaxBuckets = 2064;  // key buckets incl. the out-of-range bucket (>= 2049)
-constexpr int kRbApplySlots = 16384; // LDS hash slots of a K5 apply workgroup
 constexpr unsigned long long kEmpty64 = ~0ull;
 constexpr uint32_t kEmpty32 = 0xFFFFFFFFu;
 
@@ -87,10 +86,12 @@ hipError_t launch_ovf_rehash(int vb, const Ovf& from, uint64_t from_cap, const O
 // (nbd dense buckets) plus one out-of-range bucket.  Scratch: cnt, off:
 // nsc * (nbd+1) u32 each; nsub: nsc * 4 u32; total: nbd+1 u32; tmp: nsc *
 // rb_superchunk(vb) entries; ent: one entry per element (rb_entry_bytes(vb) each).
+// apply_log2: log2 of the apply workgroup's LDS table slots (13: 64 KiB, two
+// workgroups per CU, ~7 Ki entries per bucket in one pass; 14: 128 KiB, ~14 Ki).
 hipError_t launch_rb_add(int dtype, int mode, const GroupArgs& ga, uint32_t nsc,
                          const DenseView& d, const Ovf& o, uint32_t bshift, uint32_t nbd,
-                         uint32_t* cnt, uint32_t* off, uint32_t* nsub, uint32_t* total, void* tmp,
-                         void* ent, hipStream_t st);
+                         int apply_log2, uint32_t* cnt, uint32_t* off, uint32_t* nsub,
+                         uint32_t* total, void* tmp, void* ent, hipStream_t st);
 uint32_t rb_superchunk(int vb);
 size_t rb_entry_bytes(int vb);
 // K6: tag `flag` with `epoch` unless every batch is a dense in-range window

@@ -1171,18 +1171,19 @@ __global__ __launch_bounds__(BLOCK) void k_rb_move(DenseView d, uint32_t bshift,
 // registers in one pass, the next bucket's entries loading meanwhile;
 // otherwise rounds split it by key hash.
 constexpr int kApplyBlock = 1024;
-template <typename AT, typename BT, int MODE>
+template <typename AT, typename BT, int MODE, int LOGS>
 __global__ __launch_bounds__(kApplyBlock) void k_rb_apply(DenseView d, Ovf o, uint32_t nbd,
                                                           uint32_t nbk, const uint32_t* total,
                                                           const RbEnt<sizeof(BT)>* __restrict__ ent) {
-  constexpr int SLOTS = (MODE == 1 && sizeof(AT) == 8) ? kRbApplySlots / 2 : kRbApplySlots;
+  // f64 sums take 8 B per slot: half the slots in the same LDS
+  constexpr int SLOTS = (MODE == 1 && sizeof(AT) == 8) ? (1 << LOGS) / 2 : (1 << LOGS);
   constexpr uint32_t CAP = (uint32_t)SLOTS / 8 * 7;  // entries per round (load <= 7/8)
   constexpr int EPT = (int)((CAP + kApplyBlock - 1) / kApplyBlock);
   using Ent = RbEnt<sizeof(BT)>;
-  __shared__ uint32_t ak[SLOTS + 1];
-  __shared__ uint32_t abest[MODE == 0 ? SLOTS + 1 : 1];  // assign: 1 + max position (0 = none)
-  __shared__ AT asum[MODE == 1 ? SLOTS + 1 : 1];
-  __shared__ uint32_t sbase[kRbMaxBuckets + 1];
+  __shared__ __attribute__((aligned(16))) uint32_t ak[SLOTS + 1];
+  __shared__ __attribute__((aligned(16))) uint32_t abest[MODE == 0 ? SLOTS + 1 : 1];  // assign: 1 + max position
+  __shared__ __attribute__((aligned(16))) AT asum[MODE == 1 ? SLOTS + 1 : 1];
+  extern __shared__ uint32_t sbase[];  // nbk + 1 words (dynamic: sized to the launch)
   __shared__ uint32_t wtmp[kApplyBlock / 64];
   __shared__ uint32_t sent;
   const int tid = threadIdx.x;
@@ -1204,6 +1205,29 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_apply(DenseView d, Ovf o, ui
   };
   auto accumulate_all = [&](uint32_t b) {
     // this workgroup owns every key of the bucket: plain read-modify-write
+    if (b != nbd) {
+      // dense bucket: every lane's parameter loads issued together (addresses
+      // clamped, no branches around the loads), then the adds and stores
+      constexpr int SPT = (SLOTS + 1 + kApplyBlock - 1) / kApplyBlock;
+      AT* __restrict__ param = reinterpret_cast<AT*>(d.param);
+      uint32_t off[SPT];
+      uint32_t used = 0;
+#pragma unroll
+      for (int q = 0; q < SPT; ++q) {
+        const int s = q * kApplyBlock + tid;
+        const bool u = s < SLOTS ? ak[s] != kEmpty32 : (s == SLOTS && sent != 0);
+        const uint32_t key = s < SLOTS ? ak[s] : kEmpty32;
+        off[q] = u ? key - d.key_begin : 0u;
+        used |= u ? (1u << q) : 0u;
+      }
+      AT cur[SPT];
+#pragma unroll
+      for (int q = 0; q < SPT; ++q) cur[q] = param[off[q]];
+#pragma unroll
+      for (int q = 0; q < SPT; ++q)
+        if (used >> q & 1u) param[off[q]] = add_wrap<AT>(cur[q], asum[q * kApplyBlock + tid]);
+      return;
+    }
     for (int s = tid; s <= SLOTS; s += kApplyBlock) {
       const bool used = s == SLOTS ? sent != 0 : ak[s] != kEmpty32;
       if (!used) continue;
@@ -1220,14 +1244,24 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_apply(DenseView d, Ovf o, ui
     }
   };
   auto clear_table = [&]() {
-    for (int s = tid; s <= SLOTS; s += kApplyBlock) {
-      ak[s] = kEmpty32;
-      if (MODE == 0)
-        abest[s] = 0;
-      else
-        asum[s] = AT(0);
+    // 16-byte LDS writes (SLOTS is a multiple of 4 * kApplyBlock)
+    for (int s = tid * 4; s < SLOTS; s += kApplyBlock * 4) {
+      *reinterpret_cast<u32x4*>(&ak[s]) = u32x4{kEmpty32, kEmpty32, kEmpty32, kEmpty32};
+      if (MODE == 0) {
+        *reinterpret_cast<u32x4*>(&abest[s]) = u32x4{0u, 0u, 0u, 0u};
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) asum[s + e] = AT(0);
+      }
     }
-    if (tid == 0) sent = 0;
+    if (tid == 0) {
+      ak[SLOTS] = kEmpty32;
+      if (MODE == 0)
+        abest[SLOTS] = 0;
+      else
+        asum[SLOTS] = AT(0);
+      sent = 0;
+    }
   };
   // entries of bucket b held in registers: x[q] = entry q * kApplyBlock + tid
   auto load_bucket = [&](uint32_t b, Ent (&x)[EPT]) {
@@ -1645,8 +1679,9 @@ hipError_t launch_ovf_rehash(int vb, const Ovf& from, uint64_t from_cap, const O
 
 template <typename AT, typename BT, int MODE>
 static hipError_t rb_launch(const GroupArgs& ga, uint32_t nsc, const DenseView& d, const Ovf& o,
-                            uint32_t bshift, uint32_t nbd, uint32_t* cnt, uint32_t* off,
-                            uint32_t* nsub, uint32_t* total, void* tmp, void* ent, hipStream_t st) {
+                            uint32_t bshift, uint32_t nbd, int apply_log2, uint32_t* cnt,
+                            uint32_t* off, uint32_t* nsub, uint32_t* total, void* tmp, void* ent,
+                            hipStream_t st) {
   const uint32_t nbk = nbd + 1;
   // persistent grids: the dedup LDS is cleared once per workgroup
   const uint32_t gc = nsc < 1024u ? nsc : 1024u;  // <= 40 KiB LDS, <= 128 VGPRs: 4 per CU
@@ -1657,17 +1692,25 @@ static hipError_t rb_launch(const GroupArgs& ga, uint32_t nsc, const DenseView& 
   k_rb_scan<<<(nbk + 63) / 64, kScanBlock, 0, st>>>(cnt, off, nsc, nbk, total);
   k_rb_move<BT, kRbMoveBlock><<<gm, kRbMoveBlock, 0, st>>>(d, bshift, nbd, nbk, cnt, off, nsub, nsc,
                                                            total, t, e);
-  k_rb_apply<AT, BT, MODE><<<nbk < 256u ? nbk : 256u, kApplyBlock, 0, st>>>(d, o, nbd, nbk, total, e);
+  const size_t sb = (nbk + 1) * sizeof(uint32_t);
+  if (apply_log2 == 13) {
+    const uint32_t ga2 = nbk < 512u ? nbk : 512u;  // two workgroups per CU
+    k_rb_apply<AT, BT, MODE, 13><<<ga2, kApplyBlock, sb, st>>>(d, o, nbd, nbk, total, e);
+  } else {
+    k_rb_apply<AT, BT, MODE, 14><<<nbk < 256u ? nbk : 256u, kApplyBlock, sb, st>>>(d, o, nbd, nbk,
+                                                                                  total, e);
+  }
   return hipGetLastError();
 }
 
 hipError_t launch_rb_add(int dtype, int mode, const GroupArgs& ga, uint32_t nsc,
                          const DenseView& d, const Ovf& o, uint32_t bshift, uint32_t nbd,
-                         uint32_t* cnt, uint32_t* off, uint32_t* nsub, uint32_t* total, void* tmp,
-                         void* ent, hipStream_t st) {
+                         int apply_log2, uint32_t* cnt, uint32_t* off, uint32_t* nsub,
+                         uint32_t* total, void* tmp, void* ent, hipStream_t st) {
   if (nsc == 0) return hipSuccess;
   if (nbd + 1 > (uint32_t)kRbMaxBuckets) return hipErrorInvalidValue;
-#define PSKV_RB(AT, BT, M) rb_launch<AT, BT, M>(ga, nsc, d, o, bshift, nbd, cnt, off, nsub, total, tmp, ent, st)
+#define PSKV_RB(AT, BT, M) \
+  rb_launch<AT, BT, M>(ga, nsc, d, o, bshift, nbd, apply_log2, cnt, off, nsub, total, tmp, ent, st)
   if (mode == 0) {
     if (dtype == 0) return PSKV_RB(int, uint32_t, 0);
     if (dtype == 1) return PSKV_RB(float, uint32_t, 0);

@@ -229,6 +229,7 @@ struct pskv_shard {
   bool tune_nt = true;   // PSKV_NT: non-temporal streams (measured +12-15 % on K1 / K2g)
   bool tune_ntp = false; // PSKV_NTP: non-temporal parameter stores (dense Add)
   uint32_t tune_rb_tb = 0; // PSKV_RB_TB: K5 bucket bits (0 = by element count)
+  int tune_rb_apply_log2 = 0; // PSKV_RB_APPLY_LOG2: 13 or 14 (0 = by bucket size)
 
   DenseView dview() const { return DenseView{dense, key_begin, range}; }
 };
@@ -452,9 +453,11 @@ int radix_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t 
   const uint32_t nsc = build_group(v, b, e, rb_superchunk(s->vb), &ga);
   uint64_t elems = 0;
   for (size_t i = b; i < e; ++i) elems += v[i].n;
-  // bucket = key offset >> bshift: about one bucket per 4 Ki pushed keys (an
-  // apply workgroup resolves up to ~14 Ki entries in one register-resident
-  // pass), at most 2048 dense buckets
+  // bucket = key offset >> bshift: about one bucket per 4 Ki pushed keys, at
+  // most 2048 dense buckets (more buckets measured slower at cfg 3: longer
+  // count rows, shorter move runs).  The apply workgroup resolves a bucket
+  // from registers when its entries fit its LDS table: 2^13 slots (two
+  // workgroups per CU) while buckets average <= 2 Ki pushed keys, else 2^14.
   uint32_t bits = 0;
   while (bits < 32 && ((s->range - 1) >> bits) != 0) ++bits;
   uint32_t tb = 6;
@@ -463,6 +466,8 @@ int radix_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t 
   const uint32_t bshift = bits > tb ? bits - tb : 0;
   const uint32_t nbd = (uint32_t)(((s->range - 1) >> bshift) + 1);
   const uint32_t nbk = nbd + 1;
+  int apply_log2 = elems / nbd <= 2048 ? 13 : 14;
+  if (s->tune_rb_apply_log2) apply_log2 = s->tune_rb_apply_log2;
   if (nbk > (uint32_t)kRbMaxBuckets) return fail(PSKV_EINVAL, "radix path: too many buckets");
   size_t have_total = s->rb_total ? 4 * (size_t)kRbMaxBuckets : 0;
   const size_t eb = rb_entry_bytes(s->vb);
@@ -476,7 +481,8 @@ int radix_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t 
   if (rc) return rc;
   char* ent = static_cast<char*>(s->rb_ent);
   LaunchTimer t(s, PSKV_K_RADIX, elems);
-  PSKV_HIP(launch_rb_add(s->dtype, s->mode, ga, nsc, s->dview(), s->ovf, bshift, nbd, s->rb_cnt,
+  PSKV_HIP(launch_rb_add(s->dtype, s->mode, ga, nsc, s->dview(), s->ovf, bshift, nbd, apply_log2,
+                         s->rb_cnt,
                          s->rb_cnt + nb2, s->rb_cnt + 2 * nb2, s->rb_total,
                          ent + elems * eb, ent, s->stream));
   t.done();
@@ -977,6 +983,10 @@ int pskv_shard_create_ex(int device, uint32_t key_begin, uint64_t key_end, int d
   if (const char* e = std::getenv("PSKV_RB_TB")) {
     const int v = std::atoi(e);
     if (v >= 1 && v <= 11) s->tune_rb_tb = (uint32_t)v;
+  }
+  if (const char* e = std::getenv("PSKV_RB_APPLY_LOG2")) {
+    const int v = std::atoi(e);
+    if (v == 13 || v == 14) s->tune_rb_apply_log2 = v;
   }
   auto bail = [&](int rc) {
     pskv_shard_destroy(s);
