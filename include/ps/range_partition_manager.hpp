@@ -28,6 +28,8 @@ class RangeShardMap {
 
   size_t GetNumServers() const { return ids_.size(); }
   const std::vector<uint32_t>& GetServerThreadIds() const { return ids_; }
+  // Key range [begin, end) of the i-th server (in server order).
+  std::pair<uint64_t, uint64_t> GetRange(size_t i) const { return std::make_pair(rb_[i], re_[i]); }
 
   // Zero-copy slices (segments of `keys`), in server order.
   void Slice(const Keys& keys, std::vector<std::pair<int, Keys>>* sliced) const {

@@ -9,6 +9,9 @@
 //                                            Add{5:1,5:2,7:3}; Add{7:10}; Get{5,7,9} -> {2,10,0}
 //   SliceKeys / SliceKVs                     base/range_partition_manager_test.cpp:17-56
 //   SliceFallthrough                         SURVEY.md §0.4 probes
+//   CreateTableHip                           driver/engine.hpp:93-131 with StorageType::Hip
+//                                            (ps/storage_factory.hpp): per-server ranges, the
+//                                            last server also stores the fall-through keys
 //
 // Needs a GPU for the storage cases (run by tests/test_gpu_parity.py);
 // `--host-only` runs the range-map cases alone.
@@ -20,6 +23,7 @@
 
 #include "ps/hip_storage.hpp"
 #include "ps/range_partition_manager.hpp"
+#include "ps/storage_factory.hpp"
 
 using namespace csci5570;
 
@@ -134,6 +138,57 @@ static void SliceCases() {
   }
 }
 
+// CreateTable over three server threads: each server's HipStorage owns its
+// range; keys the slicer routes to the last server beyond its range land in
+// its overflow table.  Adds go through the models (ASP: immediate).
+static void CreateTableHip() {
+  std::printf("[ RUN ] CreateTableHip\n");
+  RangeShardMap map({0, 1, 2}, {{0, 100}, {100, 200}, {200, 300}});
+  std::vector<std::unique_ptr<ServerThread>> threads;
+  for (uint32_t i = 0; i < 3; ++i) threads.emplace_back(new ServerThread(i));
+  ReplyQueue replies;
+  auto st = CreateTable<int>(threads, map, 7, ModelType::ASP, StorageType::Hip, 0, &replies);
+  EXPECT(st.size() == 3);
+  for (size_t i = 0; i < 3; ++i) {
+    auto* hs = dynamic_cast<HipStorage<int>*>(st[i]);
+    EXPECT(hs != nullptr);
+    pskv_info info;
+    EXPECT(pskv_shard_info(hs->shard(), &info) == PSKV_OK);
+    EXPECT(info.key_begin == 100 * i && info.key_end == 100 * (i + 1));
+  }
+  // push {5, 150, 250, 4000} through the map and the models, then pull
+  const std::vector<uint32_t> ks = {5, 150, 250, 4000};
+  const std::vector<int> vs = {1, 2, 3, 4};
+  std::vector<std::pair<int, RangeShardMap::Keys>> sl;
+  third_party::SArray<uint32_t> ka(ks);
+  map.Slice(ka, &sl);
+  EXPECT(sl.size() == 3 && sl[2].second.size() == 2);  // 250 and 4000 -> the last server
+  for (auto& s : sl) {
+    const size_t off = s.second.data() - ka.data();
+    Message m;
+    m.meta.flag = Flag::kAdd;
+    m.meta.model_id = 7;
+    m.AddData(s.second);
+    m.AddData(third_party::SArray<int>(std::vector<int>(vs.begin() + off, vs.begin() + off + s.second.size())));
+    threads[s.first]->GetModel(7)->Add(m);
+  }
+  for (auto& s : sl) {
+    Message m;
+    m.meta.flag = Flag::kGet;
+    m.meta.model_id = 7;
+    m.meta.recver = s.first;
+    m.AddData(s.second);
+    threads[s.first]->GetModel(7)->Get(m);
+  }
+  std::vector<int> got;
+  Message r;
+  while (replies.Pop(&r)) {
+    auto v = third_party::SArray<int>(r.data[1]);
+    got.insert(got.end(), v.begin(), v.end());
+  }
+  EXPECT(got == vs);
+}
+
 int main(int argc, char** argv) {
   const bool host_only = argc > 1 && std::strcmp(argv[1], "--host-only") == 0;
   SliceCases();
@@ -145,6 +200,7 @@ int main(int argc, char** argv) {
     LastWriteWins<int>(0, 1ull << 20, "LastWriteWinsInt");
     LastWriteWins<float>(0, 1ull << 20, "LastWriteWinsFloat");
     LastWriteWins<double>(6, 8, "LastWriteWinsDoubleOverflow");  // 5 and 9 live in the overflow table
+    CreateTableHip();
   }
   std::printf("%d passed, %d failed\n", g_pass, g_fail);
   return g_fail ? 1 : 0;

@@ -39,6 +39,7 @@
 #include "ps/hip_storage.hpp"
 #include "ps/range_partition_manager.hpp"
 #include "ps/server_thread.hpp"
+#include "ps/storage_factory.hpp"
 
 using namespace csci5570;
 
@@ -136,7 +137,23 @@ class Replay {
     }
     map_.reset(new RangeShardMap(ids_, ranges_));
     int ndev = pskv_device_count();
-    for (int s = 0; s < c.shards; ++s) {
+    if (c.threads) {
+      // Engine::CreateTable (driver/engine.hpp:93-131) through the restated
+      // factory: one ServerThread, storage and model per range
+      for (int s = 0; s < c.shards; ++s) threads_.emplace_back(new ServerThread((uint32_t)s));
+      const ModelType mt = c.model == "ssp" ? ModelType::SSP : c.model == "bsp" ? ModelType::BSP : ModelType::ASP;
+      storages_ = CreateTable<double>(
+          threads_, *map_, 0, mt, hip ? StorageType::Hip : StorageType::Map, c.staleness, &replies_,
+          PSKV_ASSIGN, [](StorageType) { return std::unique_ptr<AbstractStorage>(new OracleStorage<double>()); });
+      for (auto& t : threads_) {
+        if (auto* bsp = dynamic_cast<BSPModel*>(t->GetModel(0))) bsp->SetGroupedFlush(!c.bsp_ungrouped);
+        t->SetOnProcessed([this] {
+          std::lock_guard<std::mutex> lk(qm_);
+          if (--inflight_ == 0) quiet_.notify_all();
+        });
+      }
+    }
+    for (int s = 0; s < c.shards && !c.threads; ++s) {
       std::unique_ptr<AbstractStorage> st;
       if (hip)
         st.reset(new HipStorage<double>(s % (ndev > 0 ? ndev : 1), (uint32_t)ranges_[s].first,
@@ -154,16 +171,7 @@ class Replay {
       } else {
         md.reset(new ASPModel(0, std::move(st), &replies_));
       }
-      if (c.threads) {  // server_thread.cpp: the model lives in its server's thread
-        threads_.emplace_back(new ServerThread((uint32_t)s));
-        threads_.back()->RegisterModel(0, std::move(md));
-        threads_.back()->SetOnProcessed([this] {
-          std::lock_guard<std::mutex> lk(qm_);
-          if (--inflight_ == 0) quiet_.notify_all();
-        });
-      } else {
-        models_.push_back(std::move(md));
-      }
+      models_.push_back(std::move(md));
     }
     server_q_.resize(c.shards);
     for (auto& t : threads_) t->Start();
