@@ -6,23 +6,10 @@
 // but declares no virtual destructor, so a subclass holding HBM would leak.
 #pragma once
 
-#include <cstdio>
-#include <cstdlib>
-
 #include <vector>
 
 #include "ps/message.hpp"
 
-#ifndef PS_CHECK
-// glog CHECK restated: print and abort (the reference's error convention).
-#define PS_CHECK(cond)                                                           \
-  do {                                                                           \
-    if (!(cond)) {                                                               \
-      std::fprintf(stderr, "Check failed: %s (%s:%d)\n", #cond, __FILE__, __LINE__); \
-      std::abort();                                                              \
-    }                                                                            \
-  } while (0)
-#endif
 
 namespace csci5570 {
 

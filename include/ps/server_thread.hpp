@@ -1,5 +1,5 @@
 // ps/server_thread.hpp — the server actor that calls the storage, restated:
-//   ThreadsafeQueue  base/threadsafe_queue.hpp:14-45 (Push / WaitAndPop / Size)
+//   (ThreadsafeQueue: ps/threadsafe_queue.hpp)
 //   ServerThread     server/server_thread.{hpp,cpp}: one std::thread per server
 //                    id, FIFO WaitAndPop, dispatch by flag to the model of the
 //                    message's model_id (server_thread.cpp:20-50); kExit stops it.
@@ -17,33 +17,9 @@
 #include <thread>
 
 #include "ps/consistency.hpp"
+#include "ps/threadsafe_queue.hpp"
 
 namespace csci5570 {
-
-template <typename T>
-class ThreadsafeQueue {
- public:
-  void Push(T v) {
-    std::lock_guard<std::mutex> lk(m_);
-    q_.push(std::move(v));
-    cv_.notify_all();
-  }
-  void WaitAndPop(T* v) {
-    std::unique_lock<std::mutex> lk(m_);
-    cv_.wait(lk, [&] { return !q_.empty(); });
-    *v = std::move(q_.front());
-    q_.pop();
-  }
-  int Size() {
-    std::lock_guard<std::mutex> lk(m_);
-    return (int)q_.size();
-  }
-
- private:
-  std::mutex m_;
-  std::condition_variable cv_;
-  std::queue<T> q_;
-};
 
 class ServerThread {
  public:

@@ -21,6 +21,7 @@ LIB_OUT = os.path.join(PKG, "libpskv.so")
 CPP_TESTS = {  # program -> (source in tests/cpp, links the oracle checker)
     "hip_storage_test": ("hip_storage_test.cpp", False),
     "ssp_replay": ("ssp_replay.cpp", True),
+    "kv_client_table_test": ("kv_client_table_test.cpp", False),
 }
 ORACLE_DIR = os.path.join(ROOT, "oracle")
 BIN_DIR = os.path.join(PKG, "bin")

@@ -113,6 +113,21 @@ def test_cpp_boundary_host_cases():
     assert "0 failed" in r.stdout
 
 
+def test_kv_client_table_host():
+    """tests/cpp/kv_client_table_test.cpp on the CPU storage: the reference's
+    KVClientTable tests (worker/kv_client_table_test.cpp), typed slicing ==
+    the reference's double path, and the worker -> server -> storage system
+    test under ASP / SSP / BSP."""
+    exe = os.path.join(ROOT, "parameter_server_amd", "bin", "kv_client_table_test")
+    if not os.path.exists(exe):
+        from parameter_server_amd import build
+
+        build.build_cpp_tests()
+    r = subprocess.run(["timeout", "-k", "10", "120", exe, "--host-only"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert " 0 failed" in r.stdout
+
+
 class FakeStorage:
     pass
 

@@ -59,6 +59,17 @@ def test_cpp_boundary_program(cuda):
     assert " 0 failed" in r.stdout
 
 
+def test_kv_client_table_system_hip(cuda):
+    """tests/cpp/kv_client_table_test.cpp with HipStorage<float> shards: worker
+    threads with KVClientTable -> sender -> ServerThreads (ASP / SSP / BSP
+    models over HBM shards built by CreateTable) -> replies -> CallbackRunner;
+    read-your-writes and the final contents of every shard, bit for bit."""
+    exe = os.path.join(ROOT, "parameter_server_amd", "bin", "kv_client_table_test")
+    r = subprocess.run(["timeout", "-k", "10", "300", exe, "--storage", "hip"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert " 0 failed" in r.stdout
+
+
 def known():
     with open(os.path.join(GOLDEN, "reference_known_answers.json")) as f:
         return json.load(f)
