@@ -284,11 +284,11 @@ def side_measurements(dev, B):
         sh.set_stream(None)
     add_b, get_b = step_bytes(J * B, u_all, J * B)
     out["zipf"] = {"workload": "cfg 3: Zipf(0.99) over 1e8 keys, 8 x 1M unsorted pushes then pulls, assign "
-                               "(general path K5: LDS dedup + radix buckets, no global atomics)",
+                               "(general path K5: LDS dedup + bucket-sorted super-chunks, no global atomics)",
                    "GB/s": (add_b + get_b) * reps / dt / 1e9, "ms_per_step": dt / reps * 1e3,
                    "unique_keys_per_batch": uniq, "distinct_keys_per_step": u_all}
     # cfg 3 in accumulate mode (the north star's LDS segmented-sum path): K5,
-    # per-sub-chunk LDS sums, radix buckets, one owner workgroup per bucket
+    # per-super-chunk LDS sums, key buckets, one owner workgroup per bucket
     with ps.Shard(0, space, np.float32, mode="accumulate") as sh:
         sh.set_stream(stream.cuda_stream)
         for _ in range(2):
@@ -302,7 +302,7 @@ def side_measurements(dev, B):
         sh.set_stream(None)
     acc_b = J * B * (4 + V) + 2 * u_all * V
     out["zipf_accumulate_add"] = {"workload": "cfg 3 pushes (8 x 1M Zipf(0.99), unsorted), accumulate mode "
-                                              "(K5: LDS sub-chunk sums + radix buckets, no global atomics)",
+                                              "(K5: LDS super-chunk sums + key buckets, no global atomics)",
                                   "GB/s": acc_b * reps / dt / 1e9, "ms_per_call": dt / reps * 1e3}
     del zb, zo
     # cfg 2 windows in accumulate mode (the north star's scatter-accumulate):

@@ -22,8 +22,8 @@ inline int stream_chunk(int unroll) { return kBlock * 4 * unroll; }  // keys per
 constexpr int kSortedChunk = kBlock * 4 * kSortedUnroll;          // 2048 keys / workgroup
 constexpr int kGeneralChunk = 2048;  // keys per workgroup in the dedup path
 constexpr int kGeneralSlots = 4096;  // LDS hash slots (load factor <= 1/2)
-constexpr int kRbChunk = 2048;       // keys per dedup sub-chunk in the radix-bucket path (K5)
 constexpr int kRbMaxBuckets = 2064;  // key buckets incl. the out-of-range bucket (>= 2049)
+constexpr uint32_t kRbMaxSc = 1024;  // K5 super-chunks per launch (one run per resolve thread)
 constexpr unsigned long long kEmpty64 = ~0ull;
 constexpr uint32_t kEmpty32 = 0xFFFFFFFFu;
 
@@ -81,17 +81,16 @@ hipError_t launch_general_commit(int vb, const GroupArgs& ga, uint32_t nwg, cons
                                  const uint32_t* cond, uint32_t epoch, hipStream_t st);
 hipError_t launch_ovf_rehash(int vb, const Ovf& from, uint64_t from_cap, const Ovf& to,
                              hipStream_t st);
-// K5 radix-bucket general Add (4 launches).  `ga` chunked by
-// rb_superchunk(vb) keys (nsc super-chunks); buckets are key offset >> bshift
-// (nbd dense buckets) plus one out-of-range bucket.  Scratch: cnt, off:
-// nsc * (nbd+1) u32 each; nsub: nsc * 4 u32; total: nbd+1 u32; tmp: nsc *
-// rb_superchunk(vb) entries; ent: one entry per element (rb_entry_bytes(vb) each).
-// apply_log2: log2 of the apply workgroup's LDS table slots (13: 64 KiB, two
+// K5 radix-bucket general Add (2 launches: K5a bin, K5b resolve).  `ga`
+// chunked by rb_superchunk(vb) keys (nsc <= kRbMaxSc super-chunks); buckets
+// are key offset >> bshift (nbd dense buckets) plus one out-of-range bucket.
+// Scratch: loff: nsc * (nbd+2) u16 (each super-chunk's bucket starts); tmp:
+// nsc * rb_superchunk(vb) entries (rb_entry_bytes(vb) each).
+// apply_log2: log2 of the resolve workgroup's LDS table slots (13: 64 KiB, two
 // workgroups per CU, ~7 Ki entries per bucket in one pass; 14: 128 KiB, ~14 Ki).
 hipError_t launch_rb_add(int dtype, int mode, const GroupArgs& ga, uint32_t nsc,
                          const DenseView& d, const Ovf& o, uint32_t bshift, uint32_t nbd,
-                         int apply_log2, uint32_t* cnt, uint32_t* off, uint32_t* nsub,
-                         uint32_t* total, void* tmp, void* ent, hipStream_t st);
+                         int apply_log2, uint16_t* loff, void* tmp, hipStream_t st);
 uint32_t rb_superchunk(int vb);
 size_t rb_entry_bytes(int vb);
 // K6: tag `flag` with `epoch` unless every batch is a dense in-range window

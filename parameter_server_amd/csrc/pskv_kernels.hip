@@ -17,7 +17,7 @@
 //                         (assign) u64 last-writer stamps / (accumulate) one
 //                         atomic add per distinct key per workgroup
 //   K4b k_general_commit  Add, any order: the stamped winner of each key stores
-//   K5  k_rb_*            Add, any order, assign: radix buckets, no global atomics
+//   K5  k_rb_bin/resolve  Add, any order: key buckets, no global atomics
 //   K6  k_dense_check     accumulate: prove every batch a dense in-range window
 //   K7  k_acc_dense       accumulate over dense windows: one RMW per key, sums in
 //                         call order, no atomics
@@ -26,6 +26,8 @@
 // order) and across calls (stream order) — map_storage.hpp:22-23 assigns in a
 // sequential loop; vector_storage.hpp:34-43 returns the LAST appended match.
 // A never-written key reads 0 (map_storage.hpp:33-37).
+#include <type_traits>
+
 #include "pskv_internal.h"
 
 namespace pskv {
@@ -653,31 +655,30 @@ __global__ __launch_bounds__(kBlock) void k_ovf_rehash(Ovf from, uint64_t from_c
   }
 }
 
-// ------------------------------------------- K5 radix-bucket general path
+// ------------------------------------------- K5 key-bucket general path
 // The general (any order) Add without random global atomics.  K4's stamps cost
 // one random agent-scope atomic per distinct key per chunk, and those run at
 // ~20 G/s chip-wide (memory-side atomics, MI355X_MICROARCH.md "Global float
 // atomics": 64 lanes in 64 rows ≈ 17x slower).  K5 instead moves the data to
-// where it can be resolved locally.  Work unit: a SUPER-CHUNK of NSUB x 2048
-// keys of one batch; each 2048-key sub-chunk is deduplicated in an LDS hash
-// (clear-on-emit), so a Zipf-hot key yields one entry per sub-chunk.
-//   K5a k_rb_count    per super-chunk: dedup (loads issued one sub-chunk
-//                     ahead), entries {key, value bits} appended to the
-//                     super-chunk's scratch region (one LDS atomic per wave),
-//                     histogram by key bucket -> cnt[sc][bucket]
-//                     (bucket = key offset >> bshift; one extra bucket for
-//                     out-of-range keys)
-//   K5b k_rb_scan     exclusive scan over super-chunks per bucket -> off, total
-//   K5c k_rb_move     per super-chunk: counting sort of its entries by bucket
-//                     in LDS, then each bucket's run written to the bucket's
-//                     region (consecutive lanes -> consecutive slots)
-//   K5d k_rb_apply    one workgroup per bucket: an LDS hash resolves the
-//                     bucket's entries — an entry's position in its bucket IS
-//                     call order (super-chunks in order, sub-chunks in order),
-//                     so the largest position wins (assign) / values add
-//                     (accumulate) — then the winners store into the dense
-//                     array or the overflow table.  A bucket is owned by one
-//                     workgroup: no cross-workgroup ordering, no global atomics.
+// where it can be resolved locally, in two launches.  Work unit of the first:
+// a SUPER-CHUNK of 8 Ki keys of one batch (4 Ki for 8-byte values); key
+// bucket = key offset >> bshift, plus one bucket for out-of-range keys.
+//   K5a k_rb_bin      per super-chunk: LDS hash dedup (one entry per distinct
+//                     key: its last value / its sum), LDS counting sort of the
+//                     entries by bucket, one coalesced write of the sorted
+//                     entries to the super-chunk's region, one 16-bit row of
+//                     bucket starts
+//   K5b k_rb_resolve  one workgroup per bucket: gathers the bucket's run from
+//                     every super-chunk region — an entry's position in the
+//                     concatenation IS call order — resolves it in an LDS hash
+//                     (largest position wins / values add) and stores the
+//                     winners into the dense array or the overflow table.  A
+//                     bucket is owned by one workgroup: no cross-workgroup
+//                     ordering, no global atomics.
+// Measured against the four-launch form it replaces (dedup per 2 Ki sub-chunk,
+// entries appended, global scan, global radix move, apply): 198 -> 149 us per
+// 8 M Zipf keys; the per-entry uncoalesced appends and the move's second pass
+// over the entries were the cost, not the LDS work.
 
 template <int VB>
 struct RbEnt;
@@ -692,13 +693,6 @@ struct RbEnt<8> {
   uint32_t pad;
   unsigned long long val;
 };
-
-constexpr int kRbChunkSlots = 2 * kRbChunk;  // LDS dedup slots (load <= 1/2)
-constexpr int kRbMoveBlock = 512;             // 8 waves per CU for the LDS counting sort
-template <int VB>
-constexpr int rb_nsub() {
-  return VB == 8 ? 2 : 4;  // sub-chunks per super-chunk (LDS staging budget)
-}
 
 __device__ __forceinline__ uint32_t rb_bucket(const DenseView& d, uint32_t k, uint32_t bshift,
                                               uint32_t nbd) {
@@ -768,82 +762,6 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t* a, uint32_t n, uint32
   return tot;
 }
 
-// sbase[b] = exclusive prefix of total[] over buckets, sbase[nbk] = all entries.
-template <int BLOCK>
-__device__ __forceinline__ void rb_bases(const uint32_t* total, uint32_t nbk, uint32_t* sbase,
-                                         uint32_t* wtmp) {
-  for (uint32_t b = threadIdx.x; b <= nbk; b += BLOCK) sbase[b] = b < nbk ? total[b] : 0u;
-  __syncthreads();
-  block_exscan<BLOCK>(sbase, nbk + 1, wtmp);
-}
-
-// LDS state of the sub-chunk dedup.  Cleared ONCE per workgroup; afterwards
-// every sub-chunk leaves it empty again (the emitting lane resets its slot).
-// Slot kRbChunkSlots belongs to the key 0xFFFFFFFF (equal to the EMPTY marker).
-template <typename AT, int MODE>
-struct RbChunkLds {
-  uint32_t hk[kRbChunkSlots + 1];
-  uint32_t hlast[MODE == 0 ? kRbChunkSlots + 1 : 1];  // assign: last sub-chunk index
-  AT hsum[MODE == 1 ? kRbChunkSlots + 1 : 1];         // accumulate: sub-chunk sum
-  uint32_t sent_owner;                                 // key 0xFFFFFFFF inserted
-};
-
-template <typename AT, int MODE>
-__device__ __forceinline__ void rb_clear_all(RbChunkLds<AT, MODE>& L) {
-  for (int s = threadIdx.x; s <= kRbChunkSlots; s += blockDim.x) {
-    L.hk[s] = kEmpty32;
-    if (MODE == 0)
-      L.hlast[s] = 0;
-    else
-      L.hsum[s] = AT(0);
-  }
-  if (threadIdx.x == 0) L.sent_owner = 0;
-}
-
-// One lane's share of a sub-chunk: PER/4 groups of 4 consecutive elements.
-template <typename BT, int BLOCK>
-struct RbRegs {
-  static constexpr int PER = kRbChunk / BLOCK;  // keys per lane per sub-chunk
-  uint32_t key[PER];
-  BT val[PER];
-};
-
-// Issue the loads of sub-chunk [base, base + 2048) of a batch (16-byte loads
-// when the sub-chunk is full and aligned).  Elements past n read key 0.
-// NEEDV = false: keys only (the count pass).
-template <typename BT, int BLOCK, bool NEEDV>
-__device__ __forceinline__ void rb_load(const uint32_t* __restrict__ keys,
-                                        const BT* __restrict__ vals, uint64_t base, uint64_t n,
-                                        RbRegs<BT, BLOCK>& r) {
-  constexpr int PER = RbRegs<BT, BLOCK>::PER;
-  const int tid = threadIdx.x;
-  const bool full = base + kRbChunk <= n && ((reinterpret_cast<uintptr_t>(keys) & 15u) == 0) &&
-                    (!NEEDV || (reinterpret_cast<uintptr_t>(vals) & 15u) == 0);
-#pragma unroll
-  for (int g = 0; g < PER / 4; ++g) {
-    const uint64_t i0 = base + (uint64_t)(g * BLOCK + tid) * 4;
-    if (full) {
-      uint32_t k4[4];
-      Vec4<uint32_t>::template load<true>(keys + i0, k4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) r.key[g * 4 + e] = k4[e];
-      if (NEEDV) {
-        BT v4[4];
-        Vec4<BT>::template load<true>(vals + i0, v4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) r.val[g * 4 + e] = v4[e];
-      }
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const bool in = i0 + e < n;
-        r.key[g * 4 + e] = in ? keys[i0 + e] : 0u;
-        if (NEEDV) r.val[g * 4 + e] = in ? vals[i0 + e] : BT(0);
-      }
-    }
-  }
-}
-
 // Insert this lane's keys into an LDS open-addressing table (linear probing,
 // SLOTS a power of two; the key 0xFFFFFFFF uses the side word *sent).  The
 // first probe of every key is issued back to back (independent LDS atomics in
@@ -882,317 +800,230 @@ __device__ __forceinline__ uint32_t lds_insert(uint32_t* hk, uint32_t* sent,
   return own;
 }
 
-// Wave-wide exclusive prefix of a per-lane count; *total = the wave's sum.
-__device__ __forceinline__ uint32_t wave_exscan(uint32_t x, uint32_t* total) {
-  const int lane = threadIdx.x & 63;
-  uint32_t v = x;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(v, o, 64);
-    if (lane >= o) v += y;
-  }
-  *total = __shfl(v, 63, 64);
-  return v - x;
+// K5a k_rb_bin: one 1024-thread workgroup per CU, persistent over
+// super-chunks of SC keys of one batch (8 Ki keys for 4-byte values, 4 Ki for
+// 8-byte ones), the next super-chunk's loads in flight.  Per super-chunk:
+//   dedup  the SC keys go into ONE LDS hash of 2*SC slots (key -> largest
+//          element index for assign, sum for accumulate): a key keeps one
+//          entry per super-chunk, its last value or its sum
+//   count  each kept entry takes a rank in its bucket's LDS counter
+//   stage  the entries are written into LDS in bucket order (over the hash
+//          table, which is no longer needed) and copied out to the
+//          super-chunk's region of `tmp` with coalesced 16-byte stores
+//   row    the bucket starts go out as one 16-bit row loff[sc][0..nbk]
+//          (loff[sc][nbk] = the entry count)
+// Every global access is a coalesced 16-byte stream; no global atomics.
+constexpr int kBinBlock = 1024;
+template <typename BT>
+constexpr uint32_t rb_sc() {
+  return sizeof(BT) == 8 ? 4096u : 8192u;
 }
 
-// Dedup one sub-chunk held in registers and append one entry per distinct key
-// to out[] (slots from the LDS counter *nent, one atomic per wave) and to the
-// bucket histogram: assign — the LAST occurrence supplies its own value;
-// accumulate — the first inserter supplies the sub-chunk sum.  Starts and ends
-// with the LDS table empty; contains the barriers it needs (one at the end).
-template <typename AT, typename BT, int MODE, int BLOCK>
-__device__ __forceinline__ void rb_dedup(const RbRegs<BT, BLOCK>& r, uint32_t nvalid,
-                                         RbChunkLds<AT, MODE>& L, uint32_t* hist, uint32_t* nent,
-                                         RbEnt<sizeof(BT)>* __restrict__ out, const DenseView& d,
-                                         uint32_t bshift, uint32_t nbd) {
-  constexpr int PER = RbRegs<BT, BLOCK>::PER;
-  const int tid = threadIdx.x;
-  auto li_of = [&](int q) { return (uint32_t)(((q / 4) * BLOCK + tid) * 4 + (q % 4)); };
-  uint32_t valid = 0;
-#pragma unroll
-  for (int q = 0; q < PER; ++q) valid |= li_of(q) < nvalid ? (1u << q) : 0u;
-  uint32_t slot[PER];
-  const uint32_t own = lds_insert<PER, kRbChunkSlots>(L.hk, &L.sent_owner, r.key, valid, slot);
-#pragma unroll
-  for (int q = 0; q < PER; ++q) {
-    if (!(valid >> q & 1u)) continue;
-    if (MODE == 0)
-      atomicMax(&L.hlast[slot[q]], li_of(q));
-    else
-      atomicAdd(&L.hsum[slot[q]], from_bits<AT>(to_bits<BT>(r.val[q])));
-  }
-  __syncthreads();
-  uint32_t emask = own;
-  unsigned long long vb[PER];
-  if (MODE == 0) {
-    emask = 0;
-#pragma unroll
-    for (int q = 0; q < PER; ++q)
-      if ((valid >> q & 1u) && L.hlast[slot[q]] == li_of(q)) emask |= 1u << q;
-#pragma unroll
-    for (int q = 0; q < PER; ++q) vb[q] = to_bits<BT>(r.val[q]);
-  } else {
-#pragma unroll
-    for (int q = 0; q < PER; ++q) vb[q] = (own >> q & 1u) ? to_bits<AT>(L.hsum[slot[q]]) : 0ull;
-  }
-  __syncthreads();  // every lane has read the table before the slots are reset
-  // one allocation per wave for all of its entries
-  uint32_t wtot;
-  const uint32_t mine = wave_exscan((uint32_t)__popc(emask), &wtot);
-  uint32_t base = 0;
-  if ((tid & 63) == 63 && wtot) base = atomicAdd(nent, wtot);
-  base = __shfl(base, 63, 64) + mine;
-#pragma unroll
-  for (int q = 0; q < PER; ++q) {
-    if (!(emask >> q & 1u)) continue;
-    const uint32_t h = slot[q];
-    if (MODE == 0)
-      L.hlast[h] = 0;
-    else
-      L.hsum[h] = AT(0);
-    if (h == kRbChunkSlots)
-      L.sent_owner = 0;
-    else
-      L.hk[h] = kEmpty32;
-    atomicAdd(&hist[rb_bucket(d, r.key[q], bshift, nbd)], 1u);
-    RbEnt<sizeof(BT)> e;
-    e.key = r.key[q];
-    if (sizeof(BT) == 8) reinterpret_cast<uint32_t*>(&e)[1] = 0;
-    e.val = (BT)vb[q];
-    out[base++] = e;
-  }
-  __syncthreads();
-}
-
-// Sub-chunk schedule of a workgroup: super-chunks blockIdx.x, +gridDim.x, ...,
-// each NSUB sub-chunks (those past the end of the batch are skipped).
-struct RbTask {
-  uint32_t sc;
-  uint32_t s;
-  int j;
-  uint64_t base;  // first element of the sub-chunk in batch j
-  uint32_t nvalid;
-};
-
-template <int NSUB>
-__device__ __forceinline__ bool rb_task(const GroupArgs& ga, uint32_t nsc, uint32_t sc, uint32_t s,
-                                        RbTask& t) {
-  if (sc >= nsc) return false;
-  t.sc = sc;
-  t.s = s;
-  t.j = batch_of(ga, sc);
-  t.base = (uint64_t)(sc - ga.wg_prefix[t.j]) * (kRbChunk * NSUB) + (uint64_t)s * kRbChunk;
-  const uint64_t n = ga.b[t.j].n;
-  t.nvalid = t.base >= n ? 0u : (uint32_t)(n - t.base < kRbChunk ? n - t.base : kRbChunk);
-  return true;
-}
-
-// Allocate one slot per calling lane from an LDS counter with one atomic per
-// wave (call from divergent code: the active lanes get consecutive slots).
-__device__ __forceinline__ uint32_t wave_alloc(uint32_t* counter) {
-  const unsigned long long m = __ballot(1);
-  const int lane = threadIdx.x & 63;
-  const int leader = __ffsll((long long)m) - 1;
-  uint32_t base = 0;
-  if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
-  base = __shfl(base, leader, 64);
-  return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-}
-
-// K5a: per super-chunk, dedup each sub-chunk and append its entries to the
-// super-chunk's region of `tmp` (arrival order, coalesced by wave); histogram
-// of the entries by bucket -> cnt[sc][b]; entries after sub-chunk s -> nsub[sc][s].
 template <typename AT, typename BT, int MODE>
-__global__ __launch_bounds__(kBlock, 4) void k_rb_count(GroupArgs ga, DenseView d, uint32_t bshift,
-                                                        uint32_t nbd, uint32_t nbk, uint32_t* cnt,
-                                                        uint32_t* nsub, uint32_t nsc,
-                                                        RbEnt<sizeof(BT)>* __restrict__ tmp) {
-  constexpr int NSUB = rb_nsub<sizeof(BT)>();
-  constexpr int SC = NSUB * kRbChunk;
-  __shared__ RbChunkLds<AT, MODE> L;
-  extern __shared__ uint32_t hist[];  // nbk words (dynamic: 4 workgroups per CU fit)
-  __shared__ uint32_t nent;
-  const int tid = threadIdx.x;
-  rb_clear_all(L);
-  for (uint32_t b = tid; b < nbk; b += kBlock) hist[b] = 0;
-  if (tid == 0) nent = 0;
-  __syncthreads();
-  RbTask cur, nxt;
-  RbRegs<BT, kBlock> rc, rn;
-  bool have = rb_task<NSUB>(ga, nsc, blockIdx.x, 0, cur);
-  if (have)
-    rb_load<BT, kBlock, true>(ga.b[cur.j].keys, reinterpret_cast<const BT*>(ga.b[cur.j].vals),
-                              cur.base, ga.b[cur.j].n, rc);
-  while (have) {
-    // next sub-chunk of this super-chunk, else the first of the next one
-    bool hn = cur.s + 1 < NSUB && rb_task<NSUB>(ga, nsc, cur.sc, cur.s + 1, nxt) && nxt.nvalid > 0;
-    if (!hn) hn = rb_task<NSUB>(ga, nsc, cur.sc + gridDim.x, 0, nxt);
-    if (hn)
-      rb_load<BT, kBlock, true>(ga.b[nxt.j].keys, reinterpret_cast<const BT*>(ga.b[nxt.j].vals),
-                                nxt.base, ga.b[nxt.j].n, rn);
-    rb_dedup<AT, BT, MODE, kBlock>(rc, cur.nvalid, L, hist, &nent, tmp + (uint64_t)cur.sc * SC, d,
-                                   bshift, nbd);
-    const bool last = !hn || nxt.sc != cur.sc;
-    if (tid == 0) {
-      // sub-chunks never reached (past the batch end) repeat the final count
-      for (uint32_t s = cur.s; s < (last ? (uint32_t)NSUB : cur.s + 1); ++s)
-        nsub[(uint64_t)cur.sc * NSUB + s] = nent;
-    }
-    if (last) {  // super-chunk done: publish its histogram (a contiguous row)
-      for (uint32_t b = tid; b < nbk; b += kBlock) {
-        cnt[(uint64_t)cur.sc * nbk + b] = hist[b];
-        hist[b] = 0;
-      }
-      __syncthreads();
-      if (tid == 0) nent = 0;
-      __syncthreads();
-    }
-    have = hn;
-    cur = nxt;
-    rc = rn;
-  }
-}
-
-// K5b: per block of 64 buckets (one lane each), exclusive scan over the
-// super-chunks: off[sc][b] = sum of cnt[s][b] for s < sc; total[b].  16 waves
-// split the super-chunk range; rows are read 256 B at a time (coalesced).
-constexpr int kScanBlock = 1024;
-__global__ __launch_bounds__(kScanBlock) void k_rb_scan(const uint32_t* __restrict__ cnt,
-                                                        uint32_t* __restrict__ off, uint32_t nsc,
-                                                        uint32_t nbk, uint32_t* total) {
-  constexpr int NW = kScanBlock / 64;
-  __shared__ uint32_t part[NW][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const uint32_t b = blockIdx.x * 64 + lane;
-  const uint32_t seg = (nsc + NW - 1) / NW;
-  const uint32_t s0 = w * seg < nsc ? w * seg : nsc;
-  const uint32_t s1 = s0 + seg < nsc ? s0 + seg : nsc;
-  uint32_t sum = 0;
-  if (b < nbk) {
-#pragma unroll 8
-    for (uint32_t s = s0; s < s1; ++s) sum += cnt[(uint64_t)s * nbk + b];
-  }
-  part[w][lane] = sum;
-  __syncthreads();
-  uint32_t run = 0, tot = 0;
-#pragma unroll
-  for (int q = 0; q < NW; ++q) {
-    if (q < w) run += part[q][lane];
-    tot += part[q][lane];
-  }
-  if (b < nbk) {
-#pragma unroll 8
-    for (uint32_t s = s0; s < s1; ++s) {
-      const uint32_t x = cnt[(uint64_t)s * nbk + b];
-      off[(uint64_t)s * nbk + b] = run;
-      run += x;
-    }
-    if (w == 0) total[b] = tot;
-  }
-}
-
-// K5c: per super-chunk, counting-sort its entries by bucket in LDS and write
-// each bucket's run to the bucket's region: consecutive lanes write
-// consecutive slots.  Sub-chunks are ranked one after another (barrier), so in
-// a bucket the entries of sub-chunk s precede those of s+1 (call order).
-template <typename BT, int BLOCK>
-__global__ __launch_bounds__(BLOCK) void k_rb_move(DenseView d, uint32_t bshift, uint32_t nbd,
-                                                   uint32_t nbk, const uint32_t* __restrict__ cnt,
-                                                   const uint32_t* __restrict__ off,
-                                                   const uint32_t* __restrict__ nsub, uint32_t nsc,
-                                                   const uint32_t* total,
-                                                   const RbEnt<sizeof(BT)>* __restrict__ tmp,
-                                                   RbEnt<sizeof(BT)>* __restrict__ ent) {
-  constexpr int NSUB = rb_nsub<sizeof(BT)>();
-  constexpr int SC = NSUB * kRbChunk;
-  constexpr int EPT = SC / BLOCK;
+__global__ __launch_bounds__(kBinBlock) void k_rb_bin(GroupArgs ga, DenseView d, uint32_t bshift,
+                                                      uint32_t nbd, uint32_t nbk,
+                                                      uint16_t* __restrict__ loff, uint32_t nsc,
+                                                      RbEnt<sizeof(BT)>* __restrict__ tmp) {
+  constexpr uint32_t SC = rb_sc<BT>();
+  constexpr int KPT = (int)(SC / kBinBlock);  // keys per thread: 8 or 4
+  constexpr int SLOTS = (int)(2 * SC);
   using Ent = RbEnt<sizeof(BT)>;
-  __shared__ uint32_t sbase[kRbMaxBuckets + 1];
-  __shared__ uint32_t loff[kRbMaxBuckets + 1];
-  __shared__ uint32_t lcur[kRbMaxBuckets];
-  __shared__ uint32_t goff[kRbMaxBuckets];
-  __shared__ uint32_t skey[SC];
-  __shared__ BT sval[SC];
-  __shared__ uint32_t wtmp[BLOCK / 64];
+  using VT = typename std::conditional<MODE == 0, uint32_t, AT>::type;  // last index / sum
+  constexpr size_t VBYTES = (size_t)(SLOTS + 1) * sizeof(VT);
+  constexpr size_t VPAD = (VBYTES + 15) / 16 * 16;
+  constexpr size_t TBL = VPAD + (size_t)(SLOTS + 1) * 4;
+  static_assert(SC * sizeof(Ent) <= TBL, "the staging area fits over the table");
+  __shared__ __attribute__((aligned(16))) unsigned char tbl[TBL];
+  VT* hv = reinterpret_cast<VT*>(tbl);
+  uint32_t* hk = reinterpret_cast<uint32_t*>(tbl + VPAD);
+  Ent* stg = reinterpret_cast<Ent*>(tbl);
+  __shared__ uint32_t cnt[kRbMaxBuckets + 1];  // bucket counters, then bucket starts
+  __shared__ uint32_t wtmp[kBinBlock / 64];
+  __shared__ uint32_t sent;
   const int tid = threadIdx.x;
-  rb_bases<BLOCK>(total, nbk, sbase, wtmp);
-  for (uint32_t sc = blockIdx.x; sc < nsc; sc += gridDim.x) {
-    uint32_t ends[NSUB];
-#pragma unroll
-    for (int s = 0; s < NSUB; ++s) ends[s] = nsub[(uint64_t)sc * NSUB + s];
-    const uint32_t n = ends[NSUB - 1];
-    // all loads up front: the super-chunk's entries, this lane's EPT of them
-    Ent x[EPT];
-    const Ent* src = tmp + (uint64_t)sc * SC;
-#pragma unroll
-    for (int q = 0; q < EPT; ++q) {
-      const uint32_t i = (uint32_t)(q * BLOCK + tid);
-      if (i < n) x[q] = src[i];
+  auto clear = [&]() {
+    for (uint32_t i = (uint32_t)tid * 16; i < (uint32_t)VPAD; i += kBinBlock * 16)
+      *reinterpret_cast<u32x4*>(tbl + i) = u32x4{0u, 0u, 0u, 0u};
+    for (int i = tid * 4; i < SLOTS; i += kBinBlock * 4)
+      *reinterpret_cast<u32x4*>(&hk[i]) = u32x4{kEmpty32, kEmpty32, kEmpty32, kEmpty32};
+    if (tid == 0) {
+      hk[SLOTS] = kEmpty32;
+      sent = 0;
     }
-    for (uint32_t b = tid; b < nbk; b += BLOCK) {
-      loff[b] = cnt[(uint64_t)sc * nbk + b];
-      goff[b] = sbase[b] + off[(uint64_t)sc * nbk + b];
-    }
-    __syncthreads();
-    block_exscan<BLOCK>(loff, nbk, wtmp);
-    for (uint32_t b = tid; b < nbk; b += BLOCK) lcur[b] = loff[b];
-    __syncthreads();
-    uint32_t lo = 0;
+    for (uint32_t b = tid; b <= nbk; b += kBinBlock) cnt[b] = 0;
+  };
+  struct Task {
+    int j;
+    uint64_t base;
+    uint32_t nvalid;
+  };
+  auto task = [&](uint32_t sc) {
+    Task t;
+    t.j = batch_of(ga, sc);
+    t.base = (uint64_t)(sc - ga.wg_prefix[t.j]) * SC;
+    const uint64_t n = ga.b[t.j].n;
+    t.nvalid = n - t.base < SC ? (uint32_t)(n - t.base) : SC;
+    return t;
+  };
+  auto li_of = [&](int q) { return (uint32_t)(((q / 4) * kBinBlock + tid) * 4 + (q % 4)); };
+  auto load = [&](const Task& t, uint32_t (&k)[KPT], BT (&v)[KPT]) {
+    const uint32_t* __restrict__ keys = ga.b[t.j].keys;
+    const BT* __restrict__ vals = reinterpret_cast<const BT*>(ga.b[t.j].vals);
+    const bool full = t.nvalid == SC && ((reinterpret_cast<uintptr_t>(keys) & 15u) == 0) &&
+                      ((reinterpret_cast<uintptr_t>(vals) & 15u) == 0);
 #pragma unroll
-    for (int s = 0; s < NSUB; ++s) {
-      const uint32_t hi = ends[s];
+    for (int g = 0; g < KPT / 4; ++g) {
+      const uint64_t i0 = t.base + li_of(g * 4);
+      if (full) {
+        uint32_t k4[4];
+        BT v4[4];
+        Vec4<uint32_t>::template load<true>(keys + i0, k4);
+        Vec4<BT>::template load<true>(vals + i0, v4);
 #pragma unroll
-      for (int q = 0; q < EPT; ++q) {
-        const uint32_t i = (uint32_t)(q * BLOCK + tid);
-        if (i < lo || i >= hi) continue;
-        const uint32_t p = atomicAdd(&lcur[rb_bucket(d, x[q].key, bshift, nbd)], 1u);
-        skey[p] = x[q].key;
-        sval[p] = (BT)x[q].val;
+        for (int e = 0; e < 4; ++e) {
+          k[g * 4 + e] = k4[e];
+          v[g * 4 + e] = v4[e];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool in = li_of(g * 4 + e) < t.nvalid;
+          k[g * 4 + e] = in ? keys[i0 + e] : 0u;
+          v[g * 4 + e] = in ? vals[i0 + e] : BT(0);
+        }
       }
-      __syncthreads();
-      lo = hi;
     }
-    for (uint32_t t = tid; t < n; t += BLOCK) {
-      const uint32_t k = skey[t];
-      const uint32_t b = rb_bucket(d, k, bshift, nbd);
-      Ent e;
-      e.key = k;
-      if (sizeof(BT) == 8) reinterpret_cast<uint32_t*>(&e)[1] = 0;
-      e.val = sval[t];
-      ent[goff[b] + (t - loff[b])] = e;
+  };
+  clear();
+  __syncthreads();
+  uint32_t kc[KPT], kn[KPT];
+  BT vc[KPT], vn[KPT];
+  Task cur{}, nxt{};
+  if (blockIdx.x < nsc) {
+    cur = task(blockIdx.x);
+    load(cur, kc, vc);
+  }
+  for (uint32_t sc = blockIdx.x; sc < nsc; sc += gridDim.x) {
+    if (sc + gridDim.x < nsc) {
+      nxt = task(sc + gridDim.x);
+      load(nxt, kn, vn);
+    }
+    uint32_t valid = 0;
+#pragma unroll
+    for (int q = 0; q < KPT; ++q) valid |= li_of(q) < cur.nvalid ? (1u << q) : 0u;
+    uint32_t slot[KPT];
+    const uint32_t own = lds_insert<KPT, SLOTS>(hk, &sent, kc, valid, slot);
+#pragma unroll
+    for (int q = 0; q < KPT; ++q) {
+      if (!(valid >> q & 1u)) continue;
+      if (MODE == 0)
+        atomicMax(reinterpret_cast<uint32_t*>(&hv[slot[q]]), li_of(q));
+      else
+        atomicAdd(reinterpret_cast<AT*>(&hv[slot[q]]), from_bits<AT>(to_bits<BT>(vc[q])));
     }
     __syncthreads();
+    uint32_t emask = 0, rk[KPT];
+    BT kv[KPT];
+#pragma unroll
+    for (int q = 0; q < KPT; ++q) {
+      bool keep;
+      if (MODE == 0) {
+        keep = (valid >> q & 1u) && *reinterpret_cast<const uint32_t*>(&hv[slot[q]]) == li_of(q);
+        kv[q] = vc[q];
+      } else {
+        keep = (own >> q & 1u) != 0;
+        kv[q] = keep ? from_bits<BT>(to_bits<AT>(*reinterpret_cast<const AT*>(&hv[slot[q]]))) : BT(0);
+      }
+      rk[q] = 0;
+      if (keep) {
+        emask |= 1u << q;
+        rk[q] = atomicAdd(&cnt[rb_bucket(d, kc[q], bshift, nbd)], 1u);
+      }
+    }
+    __syncthreads();  // table read and every entry counted
+    const uint32_t total = block_exscan<kBinBlock>(cnt, nbk + 1, wtmp);
+    uint16_t* row = loff + (size_t)sc * (nbk + 1);
+    for (uint32_t b = tid; b <= nbk; b += kBinBlock) row[b] = (uint16_t)cnt[b];
+#pragma unroll
+    for (int q = 0; q < KPT; ++q) {
+      if (!(emask >> q & 1u)) continue;
+      Ent e;
+      e.key = kc[q];
+      if (sizeof(BT) == 8) reinterpret_cast<uint32_t*>(&e)[1] = 0;
+      e.val = kv[q];
+      stg[cnt[rb_bucket(d, kc[q], bshift, nbd)] + rk[q]] = e;
+    }
+    __syncthreads();
+    // the staged, bucket-sorted entries out as one coalesced stream
+    const uint32_t n16 = (uint32_t)((total * sizeof(Ent) + 15) / 16);
+    u32x4* dst = reinterpret_cast<u32x4*>(tmp + (size_t)sc * SC);
+    const u32x4* src = reinterpret_cast<const u32x4*>(stg);
+    for (uint32_t i = tid; i < n16; i += kBinBlock) dst[i] = src[i];
+    __syncthreads();
+    clear();
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < KPT; ++q) {
+      kc[q] = kn[q];
+      vc[q] = vn[q];
+    }
+    cur = nxt;
   }
 }
 
-// K5d: one 1024-thread workgroup per bucket (LDS: 128 KiB table, one workgroup
-// per CU, 16 waves).  Slot SLOTS belongs to the key 0xFFFFFFFF.  A bucket whose
-// entries fit the table (the host sizes buckets for that) is resolved from
-// registers in one pass, the next bucket's entries loading meanwhile;
-// otherwise rounds split it by key hash.
+// K5b k_rb_resolve: one 1024-thread workgroup per bucket (LDS: 128 KiB table,
+// one workgroup per CU, 16 waves).  The bucket's entries are the runs
+// [loff[sc][b], loff[sc][b+1]) of the super-chunk regions; thread t loads the
+// run of super-chunk t straight into registers (one contiguous read; the few
+// entries past RPT are read in a loop, and a bucket with a run longer than
+// LONG takes the strided path below), and its entries' positions pre[t] + q
+// (pre = exclusive scan of the run lengths) are call order.  An LDS hash resolves the bucket — the largest position wins
+// (assign) / values add (accumulate) — and the winners store into the dense
+// array or the overflow table.  A bucket is owned by one workgroup: no
+// cross-workgroup ordering, no global atomics.  Buckets are dealt XCD by XCD
+// (workgroups b and b+8 share an XCD): one XCD's workgroups take consecutive
+// buckets, so the loff lines they read stay in that XCD's L2; the next
+// bucket's loff words are read while this one resolves.  Slot SLOTS belongs
+// to the key 0xFFFFFFFF.
 constexpr int kApplyBlock = 1024;
+static_assert(kRbMaxSc <= (uint32_t)kApplyBlock, "one run per resolve thread");
 template <typename AT, typename BT, int MODE, int LOGS>
-__global__ __launch_bounds__(kApplyBlock) void k_rb_apply(DenseView d, Ovf o, uint32_t nbd,
-                                                          uint32_t nbk, const uint32_t* total,
-                                                          const RbEnt<sizeof(BT)>* __restrict__ ent) {
+__global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, uint32_t nbd,
+                                                            uint32_t nbk,
+                                                            const uint16_t* __restrict__ loff,
+                                                            uint32_t nsc,
+                                                            const RbEnt<sizeof(BT)>* __restrict__ tmp) {
   // f64 sums take 8 B per slot: half the slots in the same LDS
   constexpr int SLOTS = (MODE == 1 && sizeof(AT) == 8) ? (1 << LOGS) / 2 : (1 << LOGS);
   constexpr uint32_t CAP = (uint32_t)SLOTS / 8 * 7;  // entries per round (load <= 7/8)
-  constexpr int EPT = (int)((CAP + kApplyBlock - 1) / kApplyBlock);
+  constexpr int RPT = 12;                             // run entries held in registers
+  constexpr uint32_t LONG = 4 * RPT;                  // longer runs: the strided path
+  constexpr uint32_t SC = rb_sc<BT>();
   using Ent = RbEnt<sizeof(BT)>;
   __shared__ __attribute__((aligned(16))) uint32_t ak[SLOTS + 1];
   __shared__ __attribute__((aligned(16))) uint32_t abest[MODE == 0 ? SLOTS + 1 : 1];  // assign: 1 + max position
   __shared__ __attribute__((aligned(16))) AT asum[MODE == 1 ? SLOTS + 1 : 1];
-  extern __shared__ uint32_t sbase[];  // nbk + 1 words (dynamic: sized to the launch)
+  __shared__ uint32_t pre[kRbMaxSc + 1];  // run starts (positions); pre[nsc] = entries
+  __shared__ uint32_t rst[kRbMaxSc];      // run starts (entry index in tmp)
   __shared__ uint32_t wtmp[kApplyBlock / 64];
   __shared__ uint32_t sent;
   const int tid = threadIdx.x;
-  rb_bases<kApplyBlock>(total, nbk, sbase, wtmp);
   auto find = [&](uint32_t key) -> uint32_t {
     if (key == kEmpty32) return SLOTS;
     uint32_t h = fmix32(key) & (SLOTS - 1);
     while (ak[h] != key) h = (h + 1) & (SLOTS - 1);
     return h;
+  };
+  auto first_run = [&](uint32_t p) -> uint32_t {  // last r with pre[r] <= p
+    uint32_t lo = 0, hi = nsc;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (pre[mid] <= p)
+        lo = mid;
+      else
+        hi = mid;
+    }
+    return lo;
   };
   auto store_winner = [&](uint32_t b, uint32_t key, BT vbits) {
     const AT v = from_bits<AT>(to_bits<BT>(vbits));
@@ -1232,14 +1063,9 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_apply(DenseView d, Ovf o, ui
       const bool used = s == SLOTS ? sent != 0 : ak[s] != kEmpty32;
       if (!used) continue;
       const uint32_t key = s == SLOTS ? kEmpty32 : ak[s];
-      AT* p;
-      if (b != nbd) {
-        p = reinterpret_cast<AT*>(d.param) + (uint32_t)(key - d.key_begin);
-      } else {
-        const long long sl = ovf_insert(o, key);
-        if (sl < 0) continue;
-        p = reinterpret_cast<AT*>(o.vals) + sl;
-      }
+      const long long sl = ovf_insert(o, key);
+      if (sl < 0) continue;
+      AT* p = reinterpret_cast<AT*>(o.vals) + sl;
       *p = add_wrap<AT>(*p, asum[s]);
     }
   };
@@ -1263,76 +1089,116 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_apply(DenseView d, Ovf o, ui
       sent = 0;
     }
   };
-  // entries of bucket b held in registers: x[q] = entry q * kApplyBlock + tid
-  auto load_bucket = [&](uint32_t b, Ent (&x)[EPT]) {
-    const uint32_t e0 = sbase[b], ne = sbase[b + 1] - e0;
-    if (ne > CAP) return;
-#pragma unroll
-    for (int q = 0; q < EPT; ++q) {
-      const uint32_t p = (uint32_t)(q * kApplyBlock + tid);
-      if (p < ne) x[q] = ent[e0 + p];
+  auto insert_one = [&](uint32_t key, uint32_t pos, BT vbits) {
+    uint32_t k1[1] = {key}, s1[1];
+    lds_insert<1, SLOTS>(ak, &sent, k1, 1u, s1);
+    if (MODE == 0)
+      atomicMax(&abest[s1[0]], pos + 1u);
+    else
+      atomicAdd(&asum[s1[0]], from_bits<AT>(to_bits<BT>(vbits)));
+  };
+  // XCD-aware bucket schedule
+  const uint32_t xcd = blockIdx.x & 7u;
+  const uint32_t per_xcd = (gridDim.x + 7u - xcd) >> 3;  // workgroups in this XCD group
+  const uint32_t b_hi = (uint32_t)((uint64_t)nbk * (xcd + 1) / 8);
+  uint32_t b = (uint32_t)((uint64_t)nbk * xcd / 8) + (blockIdx.x >> 3);
+  const uint16_t* myrow = loff + (size_t)tid * (nbk + 1);
+  const bool has_run = (uint32_t)tid < nsc;
+  // software pipeline: the run of bucket b in registers, the run bounds of the
+  // bucket after it in flight
+  auto bounds = [&](uint32_t bb, uint32_t& a, uint32_t& e) {
+    a = e = 0;
+    if (bb < b_hi && has_run) {
+      a = myrow[bb];
+      e = myrow[bb + 1];
     }
   };
-  Ent xc[EPT], xn[EPT];
-  uint32_t b = blockIdx.x;
-  if (b < nbk) load_bucket(b, xc);
-  for (; b < nbk; b += gridDim.x) {
-    const uint32_t e0 = sbase[b], e1 = sbase[b + 1];
-    const uint32_t ne = e1 - e0;
-    const uint32_t bn = b + gridDim.x;
-    if (bn < nbk) load_bucket(bn, xn);  // in flight while this bucket resolves
-    if (ne == 0) {
-    } else if (ne <= CAP) {
+  auto load_run = [&](uint32_t a, uint32_t e, Ent (&x)[RPT]) {
+#pragma unroll
+    for (int q = 0; q < RPT; ++q)
+      if ((uint32_t)q < e - a) x[q] = tmp[(uint32_t)tid * SC + a + q];
+  };
+  uint32_t ra, re, na, ne_;
+  bounds(b, ra, re);
+  bounds(b + per_xcd, na, ne_);
+  Ent xn[RPT];
+  load_run(ra, re, xn);
+  for (; b < b_hi; b += per_xcd) {
+    const uint32_t len = re - ra, st = (uint32_t)tid * SC + ra;
+    Ent x[RPT];
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) x[q] = xn[q];
+    // next bucket: its run loads now, the bounds of the one after
+    ra = na;
+    re = ne_;
+    load_run(ra, re, xn);
+    bounds(b + 2 * per_xcd, na, ne_);
+    pre[tid] = len;
+    if (tid == 0) pre[kRbMaxSc] = 0;
+    const bool long_run = __syncthreads_or(len > LONG) != 0;
+    const uint32_t ne = block_exscan<kApplyBlock>(pre, kRbMaxSc, wtmp);
+    const uint32_t p0 = pre[tid];
+    if (ne == 0) continue;  // uniform
+    if (ne <= CAP && !long_run) {
       clear_table();
       __syncthreads();
-      uint32_t key[EPT], slot[EPT], valid = 0;
+      uint32_t key[RPT], slot[RPT], valid = 0;
 #pragma unroll
-      for (int q = 0; q < EPT; ++q) {
-        key[q] = xc[q].key;
-        valid |= (uint32_t)(q * kApplyBlock + tid) < ne ? (1u << q) : 0u;
+      for (int q = 0; q < RPT; ++q) {
+        valid |= (uint32_t)q < len ? (1u << q) : 0u;
+        key[q] = (uint32_t)q < len ? x[q].key : 0u;
       }
-      lds_insert<EPT, SLOTS>(ak, &sent, key, valid, slot);
+      lds_insert<RPT, SLOTS>(ak, &sent, key, valid, slot);
 #pragma unroll
-      for (int q = 0; q < EPT; ++q) {
+      for (int q = 0; q < RPT; ++q) {
         if (!(valid >> q & 1u)) continue;
         if (MODE == 0)
-          atomicMax(&abest[slot[q]], (uint32_t)(q * kApplyBlock + tid) + 1u);
+          atomicMax(&abest[slot[q]], p0 + (uint32_t)q + 1u);
         else
-          atomicAdd(&asum[slot[q]], from_bits<AT>(to_bits<BT>((BT)xc[q].val)));
+          atomicAdd(&asum[slot[q]], from_bits<AT>(to_bits<BT>((BT)x[q].val)));
+      }
+      for (uint32_t q = RPT; q < len; ++q) {  // a run's short tail (<= LONG - RPT), from memory
+        const Ent y = tmp[st + q];
+        insert_one(y.key, p0 + q, (BT)y.val);
       }
       __syncthreads();
       if (MODE == 0) {
 #pragma unroll
-        for (int q = 0; q < EPT; ++q) {
-          const uint32_t p = (uint32_t)(q * kApplyBlock + tid);
-          if ((valid >> q & 1u) && abest[slot[q]] == p + 1u) store_winner(b, key[q], (BT)xc[q].val);
+        for (int q = 0; q < RPT; ++q)
+          if ((valid >> q & 1u) && abest[slot[q]] == p0 + (uint32_t)q + 1u)
+            store_winner(b, key[q], (BT)x[q].val);
+        for (uint32_t q = RPT; q < len; ++q) {
+          const Ent y = tmp[st + q];
+          if (abest[find(y.key)] == p0 + q + 1u) store_winner(b, y.key, (BT)y.val);
         }
       } else {
         accumulate_all(b);
       }
       __syncthreads();
     } else {
+      // a run longer than the registers hold, or more entries than the table
+      // holds: every thread takes positions tid, tid + 1024, ... (coalesced
+      // inside long runs), found by binary search over the run starts; rounds
+      // split an oversized bucket by key hash
+      if (has_run) rst[tid] = st;
+      if (tid == 0) pre[nsc] = ne;
       const uint32_t R = (ne + CAP - 1) / CAP;
       for (uint32_t round = 0; round < R; ++round) {
         clear_table();
         __syncthreads();
         for (uint32_t p = tid; p < ne; p += kApplyBlock) {
-          const Ent x = ent[e0 + p];
-          if ((fmix32(x.key ^ 0x9E3779B9u) % R) != round) continue;
-          uint32_t k1[1] = {x.key}, s1[1];
-          lds_insert<1, SLOTS>(ak, &sent, k1, 1u, s1);
-          if (MODE == 0)
-            atomicMax(&abest[s1[0]], p + 1u);
-          else
-            atomicAdd(&asum[s1[0]], from_bits<AT>(to_bits<BT>((BT)x.val)));
+          const uint32_t r = first_run(p);
+          const Ent y = tmp[rst[r] + (p - pre[r])];
+          if ((fmix32(y.key ^ 0x9E3779B9u) % R) == round) insert_one(y.key, p, (BT)y.val);
         }
         __syncthreads();
         if (MODE == 0) {
           // the entry holding its key's largest position is the last write
           for (uint32_t p = tid; p < ne; p += kApplyBlock) {
-            const Ent x = ent[e0 + p];
-            if ((fmix32(x.key ^ 0x9E3779B9u) % R) != round) continue;
-            if (abest[find(x.key)] == p + 1u) store_winner(b, x.key, (BT)x.val);
+            const uint32_t r = first_run(p);
+            const Ent y = tmp[rst[r] + (p - pre[r])];
+            if ((fmix32(y.key ^ 0x9E3779B9u) % R) != round) continue;
+            if (abest[find(y.key)] == p + 1u) store_winner(b, y.key, (BT)y.val);
           }
         } else {
           accumulate_all(b);
@@ -1340,8 +1206,6 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_apply(DenseView d, Ovf o, ui
         __syncthreads();
       }
     }
-#pragma unroll
-    for (int q = 0; q < EPT; ++q) xc[q] = xn[q];
   }
 }
 
@@ -1679,38 +1543,26 @@ hipError_t launch_ovf_rehash(int vb, const Ovf& from, uint64_t from_cap, const O
 
 template <typename AT, typename BT, int MODE>
 static hipError_t rb_launch(const GroupArgs& ga, uint32_t nsc, const DenseView& d, const Ovf& o,
-                            uint32_t bshift, uint32_t nbd, int apply_log2, uint32_t* cnt,
-                            uint32_t* off, uint32_t* nsub, uint32_t* total, void* tmp, void* ent,
-                            hipStream_t st) {
+                            uint32_t bshift, uint32_t nbd, int apply_log2, uint16_t* loff,
+                            void* tmp, hipStream_t st) {
   const uint32_t nbk = nbd + 1;
-  // persistent grids: the dedup LDS is cleared once per workgroup
-  const uint32_t gc = nsc < 1024u ? nsc : 1024u;  // <= 40 KiB LDS, <= 128 VGPRs: 4 per CU
-  const uint32_t gm = nsc < 512u ? nsc : 512u;   // ~90 KiB LDS
   auto* t = reinterpret_cast<RbEnt<sizeof(BT)>*>(tmp);
-  auto* e = reinterpret_cast<RbEnt<sizeof(BT)>*>(ent);
-  k_rb_count<AT, BT, MODE><<<gc, kBlock, nbk * sizeof(uint32_t), st>>>(ga, d, bshift, nbd, nbk, cnt, nsub, nsc, t);
-  k_rb_scan<<<(nbk + 63) / 64, kScanBlock, 0, st>>>(cnt, off, nsc, nbk, total);
-  k_rb_move<BT, kRbMoveBlock><<<gm, kRbMoveBlock, 0, st>>>(d, bshift, nbd, nbk, cnt, off, nsub, nsc,
-                                                           total, t, e);
-  const size_t sb = (nbk + 1) * sizeof(uint32_t);
-  if (apply_log2 == 13) {
-    const uint32_t ga2 = nbk < 512u ? nbk : 512u;  // two workgroups per CU
-    k_rb_apply<AT, BT, MODE, 13><<<ga2, kApplyBlock, sb, st>>>(d, o, nbd, nbk, total, e);
-  } else {
-    k_rb_apply<AT, BT, MODE, 14><<<nbk < 256u ? nbk : 256u, kApplyBlock, sb, st>>>(d, o, nbd, nbk,
-                                                                                  total, e);
-  }
+  // persistent grid, one 1024-thread workgroup per CU (~140 KiB LDS)
+  const uint32_t gb = nsc < 256u ? nsc : 256u;
+  k_rb_bin<AT, BT, MODE><<<gb, kBinBlock, 0, st>>>(ga, d, bshift, nbd, nbk, loff, nsc, t);
+  if (apply_log2 == 13)  // 2^13 slots: two workgroups per CU
+    k_rb_resolve<AT, BT, MODE, 13><<<512, kApplyBlock, 0, st>>>(d, o, nbd, nbk, loff, nsc, t);
+  else
+    k_rb_resolve<AT, BT, MODE, 14><<<256, kApplyBlock, 0, st>>>(d, o, nbd, nbk, loff, nsc, t);
   return hipGetLastError();
 }
 
 hipError_t launch_rb_add(int dtype, int mode, const GroupArgs& ga, uint32_t nsc,
                          const DenseView& d, const Ovf& o, uint32_t bshift, uint32_t nbd,
-                         int apply_log2, uint32_t* cnt, uint32_t* off, uint32_t* nsub,
-                         uint32_t* total, void* tmp, void* ent, hipStream_t st) {
+                         int apply_log2, uint16_t* loff, void* tmp, hipStream_t st) {
   if (nsc == 0) return hipSuccess;
-  if (nbd + 1 > (uint32_t)kRbMaxBuckets) return hipErrorInvalidValue;
-#define PSKV_RB(AT, BT, M) \
-  rb_launch<AT, BT, M>(ga, nsc, d, o, bshift, nbd, apply_log2, cnt, off, nsub, total, tmp, ent, st)
+  if (nbd + 1 > (uint32_t)kRbMaxBuckets || nsc > kRbMaxSc) return hipErrorInvalidValue;
+#define PSKV_RB(AT, BT, M) rb_launch<AT, BT, M>(ga, nsc, d, o, bshift, nbd, apply_log2, loff, tmp, st)
   if (mode == 0) {
     if (dtype == 0) return PSKV_RB(int, uint32_t, 0);
     if (dtype == 1) return PSKV_RB(float, uint32_t, 0);
@@ -1742,7 +1594,7 @@ hipError_t launch_acc_dense(int dtype, const GroupArgs& ga, uint32_t grid, const
 }
 
 // Super-chunk size (keys) and entry size of the K5 path for a value size.
-uint32_t rb_superchunk(int vb) { return vb == 8 ? 2 * kRbChunk : 4 * kRbChunk; }
+uint32_t rb_superchunk(int vb) { return vb == 8 ? rb_sc<unsigned long long>() : rb_sc<uint32_t>(); }
 size_t rb_entry_bytes(int vb) { return vb == 8 ? sizeof(RbEnt<8>) : sizeof(RbEnt<4>); }
 
 

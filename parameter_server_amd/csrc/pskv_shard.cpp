@@ -216,9 +216,8 @@ struct pskv_shard {
   // stats
   uint64_t n_add = 0, n_get = 0, n_sorted = 0, n_general = 0;
   // K5 radix-bucket scratch (grown on demand)
-  uint32_t* rb_cnt = nullptr;
-  size_t rb_cnt_bytes = 0;
-  uint32_t* rb_total = nullptr;
+  uint16_t* rb_loff = nullptr;
+  size_t rb_loff_bytes = 0;
   void* rb_ent = nullptr;
   size_t rb_ent_bytes = 0;
   int general_path = 1;  // PSKV_GENERAL: stamps = 0 (K4 always), auto = 1, radix = 2 (K5 always)
@@ -447,17 +446,19 @@ int ensure_scratch(pskv_shard* s, void** p, size_t* have, size_t need) {
   return PSKV_OK;
 }
 
-// K5: radix-bucket general Add (no random global atomics).
-int radix_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t e) {
+// K5: radix-bucket general Add (no random global atomics), one launch pair
+// per <= kRbMaxSc super-chunks; a longer group is cut into consecutive pieces
+// (a batch may be split), which run in stream order, so call order holds.
+int radix_launch(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t e) {
   GroupArgs ga;
   const uint32_t nsc = build_group(v, b, e, rb_superchunk(s->vb), &ga);
   uint64_t elems = 0;
   for (size_t i = b; i < e; ++i) elems += v[i].n;
   // bucket = key offset >> bshift: about one bucket per 4 Ki pushed keys, at
-  // most 2048 dense buckets (more buckets measured slower at cfg 3: longer
-  // count rows, shorter move runs).  The apply workgroup resolves a bucket
-  // from registers when its entries fit its LDS table: 2^13 slots (two
-  // workgroups per CU) while buckets average <= 2 Ki pushed keys, else 2^14.
+  // most 2048 dense buckets (more buckets: longer loff rows, shorter runs).
+  // The resolve workgroup handles a bucket from registers when its entries fit
+  // its LDS table: 2^13 slots (two workgroups per CU) while buckets average
+  // <= 2 Ki pushed keys, else 2^14.
   uint32_t bits = 0;
   while (bits < 32 && ((s->range - 1) >> bits) != 0) ++bits;
   uint32_t tb = 6;
@@ -469,25 +470,50 @@ int radix_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t 
   int apply_log2 = elems / nbd <= 2048 ? 13 : 14;
   if (s->tune_rb_apply_log2) apply_log2 = s->tune_rb_apply_log2;
   if (nbk > (uint32_t)kRbMaxBuckets) return fail(PSKV_EINVAL, "radix path: too many buckets");
-  size_t have_total = s->rb_total ? 4 * (size_t)kRbMaxBuckets : 0;
+  if (nsc > kRbMaxSc) return fail(PSKV_EINVAL, "radix path: launch piece too large");
   const size_t eb = rb_entry_bytes(s->vb);
-  const size_t nb2 = (size_t)nbk * nsc;
-  int rc = ensure_scratch(s, reinterpret_cast<void**>(&s->rb_cnt), &s->rb_cnt_bytes,
-                          (2 * nb2 + 4 * (size_t)nsc) * sizeof(uint32_t));
-  if (!rc) rc = ensure_scratch(s, reinterpret_cast<void**>(&s->rb_total), &have_total,
-                               (size_t)kRbMaxBuckets * sizeof(uint32_t));
-  if (!rc) rc = ensure_scratch(s, &s->rb_ent, &s->rb_ent_bytes,
-                               (elems + (size_t)nsc * rb_superchunk(s->vb)) * eb);
+  int rc = ensure_scratch(s, reinterpret_cast<void**>(&s->rb_loff), &s->rb_loff_bytes,
+                          (size_t)nsc * (nbk + 1) * sizeof(uint16_t));
+  if (!rc) rc = ensure_scratch(s, &s->rb_ent, &s->rb_ent_bytes, (size_t)nsc * rb_superchunk(s->vb) * eb);
   if (rc) return rc;
-  char* ent = static_cast<char*>(s->rb_ent);
   LaunchTimer t(s, PSKV_K_RADIX, elems);
   PSKV_HIP(launch_rb_add(s->dtype, s->mode, ga, nsc, s->dview(), s->ovf, bshift, nbd, apply_log2,
-                         s->rb_cnt,
-                         s->rb_cnt + nb2, s->rb_cnt + 2 * nb2, s->rb_total,
-                         ent + elems * eb, ent, s->stream));
+                         s->rb_loff, s->rb_ent, s->stream));
   t.done();
-  s->n_general += 4;
+  s->n_general += 2;
   return PSKV_OK;
+}
+
+int radix_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t e) {
+  const uint64_t sc = rb_superchunk(s->vb);
+  uint64_t nsc = 0;
+  for (size_t i = b; i < e; ++i) nsc += (v[i].n + sc - 1) / sc;
+  if (nsc <= kRbMaxSc) return radix_launch(s, v, b, e);
+  // pieces of whole super-chunks, each <= kRbMaxSc of them
+  std::vector<pskv_batch> piece;
+  uint64_t used = 0;  // super-chunks in `piece`
+  auto flush = [&]() -> int {
+    if (piece.empty()) return PSKV_OK;
+    const int rc = radix_launch(s, piece, 0, piece.size());
+    piece.clear();
+    used = 0;
+    return rc;
+  };
+  for (size_t i = b; i < e; ++i) {
+    uint64_t off = 0;
+    while (off < v[i].n) {
+      if (used == kRbMaxSc || piece.size() == (size_t)kMaxBatches) {
+        if (int rc = flush()) return rc;
+      }
+      const uint64_t room = (kRbMaxSc - used) * sc;
+      const uint64_t n = std::min<uint64_t>(v[i].n - off, room);
+      piece.push_back(pskv_batch{v[i].keys + off,
+                                 static_cast<char*>(v[i].vals) + off * (uint64_t)s->vb, n});
+      used += (n + sc - 1) / sc;
+      off += n;
+    }
+  }
+  return flush();
 }
 
 // The general (any order) Add over one launch group.  `cond` non-null makes
@@ -1039,8 +1065,7 @@ int pskv_shard_destroy(pskv_shard* s) {
   if (s->flag) (void)hipFree(s->flag);
   free_overflow(&s->ovf);
   if (s->dstage) (void)hipFree(s->dstage);
-  if (s->rb_cnt) (void)hipFree(s->rb_cnt);
-  if (s->rb_total) (void)hipFree(s->rb_total);
+  if (s->rb_loff) (void)hipFree(s->rb_loff);
   if (s->rb_ent) (void)hipFree(s->rb_ent);
   if (s->hstage) (void)hipHostFree(s->hstage);
   if (s->hstage_free) (void)hipEventDestroy(s->hstage_free);

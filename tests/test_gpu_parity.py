@@ -569,6 +569,53 @@ def test_radix_path_hot_bucket_many_rounds(cuda, oracle_mod, mode, dtype, monkey
             assert np.allclose(got, want, rtol=1e-12, atol=1e-9)
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_radix_path_long_runs(cuda, oracle_mod, dtype):
+    """K5 resolve with runs longer than its registers hold (few, narrow key
+    buckets; every super-chunk puts ~45 entries into each) but few enough
+    entries for one table: the strided single-round path."""
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(77)
+    kb, size = 5000, 4096
+    dense = np.zeros(size, dtype)
+    batches = []
+    for j in range(3):
+        k = rng.integers(kb, kb + size, size=5000 + j).astype(np.uint32)
+        v = rng.standard_normal(k.size).astype(dtype)
+        batches.append((k, v))
+        oracle_mod.dense_last_wins(dense, kb, k, v)
+    with ps.Shard(kb, kb + size, dtype) as sh:
+        sh.add_grouped([(tdev(k, cuda), tdev(v, cuda)) for k, v in batches])
+        got = sh.get(np.arange(kb, kb + size, dtype=np.uint32))
+    assert_bits_equal(got, dense, "long runs")
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_radix_path_split_launches(cuda, oracle_mod, dtype):
+    """An unsorted group larger than one K5 launch (1024 super-chunks: 8 M keys
+    for 4-byte values, 4 M for 8-byte) is cut into consecutive pieces, a batch
+    split across two of them; duplicates across the cut keep call order."""
+    import torch
+
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(99)
+    size = 3_000_000
+    n_big = 9_000_000 if dtype is np.float32 else 4_500_000
+    big = rng.integers(0, size, size=n_big).astype(np.uint32)
+    vb = rng.standard_normal(n_big).astype(dtype)
+    small = rng.integers(0, size, size=700_000).astype(np.uint32)
+    vs = rng.standard_normal(small.size).astype(dtype)
+    dense = np.zeros(size, dtype)
+    oracle_mod.dense_last_wins(dense, 0, small, vs)
+    oracle_mod.dense_last_wins(dense, 0, big, vb)
+    with ps.Shard(0, size, dtype) as sh:
+        sh.add_grouped([(tdev(small, cuda), tdev(vs, cuda)), (tdev(big, cuda), tdev(vb, cuda))])
+        got = sh.get(torch.arange(size, dtype=torch.int32, device=cuda)).cpu().numpy()
+    assert_bits_equal(got, dense, "split")
+
+
 def test_general_path_stamps_variant_matches(cuda, oracle_mod, monkeypatch):
     """The K4 stamp path (kept for repairs) as the unhinted general path."""
     import parameter_server_amd as ps
