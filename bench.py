@@ -383,6 +383,47 @@ def side_measurements(dev, B):
     return out
 
 
+def cold_get_step(shard, adds, bases, J, B, dev, steps):
+    """The headline step pulls the windows it just pushed: 48 distinct 4 MB
+    windows = 192 MB of parameters, which the Infinity Cache (256 MB) can still
+    hold when the Get reads them.  This variant pulls J windows that the step
+    did NOT push (seed 4242, pushed bases excluded), so K1's parameter reads
+    come from HBM: the cache-cold figure SURVEY §8d asks to keep apart."""
+    import torch
+
+    from parameter_server_amd import _lib, workload
+
+    pushed = set(int(b) for b in bases)
+    cand = [int(b) for b in workload.dense_bases(4 * J, 100_000_000, B, seed=4242) if int(b) not in pushed]
+    other = sorted(set(cand))[:J] if len(set(cand)) >= J else cand[:J]
+    pulls = [torch.arange(b, b + B, dtype=torch.int64, device=dev).to(torch.int32) for b in other]
+    outs = [torch.empty(B, dtype=torch.float32, device=dev) for _ in pulls]
+    gets = shard.prepare(list(zip(pulls, outs)), is_get=True)
+    for _ in range(2):
+        shard.add_grouped(adds, sorted_hint=True)
+        shard.get_grouped(gets)
+    torch.cuda.synchronize()
+    shard.reset_timing()
+    shard.set_timing(True, kernels=[_lib.PSKV_K_GATHER, _lib.PSKV_K_ASSIGN_TILES])
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        shard.add_grouped(adds, sorted_hint=True)
+        shard.get_grouped(gets)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    shard.set_timing(False)
+    g = shard.kernel_time(_lib.PSKV_K_GATHER)
+    a = shard.kernel_time(_lib.PSKV_K_ASSIGN_TILES)
+    u_push = len(pushed) * B
+    add_b, get_b = step_bytes(J * B, u_push, len(pulls) * B)
+    k1_ms = g["total_ms"] / max(1, g["launches"])
+    return {"workload": f"cfg 2 step with the Get pulling {len(pulls)} windows not pushed in the step "
+                        "(parameters read from HBM, not from the Infinity Cache)",
+            "GB/s": (add_b + get_b) * steps / dt / 1e9, "ms_per_step": dt / steps * 1e3,
+            "k_gather_ms": k1_ms, "k_gather_GB/s": get_b / (k1_ms * 1e-3) / 1e9,
+            "k_assign_tiles_ms": a["total_ms"] / max(1, a["launches"])}
+
+
 def main():
     args = parse()
     import torch
@@ -485,8 +526,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(bases, B, args.cpu_batches)
     if rank == 0 and world == 1 and not args.no_extra:
+        cold = cold_get_step(shard, adds, bases, J, B, dev, args.steps)
         shard.set_stream(None)
         result["extra"] = side_measurements(dev, B)
+        result["extra"]["cold_get_step"] = cold
     shard.close()
     if rank == 0:
         print(json.dumps(result), flush=True)
