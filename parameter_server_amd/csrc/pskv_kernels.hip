@@ -988,8 +988,8 @@ __global__ __launch_bounds__(kBinBlock) void k_rb_bin(GroupArgs ga, DenseView d,
 constexpr int kApplyBlock = 1024;
 static_assert(kRbMaxSc <= (uint32_t)kApplyBlock, "one run per resolve thread");
 template <typename AT, typename BT, int MODE, int LOGS>
-__global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, uint32_t nbd,
-                                                            uint32_t nbk,
+__global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, uint32_t bshift,
+                                                            uint32_t nbd, uint32_t nbk,
                                                             const uint16_t* __restrict__ loff,
                                                             uint32_t nsc,
                                                             const RbEnt<sizeof(BT)>* __restrict__ tmp) {
@@ -998,11 +998,21 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
   constexpr uint32_t CAP = (uint32_t)SLOTS / 8 * 7;  // entries per round (load <= 7/8)
   constexpr int RPT = 12;                             // run entries held in registers
   constexpr uint32_t LONG = 4 * RPT;                  // longer runs: the strided path
+  static_assert(LONG <= 64, "a run's winners fit one 64-bit mask");
   constexpr uint32_t SC = rb_sc<BT>();
   using Ent = RbEnt<sizeof(BT)>;
-  __shared__ __attribute__((aligned(16))) uint32_t ak[SLOTS + 1];
-  __shared__ __attribute__((aligned(16))) uint32_t abest[MODE == 0 ? SLOTS + 1 : 1];  // assign: 1 + max position
+  // assign: keys ak[0..SLOTS] and 1 + max position abest[0..SLOTS] in one
+  // array, which the direct path reuses whole as best[0..DSPAN)
+  __shared__ __attribute__((aligned(16))) uint32_t ak[MODE == 0 ? 2 * SLOTS + 8 : SLOTS + 1];
+  uint32_t* abest = ak + SLOTS + 4;  // 16-byte aligned
   __shared__ __attribute__((aligned(16))) AT asum[MODE == 1 ? SLOTS + 1 : 1];
+  // assign, dense buckets: a direct-indexed table best[key offset in the
+  // bucket's DSPAN-key window] = tag << kPosBits | (1 + position); the tag
+  // grows every pass, so stale values always lose and the table is never
+  // cleared between buckets (only after a hash-path bucket used the memory)
+  constexpr uint32_t DSPAN = MODE == 0 ? 2u * SLOTS : 1u;
+  constexpr uint32_t kPosBits = 18;
+  uint32_t* best = ak;
   __shared__ uint32_t pre[kRbMaxSc + 1];  // run starts (positions); pre[nsc] = entries
   __shared__ uint32_t rst[kRbMaxSc];      // run starts (entry index in tmp)
   __shared__ uint32_t wtmp[kApplyBlock / 64];
@@ -1118,6 +1128,15 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
     for (int q = 0; q < RPT; ++q)
       if ((uint32_t)q < e - a) x[q] = tmp[(uint32_t)tid * SC + a + q];
   };
+  uint32_t dlog = 0;
+  while ((1u << dlog) < DSPAN) ++dlog;
+  const uint32_t halves = bshift > dlog ? 1u << (bshift - dlog) : 1u;  // direct passes per bucket
+  bool clean = false;  // best[] holds only values below tag << kPosBits
+  uint32_t tag = 0;
+  auto zero_best = [&]() {
+    for (uint32_t i = (uint32_t)tid * 4; i < DSPAN; i += kApplyBlock * 4)
+      *reinterpret_cast<u32x4*>(&best[i]) = u32x4{0u, 0u, 0u, 0u};
+  };
   uint32_t ra, re, na, ne_;
   bounds(b, ra, re);
   bounds(b + per_xcd, na, ne_);
@@ -1139,6 +1158,58 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
     const uint32_t ne = block_exscan<kApplyBlock>(pre, kRbMaxSc, wtmp);
     const uint32_t p0 = pre[tid];
     if (ne == 0) continue;  // uniform
+    const bool direct = MODE == 0 && b != nbd && !long_run && halves <= 4 &&
+                        ne < (1u << kPosBits) - 1u;
+    if (direct) {
+      const uint32_t bbase = b << bshift;
+      uint32_t rel[RPT];
+#pragma unroll
+      for (int q = 0; q < RPT; ++q) rel[q] = (uint32_t)q < len ? x[q].key - d.key_begin - bbase : 0u;
+      // every pass only marks this lane's winners (bit q of win); the stores
+      // of all passes go out together afterwards, so the random parameter
+      // stores of the whole bucket are in flight at once
+      uint64_t win = 0;
+      for (uint32_t h = 0; h < halves; ++h) {
+        if (!clean || tag + 1 >= (1u << (32 - kPosBits))) {  // uniform
+          zero_best();
+          __syncthreads();
+          clean = true;
+          tag = 0;
+        }
+        const uint32_t tg = ++tag << kPosBits;
+#pragma unroll
+        for (int q = 0; q < RPT; ++q)
+          if ((uint32_t)q < len && (rel[q] >> dlog) == h)
+            atomicMax(&best[rel[q] & (DSPAN - 1)], tg | (p0 + (uint32_t)q + 1u));
+        for (uint32_t q = RPT; q < len; ++q) {  // a run's short tail, from memory
+          const uint32_t r = tmp[st + q].key - d.key_begin - bbase;
+          if ((r >> dlog) == h) atomicMax(&best[r & (DSPAN - 1)], tg | (p0 + q + 1u));
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < RPT; ++q)
+          if ((uint32_t)q < len && (rel[q] >> dlog) == h &&
+              best[rel[q] & (DSPAN - 1)] == (tg | (p0 + (uint32_t)q + 1u)))
+            win |= 1ull << q;
+        for (uint32_t q = RPT; q < len; ++q) {
+          const uint32_t r = tmp[st + q].key - d.key_begin - bbase;
+          if ((r >> dlog) == h && best[r & (DSPAN - 1)] == (tg | (p0 + q + 1u))) win |= 1ull << q;
+        }
+        if (h + 1 < halves) __syncthreads();  // the table is read before the next pass
+      }
+#pragma unroll
+      for (int q = 0; q < RPT; ++q)
+        if (win >> q & 1u) store_winner(b, x[q].key, (BT)x[q].val);
+      for (uint32_t q = RPT; q < len; ++q)
+        if (win >> q & 1u) {
+          const Ent y = tmp[st + q];
+          store_winner(b, y.key, (BT)y.val);
+        }
+      // the next bucket's first atomics come after its scan's barriers, so
+      // the reads above are done before best[] changes again
+      continue;
+    }
+    clean = false;  // the hash paths below overwrite best[]
     if (ne <= CAP && !long_run) {
       clear_table();
       __syncthreads();
@@ -1551,9 +1622,9 @@ static hipError_t rb_launch(const GroupArgs& ga, uint32_t nsc, const DenseView& 
   const uint32_t gb = nsc < 256u ? nsc : 256u;
   k_rb_bin<AT, BT, MODE><<<gb, kBinBlock, 0, st>>>(ga, d, bshift, nbd, nbk, loff, nsc, t);
   if (apply_log2 == 13)  // 2^13 slots: two workgroups per CU
-    k_rb_resolve<AT, BT, MODE, 13><<<512, kApplyBlock, 0, st>>>(d, o, nbd, nbk, loff, nsc, t);
+    k_rb_resolve<AT, BT, MODE, 13><<<512, kApplyBlock, 0, st>>>(d, o, bshift, nbd, nbk, loff, nsc, t);
   else
-    k_rb_resolve<AT, BT, MODE, 14><<<256, kApplyBlock, 0, st>>>(d, o, nbd, nbk, loff, nsc, t);
+    k_rb_resolve<AT, BT, MODE, 14><<<256, kApplyBlock, 0, st>>>(d, o, bshift, nbd, nbk, loff, nsc, t);
   return hipGetLastError();
 }
 
