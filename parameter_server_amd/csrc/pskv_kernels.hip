@@ -373,6 +373,9 @@ __device__ __forceinline__ bool dense_chunk(const GroupArgs& ga, const DenseView
   // later batches whose interval meets this chunk's interval (every wave computes it)
   const bool ov = lane > j && lane < ga.nb && s_first[lane] <= c_hi && s_last[lane] >= c_lo;
   const unsigned long long later = __ballot(ov);
+  // one later batch covers the whole chunk: none of its values can survive, so
+  // they are not even read (the keys still are: they prove batch j dense)
+  const bool covered = __ballot(ov && s_first[lane] <= c_lo && s_last[lane] >= c_hi) != 0;
   VT* __restrict__ param = reinterpret_cast<VT*>(d.param);
   bool bad = false;
   auto shadowed = [&](uint32_t k) {
@@ -385,7 +388,16 @@ __device__ __forceinline__ bool dense_chunk(const GroupArgs& ga, const DenseView
     }
     return sh;
   };
-  if (VEC && end - base == CH) {
+  if (VEC && end - base == CH && covered) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = base + (uint64_t)(u * kBlock + tid) * 4;
+      uint32_t k[4];
+      Vec4<uint32_t>::load<NT>(keys + i, k);
+      const uint32_t k0 = first + (uint32_t)i;
+      bad |= (k[0] != k0) | (k[1] != k0 + 1u) | (k[2] != k0 + 2u) | (k[3] != k0 + 3u);
+    }
+  } else if (VEC && end - base == CH) {
     uint32_t k[U][4];
     VT v[U][4];
 #pragma unroll
