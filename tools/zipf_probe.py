@@ -43,10 +43,12 @@ def main():
                 os.environ.pop(k) if o is None else os.environ.__setitem__(k, o)
             adds = sh.prepare(zb)
             gets = sh.prepare([(k, o) for (k, _), o in zip(zb, zo)], is_get=True)
-            shards.append((f"{v or 'default'}/{mode}", sh, adds, gets))
+            shards.append((f"{v or 'default'}/{mode}", sh, adds, gets, env))
     res = {n: {} for n, *_ in shards}
     for r in range(rounds + 1):
-        for name, sh, adds, gets in shards:
+        for name, sh, adds, gets, env in shards:
+            old = {k: os.environ.get(k) for k in env}
+            os.environ.update(env)  # launch-time knobs (read per launch) see the variant too
             sh.reset_timing()
             sh.set_timing(r > 0)
             torch.cuda.synchronize()
@@ -58,6 +60,8 @@ def main():
             torch.cuda.synchronize()
             t2 = time.perf_counter()
             sh.set_timing(False)
+            for k, o in old.items():
+                os.environ.pop(k) if o is None else os.environ.__setitem__(k, o)
             if r == 0:
                 continue
             res[name].setdefault("add_wall", []).append((t1 - t0) * 1e3)
