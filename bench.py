@@ -421,7 +421,7 @@ def cold_get_step(shard, adds, bases, J, B, dev, steps):
                         "(parameters read from HBM, not from the Infinity Cache)",
             "GB/s": (add_b + get_b) * steps / dt / 1e9, "ms_per_step": dt / steps * 1e3,
             "k_gather_ms": k1_ms, "k_gather_GB/s": get_b / (k1_ms * 1e-3) / 1e9,
-            "k_assign_tiles_ms": a["total_ms"] / max(1, a["launches"])}
+            "k_assign_group_ms": a["total_ms"] / max(1, a["launches"])}
 
 
 def main():

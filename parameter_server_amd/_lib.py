@@ -36,7 +36,7 @@ PSKV_K_COUNT = 8
 KERNEL_NAMES = {
     PSKV_K_GATHER: "k_gather",
     PSKV_K_ASSIGN_SORTED: "k_assign_sorted",
-    PSKV_K_ASSIGN_TILES: "k_assign_tiles",
+    PSKV_K_ASSIGN_TILES: "k_assign_group",
     PSKV_K_GENERAL_MARK: "k_general_mark",
     PSKV_K_GENERAL_COMMIT: "k_general_commit",
     PSKV_K_RADIX: "k_radix_bucket",

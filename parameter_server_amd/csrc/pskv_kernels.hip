@@ -11,7 +11,7 @@
 //   K1  k_gather          Get: out[i] = value(keys[i])                 (map_storage.hpp:29-45)
 //   K2  k_assign_sorted   Add, one batch, sorted keys: the last element of
 //                         each equal-key run stores, nothing else does
-//   K2g k_assign_tiles    Add, grouped sorted batches: one workgroup owns a
+//   K2g k_assign_group    Add, grouped sorted batches: one workgroup owns a
 //                         key tile and applies the batches in call order
 //   K4a k_general_mark    Add, any order: per-workgroup LDS hash dedup, then
 //                         (assign) u64 last-writer stamps / (accumulate) one

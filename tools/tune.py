@@ -88,7 +88,7 @@ def main():
         for k, v in d.items():
             med = statistics.median(v)
             extra = ""
-            if k in ("k_gather", "k_assign_tiles"):
+            if k in ("k_gather", "k_assign_group"):
                 extra = f" ({J * 1e6 * 12 / (med / 1e3) / 1e9:.0f} GB/s)"
             if k in ("step", "step_untimed"):
                 extra = f" ({J * 1e6 * 24 / (med / 1e3) / 1e9:.0f} GB/s)"
