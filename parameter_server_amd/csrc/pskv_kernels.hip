@@ -511,6 +511,54 @@ __global__ __launch_bounds__(kBlock) void k_assign_group(GroupArgs ga, DenseView
   if (bad) *flag = epoch;
 }
 
+// a + b with two's-complement wrap for int32 (the reference's int values),
+// plain IEEE addition for float/double
+template <typename T>
+__device__ __forceinline__ T add_wrap(T a, T b) {
+  return a + b;
+}
+template <>
+__device__ __forceinline__ int add_wrap<int>(int a, int b) {
+  return (int)((uint32_t)a + (uint32_t)b);
+}
+
+template <typename T>
+__device__ __forceinline__ unsigned long long to_bits(T v) {
+  if (sizeof(T) == 8) return *reinterpret_cast<const unsigned long long*>(&v);
+  return (unsigned long long)*reinterpret_cast<const uint32_t*>(&v);
+}
+template <typename T>
+__device__ __forceinline__ T from_bits(unsigned long long b) {
+  if (sizeof(T) == 8) return *reinterpret_cast<const T*>(&b);
+  const uint32_t lo = (uint32_t)b;
+  return *reinterpret_cast<const T*>(&lo);
+}
+
+// *p += v on an LDS word.  Integer adds are ds_add (full rate).  The LDS unit
+// runs ds_add_f32 at ~1/40 of the integer atomics' rate on gfx950 (measured:
+// 0.2 vs 8 T atomics/s chip-wide, tools/micro/lds_atomic.hip), so float and
+// double sums first try an integer compare-and-swap (2.6 T/s uncontended);
+// a lane that loses twice (a hot key shared within the wave) falls back to the
+// hardware float atomic, whose cost does not grow with contention.  Both are
+// atomic read-modify-writes of the LDS unit, so they mix safely.
+template <typename T>
+__device__ __forceinline__ void lds_add(T* p, T v) {
+  if constexpr (std::is_integral<T>::value) {
+    atomicAdd(p, v);
+  } else {
+    using U = typename std::conditional<sizeof(T) == 8, unsigned long long, uint32_t>::type;
+    U* w = reinterpret_cast<U*>(p);
+    U old = *w;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const U assumed = old;
+      old = atomicCAS(w, assumed, (U)to_bits<T>(from_bits<T>(assumed) + v));
+      if (old == assumed) return;
+    }
+    atomicAdd(p, v);
+  }
+}
+
 // ------------------------------------------------ K4 general (any order)
 // K4a: a workgroup takes 2048 consecutive elements of one batch and folds them
 // into a 4096-slot LDS hash (key -> max element index, or key -> sum).  Then
@@ -603,7 +651,7 @@ __global__ __launch_bounds__(kBlock) void k_general_mark(GroupArgs ga, DenseView
           if (MODE == 0)
             atomicMax(&hidx[h], (uint32_t)li);
           else
-            atomicAdd(&hsum[h], vals[i]);
+            lds_add(&hsum[h], vals[i]);
         }
       }
     }
@@ -710,29 +758,6 @@ __device__ __forceinline__ uint32_t rb_bucket(const DenseView& d, uint32_t k, ui
                                               uint32_t nbd) {
   const uint32_t off = k - d.key_begin;
   return (uint64_t)off < d.range ? (off >> bshift) : nbd;  // nbd = the out-of-range bucket
-}
-
-// a + b with two's-complement wrap for int32 (the reference's int values),
-// plain IEEE addition for float/double
-template <typename T>
-__device__ __forceinline__ T add_wrap(T a, T b) {
-  return a + b;
-}
-template <>
-__device__ __forceinline__ int add_wrap<int>(int a, int b) {
-  return (int)((uint32_t)a + (uint32_t)b);
-}
-
-template <typename T>
-__device__ __forceinline__ unsigned long long to_bits(T v) {
-  if (sizeof(T) == 8) return *reinterpret_cast<const unsigned long long*>(&v);
-  return (unsigned long long)*reinterpret_cast<const uint32_t*>(&v);
-}
-template <typename T>
-__device__ __forceinline__ T from_bits(unsigned long long b) {
-  if (sizeof(T) == 8) return *reinterpret_cast<const T*>(&b);
-  const uint32_t lo = (uint32_t)b;
-  return *reinterpret_cast<const T*>(&lo);
 }
 
 // Block-wide exclusive scan of a[0..n) in LDS, in place (n <= kRbMaxBuckets + 1).
@@ -931,7 +956,7 @@ __global__ __launch_bounds__(kBinBlock) void k_rb_bin(GroupArgs ga, DenseView d,
       if (MODE == 0)
         atomicMax(reinterpret_cast<uint32_t*>(&hv[slot[q]]), li_of(q));
       else
-        atomicAdd(reinterpret_cast<AT*>(&hv[slot[q]]), from_bits<AT>(to_bits<BT>(vc[q])));
+        lds_add(reinterpret_cast<AT*>(&hv[slot[q]]), from_bits<AT>(to_bits<BT>(vc[q])));
     }
     __syncthreads();
     uint32_t emask = 0, rk[KPT];
@@ -1117,7 +1142,7 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
     if (MODE == 0)
       atomicMax(&abest[s1[0]], pos + 1u);
     else
-      atomicAdd(&asum[s1[0]], from_bits<AT>(to_bits<BT>(vbits)));
+      lds_add(&asum[s1[0]], from_bits<AT>(to_bits<BT>(vbits)));
   };
   // XCD-aware bucket schedule
   const uint32_t xcd = blockIdx.x & 7u;
@@ -1238,7 +1263,7 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
         if (MODE == 0)
           atomicMax(&abest[slot[q]], p0 + (uint32_t)q + 1u);
         else
-          atomicAdd(&asum[slot[q]], from_bits<AT>(to_bits<BT>((BT)x[q].val)));
+          lds_add(&asum[slot[q]], from_bits<AT>(to_bits<BT>((BT)x[q].val)));
       }
       for (uint32_t q = RPT; q < len; ++q) {  // a run's short tail (<= LONG - RPT), from memory
         const Ent y = tmp[st + q];
