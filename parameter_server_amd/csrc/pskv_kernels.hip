@@ -809,23 +809,26 @@ __device__ __forceinline__ uint32_t lds_insert(uint32_t* hk, uint32_t* sent,
                                                const uint32_t (&key)[PER], uint32_t valid_mask,
                                                uint32_t (&slot)[PER]) {
   uint32_t old[PER];
+  uint32_t own = 0;
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
     slot[q] = kEmpty32;
     old[q] = 0;
     if (!(valid_mask >> q & 1u)) continue;
     if (key[q] == kEmpty32) {
+      // the sentinel key owns the side word: the lane that sets it inserted
+      // the key (its own value equals EMPTY, so it cannot mark a lost race)
       slot[q] = SLOTS;
-      old[q] = atomicCAS(sent, 0u, 1u) == 0u ? kEmpty32 : key[q];
+      own |= atomicCAS(sent, 0u, 1u) == 0u ? (1u << q) : 0u;
+      old[q] = key[q];
     } else {
       slot[q] = fmix32(key[q]) & (SLOTS - 1);
       old[q] = atomicCAS(&hk[slot[q]], kEmpty32, key[q]);
     }
   }
-  uint32_t own = 0;
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
-    if (!(valid_mask >> q & 1u)) continue;
+    if (!(valid_mask >> q & 1u) || key[q] == kEmpty32) continue;
     uint32_t o = old[q], h = slot[q];
     while (o != kEmpty32 && o != key[q]) {  // collision: probe on
       h = (h + 1) & (SLOTS - 1);

@@ -569,6 +569,88 @@ def test_radix_path_hot_bucket_many_rounds(cuda, oracle_mod, mode, dtype, monkey
             assert np.allclose(got, want, rtol=1e-12, atol=1e-9)
 
 
+@pytest.mark.parametrize("layout", ["sentinel_dense", "sentinel_overflow"])
+@pytest.mark.parametrize("path", ["device", "host"])
+def test_accumulate_sentinel_key_duplicates(cuda, layout, path):
+    """Key 0xFFFFFFFF (the LDS tables' EMPTY, kept in a side word) pushed many
+    times in one batch: its duplicates fold into ONE entry per super-chunk
+    (regression: every duplicate used to claim ownership of the side word)."""
+    import parameter_server_amd as ps
+
+    kb, ke = (2**32 - 1000, 2**32) if layout == "sentinel_dense" else (0, 1000)
+    for n_ff in (1, 2, 5, 3000):
+        k = np.array([kb + 5] * 3 + [2**32 - 1] * n_ff + [2**32 - 2] * 2, np.uint32)
+        v = np.arange(1, k.size + 1, dtype=np.int32)
+        with ps.Shard(kb, ke, np.int32, mode="accumulate", overflow_slots=1 << 10) as sh:
+            if path == "device":
+                sh.add_grouped([(tdev(k, cuda), tdev(v, cuda))])
+            else:
+                sh.add(k, v)
+            got = sh.get(np.array([kb + 5, 2**32 - 1, 2**32 - 2], np.uint32))
+        want = np.array([v[:3].sum(), v[3:3 + n_ff].sum(), v[-2:].sum()], np.int64).astype(np.int32)
+        assert_bits_equal(got, want, f"sentinel x{n_ff}")
+
+
+def test_radix_accumulate_full_key_space_edges(cuda):
+    """K5 accumulate on the reference's argument-less storage (the whole uint32
+    key space in one shard, 16 GiB of int32 in HBM): the K5b -> K5c pair
+    hand-off carries key offset 0xFFFFFFFF and 0 like any other; int32 sums
+    wrap and are exact."""
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(91)
+    batches = []
+    for j in range(5):
+        n = 200_000 + 17 * j
+        k = rng.integers(0, 2**32, size=n, dtype=np.uint64)
+        k[:3000] = rng.choice(np.array([0, 1, 2**32 - 1, 2**32 - 2, 2**31], np.uint64), size=3000)
+        k = k.astype(np.uint32)
+        v = rng.integers(-2**31, 2**31 - 1, size=n, dtype=np.int64).astype(np.int32)
+        batches.append((k, v))
+    acc = {}
+    for k, v in batches:
+        for kk, vv in zip(k.tolist(), v.tolist()):
+            acc[kk] = acc.get(kk, 0) + vv
+    q = np.array(sorted(acc) + [12345, 2**32 - 3], dtype=np.uint32)
+    want = np.array([acc.get(int(x), 0) for x in q], np.int64)
+    want = ((want + 2**31) % 2**32 - 2**31).astype(np.int32)
+    with ps.Shard(0, 2**32, np.int32, mode="accumulate") as sh:
+        sh.add_grouped([(tdev(k, cuda), tdev(v, cuda)) for k, v in batches])
+        got = sh.get(q)
+    assert_bits_equal(got, want, "full key space accumulate")
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_radix_accumulate_zipf_split_launches(cuda, dtype):
+    """cfg-3-shaped accumulate through K5 (bin, resolve, pair apply): Zipf
+    pushes over several launch pieces (> 8 M keys for 4-byte values), checked
+    against float64 sums with the recursive-summation bound."""
+    import torch
+
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(123)
+    size = 20_000_000
+    n_total = 9_000_000 if dtype is np.float32 else 4_600_000
+    perm_seed = 5
+    ranks = rng.zipf(1.1, size=n_total) % size
+    keys = ((ranks * 2654435761 + perm_seed) % size).astype(np.uint32)
+    vals = rng.standard_normal(n_total).astype(dtype)
+    cut = n_total // 3
+    idx = keys.astype(np.int64)
+    p64 = np.bincount(idx, weights=vals.astype(np.float64), minlength=size)
+    a64 = np.bincount(idx, weights=np.abs(vals.astype(np.float64)), minlength=size)
+    cnt = np.bincount(idx, minlength=size)
+    with ps.Shard(0, size, dtype, mode="accumulate") as sh:
+        sh.add_grouped([(tdev(keys[:cut], cuda), tdev(vals[:cut], cuda)),
+                        (tdev(keys[cut:], cuda), tdev(vals[cut:], cuda))])
+        got = sh.get(torch.arange(size, dtype=torch.int32, device=cuda)).cpu().numpy()
+    u = 2.0**-24 if dtype is np.float32 else 2.0**-53
+    tol = 1.01 * (cnt + 1) * u * a64
+    err = np.abs(got.astype(np.float64) - p64)
+    assert np.all(err <= tol), f"max err/tol {np.max(err / np.maximum(tol, 1e-300))}"
+
+
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 def test_radix_path_long_runs(cuda, oracle_mod, dtype):
     """K5 resolve with runs longer than its registers hold (few, narrow key
