@@ -569,6 +569,52 @@ def test_radix_path_hot_bucket_many_rounds(cuda, oracle_mod, mode, dtype, monkey
             assert np.allclose(got, want, rtol=1e-12, atol=1e-9)
 
 
+@pytest.mark.parametrize("mode", ["assign", "accumulate"])
+@pytest.mark.parametrize("path", ["host", "device_hint", "device_hint_single", "device_unhinted"])
+def test_windows_ending_at_top_of_key_space(cuda, oracle_mod, mode, path):
+    """Dense windows and sorted batches that end at key 0xFFFFFFFF in a shard
+    whose key_end is 2^32: no uint32 wrap in the window / density / tile
+    arithmetic of K2, K2g, K6/K7 or the host checks.  int32 values: assign and
+    accumulate are both bit-exact."""
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(2024)
+    kb = 2**32 - (1 << 20)
+    ref = np.zeros(1 << 20, np.int64)
+    batches = []
+    for j in range(9):
+        if j % 3 == 0:
+            n = int(rng.choice([1, 7, 4096, 70_001]))
+            k = np.arange(2**32 - n, 2**32, dtype=np.uint64).astype(np.uint32)      # window to the top
+        elif j % 3 == 1:
+            f = int(rng.integers(kb, 2**32 - 50_000))
+            k = np.arange(f, f + 50_000, dtype=np.uint64).astype(np.uint32)         # window below
+        else:
+            k = np.sort(rng.integers(2**32 - 300_000, 2**32, size=40_000)).astype(np.uint32)  # sorted, dups
+            k[-3:] = 0xFFFFFFFF
+        v = rng.integers(-2**31, 2**31 - 1, size=k.size, dtype=np.int64).astype(np.int32)
+        batches.append((k, v))
+    for k, v in batches:
+        idx = k.astype(np.int64) - kb
+        if mode == "assign":
+            oracle_mod.dense_last_wins(ref, kb, k, v.astype(np.int64))
+        else:
+            np.add.at(ref, idx, v.astype(np.int64))
+    want = ((ref + 2**31) % 2**32 - 2**31).astype(np.int32)
+    with ps.Shard(kb, 2**32, np.int32, mode=mode) as sh:
+        if path == "host":
+            sh.add_grouped(batches)
+        elif path == "device_hint":
+            sh.add_grouped([(tdev(k, cuda), tdev(v, cuda)) for k, v in batches], sorted_hint=True)
+        elif path == "device_hint_single":
+            for k, v in batches:
+                sh.add(tdev(k, cuda), tdev(v, cuda), sorted_hint=True)
+        else:
+            sh.add_grouped([(tdev(k, cuda), tdev(v, cuda)) for k, v in batches])
+        got = sh.get(np.arange(kb, 2**32, dtype=np.uint64).astype(np.uint32))
+    assert_bits_equal(got, want, f"{mode} {path} top of key space")
+
+
 @pytest.mark.parametrize("layout", ["sentinel_dense", "sentinel_overflow"])
 @pytest.mark.parametrize("path", ["device", "host"])
 def test_accumulate_sentinel_key_duplicates(cuda, layout, path):
