@@ -783,11 +783,18 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t* a, uint32_t n, uint32
   }
   if (lane == 63) wtmp[w] = v;
   __syncthreads();
+  // the wave totals as 16-byte broadcast reads (NW / 4 LDS reads, not NW)
+  static_assert(NW % 4 == 0, "whole 16-byte groups of wave totals");
   uint32_t before = 0, tot = 0;
 #pragma unroll
-  for (int q = 0; q < NW; ++q) {
-    if (q < w) before += wtmp[q];
-    tot += wtmp[q];
+  for (int g = 0; g < NW / 4; ++g) {
+    const u32x4 t4 = reinterpret_cast<const u32x4*>(wtmp)[g];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int q = g * 4 + e;
+      if (q < w) before += t4[e];
+      tot += t4[e];
+    }
   }
   uint32_t run = before + v - sum;
 #pragma unroll
@@ -878,7 +885,7 @@ __global__ __launch_bounds__(kBinBlock) void k_rb_bin(GroupArgs ga, DenseView d,
   uint32_t* hk = reinterpret_cast<uint32_t*>(tbl + VPAD);
   Ent* stg = reinterpret_cast<Ent*>(tbl);
   __shared__ uint32_t cnt[kRbMaxBuckets + 1];  // bucket counters, then bucket starts
-  __shared__ uint32_t wtmp[kBinBlock / 64];
+  __shared__ __attribute__((aligned(16))) uint32_t wtmp[kBinBlock / 64];
   __shared__ uint32_t sent;
   const int tid = threadIdx.x;
   auto clear = [&]() {
@@ -994,13 +1001,26 @@ __global__ __launch_bounds__(kBinBlock) void k_rb_bin(GroupArgs ga, DenseView d,
       stg[cnt[rb_bucket(d, kc[q], bshift, nbd)] + rk[q]] = e;
     }
     __syncthreads();
-    // the staged, bucket-sorted entries out as one coalesced stream
+    // the staged, bucket-sorted entries out as one coalesced stream.  The
+    // thread that copies a 16-byte piece also returns it to its cleared state
+    // (hv zero, hk EMPTY; nobody else reads it), the pieces past the staged
+    // ones are cleared in the same pass, and so are the bucket counters (last
+    // read by the staging above): one barrier where copy and clear took two
     const uint32_t n16 = (uint32_t)((total * sizeof(Ent) + 15) / 16);
     u32x4* dst = reinterpret_cast<u32x4*>(tmp + (size_t)sc * SC);
-    const u32x4* src = reinterpret_cast<const u32x4*>(stg);
-    for (uint32_t i = tid; i < n16; i += kBinBlock) dst[i] = src[i];
-    __syncthreads();
-    clear();
+    u32x4* src = reinterpret_cast<u32x4*>(stg);
+    constexpr uint32_t T16 = (uint32_t)((VPAD + (size_t)SLOTS * 4) / 16);
+    static_assert((VPAD + (size_t)SLOTS * 4) % 16 == 0, "whole 16-byte pieces");
+    for (uint32_t i = tid; i < T16; i += kBinBlock) {
+      if (i < n16) dst[i] = src[i];
+      const uint32_t z = (size_t)i * 16 < VPAD ? 0u : kEmpty32;
+      src[i] = u32x4{z, z, z, z};
+    }
+    if (tid == 0) {
+      hk[SLOTS] = kEmpty32;
+      sent = 0;
+    }
+    for (uint32_t b = tid; b <= nbk; b += kBinBlock) cnt[b] = 0;
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < KPT; ++q) {
@@ -1055,7 +1075,7 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
   uint32_t* best = ak;
   __shared__ uint32_t pre[kRbMaxSc + 1];  // run starts (positions); pre[nsc] = entries
   __shared__ uint32_t rst[kRbMaxSc];      // run starts (entry index in tmp)
-  __shared__ uint32_t wtmp[kApplyBlock / 64];
+  __shared__ __attribute__((aligned(16))) uint32_t wtmp[kApplyBlock / 64];
   __shared__ uint32_t sent;
   const int tid = threadIdx.x;
   auto find = [&](uint32_t key) -> uint32_t {
