@@ -426,6 +426,11 @@ def cold_get_step(shard, adds, bases, J, B, dev, steps):
 
 def main():
     args = parse()
+    # the JSON line is the only thing on stdout: everything else the run prints
+    # (torch.distributed / gloo / RCCL banners, library notices) goes to stderr
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     import torch
 
     import parameter_server_amd as ps
@@ -548,7 +553,8 @@ def main():
         result["extra"]["cold_get_step"] = cold
     shard.close()
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        json_out.write(json.dumps(result) + "\n")
+        json_out.flush()
     if world > 1:
         import torch.distributed as dist
 
