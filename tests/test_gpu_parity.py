@@ -799,13 +799,16 @@ def _pinned(a):
     return out.view(np.uint32) if a.dtype == np.uint32 else out
 
 
+@pytest.mark.parametrize("pageable_path", ["dma", "staged"])
 @pytest.mark.parametrize("mode", ["assign", "accumulate"])
-def test_pinned_host_buffers_direct_dma(cuda, oracle_mod, mode):
+def test_pinned_host_buffers_direct_dma(cuda, oracle_mod, mode, pageable_path, monkeypatch):
     """Page-locked caller buffers (the zmq frames after the SURVEY §8f-3 mailbox
     change) are DMA'd directly, without the staging copy: same results as
     pageable buffers, for sorted, dense and unsorted batches, Add and Get."""
     import parameter_server_amd as ps
 
+    # pageable buffers go by direct DMA (default) or through pinned staging
+    monkeypatch.setenv("PSKV_PAGEABLE_DMA", "1" if pageable_path == "dma" else "0")
     rng = np.random.default_rng(71)
     kb, size = 10, 400_000
     batches = []
