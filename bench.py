@@ -467,6 +467,7 @@ def main():
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
+    t_own = time.perf_counter()  # this rank's own work done
     barrier(world)
     t1 = time.perf_counter()
     elapsed = max_over_ranks(t1 - t0, world, dev)
@@ -495,6 +496,9 @@ def main():
     add_b, get_b = step_bytes(J * B, u_push, J * B)
     total_bytes = sum_over_ranks(float((add_b + get_b) * args.steps), world, dev)
     value = total_bytes / elapsed / 1e9
+    own = (add_b + get_b) * args.steps / (t_own - t0) / 1e9
+    per_gpu = {"mean_GB/s": value / world, "min_GB/s": -max_over_ranks(-own, world, dev),
+               "max_GB/s": max_over_ranks(own, world, dev)}
 
     # dominant kernel: the one with the most time in the timed region
     dom = max(ktimes.items(), key=lambda kv: kv[1]["avg_ms"] * kv[1]["launches"])
@@ -543,6 +547,9 @@ def main():
             "parallelism": f"range-sharded x{world} (no collective)",
         },
         "roofline": roof,
+        # cfg 4 reports per-GPU next to aggregate: each rank's own
+        # bytes over its own time, min / max over ranks
+        "per_gpu": per_gpu,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(bases, B, args.cpu_batches)
