@@ -252,6 +252,27 @@ def load_pmc(kernel_substr, config):
     return None, None
 
 
+def _zipf_cpu_sample(zb, B):
+    """The oracle's MapStorage restatement (1 thread) on the first cfg-3 Zipf
+    batches, same byte accounting as the GPU number (the baseline for cfg 3)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test infrastructure: the CPU baseline leg
+
+    ks = [k.cpu().numpy().view(np.uint32) for k, _ in zb]
+    vs = [v.cpu().numpy() for _, v in zb]
+    m = oracle.MapStorageRef(np.float32)
+    t0 = time.perf_counter()
+    for k, v in zip(ks, vs):
+        m.add(k, v)
+    for k in ks:
+        m.get(k)
+    t = time.perf_counter() - t0
+    u = int(np.unique(np.concatenate(ks)).size)
+    add_b, get_b = step_bytes(len(ks) * B, u, len(ks) * B)
+    return {"GB/s": (add_b + get_b) / t / 1e9, "seconds": t, "cores": 1, "kind": "port",
+            "sample": f"{len(ks)} x {B} Zipf keys of the same workload, Add then Get"}
+
+
 def side_measurements(dev, B):
     """Secondary numbers (same JSON line, under "extra"): cfg 3 Zipf through the
     general path, and the end-to-end rate with host (pageable) buffers."""
@@ -286,7 +307,8 @@ def side_measurements(dev, B):
     out["zipf"] = {"workload": "cfg 3: Zipf(0.99) over 1e8 keys, 8 x 1M unsorted pushes then pulls, assign "
                                "(general path K5: LDS dedup + bucket-sorted super-chunks, no global atomics)",
                    "GB/s": (add_b + get_b) * reps / dt / 1e9, "ms_per_step": dt / reps * 1e3,
-                   "unique_keys_per_batch": uniq, "distinct_keys_per_step": u_all}
+                   "unique_keys_per_batch": uniq, "distinct_keys_per_step": u_all,
+                   "cpu_map_storage": _zipf_cpu_sample(zb[:2], B)}
     # cfg 3 in accumulate mode (the north star's LDS segmented-sum path): K5,
     # per-super-chunk LDS sums, key buckets, one owner workgroup per bucket
     with ps.Shard(0, space, np.float32, mode="accumulate") as sh:
