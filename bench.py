@@ -405,6 +405,39 @@ def side_measurements(dev, B):
     return out
 
 
+def dense_f64_step(batches, bases, J, B, dev, steps):
+    """The headline step with 8-byte values (the reference apps' Val = double,
+    app/logistic_regression.cpp): same keys and windows, f64 shard; bytes
+    counted with V = 8."""
+    import torch
+
+    import parameter_server_amd as ps
+
+    b64 = [(k, v.to(torch.float64)) for k, v in batches]
+    o64 = [torch.empty(B, dtype=torch.float64, device=dev) for _ in range(J)]
+    with ps.Shard(0, 100_000_000, np.float64) as sh:
+        sh.set_stream(torch.cuda.current_stream().cuda_stream)
+        adds = sh.prepare(b64)
+        gets = sh.prepare([(k, o) for (k, _), o in zip(b64, o64)], is_get=True)
+        for _ in range(2):
+            sh.add_grouped(adds, sorted_hint=True)
+            sh.get_grouped(gets)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            sh.add_grouped(adds, sorted_hint=True)
+            sh.get_grouped(gets)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        last = {int(b): j for j, b in enumerate(bases)}
+        assert all(torch.equal(o64[j], b64[last[int(b)]][1]) for j, b in enumerate(bases))
+        sh.set_stream(None)
+    u = len(set(int(b) for b in bases)) * B
+    step_b = J * B * (4 + 8) + u * 8 + J * B * (4 + 2 * 8)
+    return {"workload": f"cfg 2 step with float64 values ({J} x {B} windows, assign)",
+            "GB/s": step_b * steps / dt / 1e9, "ms_per_step": dt / steps * 1e3}
+
+
 def cold_get_step(shard, adds, bases, J, B, dev, steps):
     """The headline step pulls the windows it just pushed: 48 distinct 4 MB
     windows = 192 MB of parameters, which the Infinity Cache (256 MB) can still
@@ -580,6 +613,7 @@ def main():
         shard.set_stream(None)
         result["extra"] = side_measurements(dev, B)
         result["extra"]["cold_get_step"] = cold
+        result["extra"]["dense_f64_step"] = dense_f64_step(batches, bases, J, B, dev, args.steps)
     shard.close()
     if rank == 0:
         json_out.write(json.dumps(result) + "\n")
