@@ -637,6 +637,47 @@ def test_accumulate_sentinel_key_duplicates(cuda, layout, path):
         assert_bits_equal(got, want, f"sentinel x{n_ff}")
 
 
+@pytest.mark.parametrize("mode", ["assign", "accumulate"])
+def test_many_ragged_batches_grouped(cuda, oracle_mod, mode):
+    """150 ragged batches in one grouped Add and one grouped Get (more than the
+    64 a launch's kernarg holds, so both calls are cut into several launches):
+    empty, 1-key and 20 K-key batches, unsorted with duplicates and
+    out-of-range keys.  int32 values: assign and accumulate are bit-exact."""
+    import torch
+
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(150)
+    kb, size = 1000, 300_000
+    batches = []
+    for j in range(150):
+        n = int(rng.choice([0, 1, 2, 17, 999, 20_000]))
+        k = rng.integers(0, kb + size + 5000, size=n).astype(np.uint32)
+        v = rng.integers(-2**31, 2**31 - 1, size=n, dtype=np.int64).astype(np.int32)
+        batches.append((k, v))
+    q_batches = [rng.integers(0, kb + size + 5000, size=int(rng.choice([0, 1, 3000]))).astype(np.uint32)
+                 for _ in range(150)]
+    if mode == "assign":
+        ref = oracle_mod.MapStorageRef(np.int32)
+        for k, v in batches:
+            ref.add(k, v)
+        wants = [ref.get(q) for q in q_batches]
+    else:
+        acc = {}
+        for k, v in batches:
+            for kk, vv in zip(k.tolist(), v.tolist()):
+                acc[kk] = acc.get(kk, 0) + vv
+        wrap = lambda x: ((np.asarray(x, np.int64) + 2**31) % 2**32 - 2**31).astype(np.int32)
+        wants = [wrap([acc.get(int(x), 0) for x in q]) for q in q_batches]
+    with ps.Shard(kb, kb + size, np.int32, mode=mode, overflow_slots=1 << 16) as sh:
+        sh.add_grouped([(tdev(k, cuda), tdev(v, cuda)) for k, v in batches])
+        outs = [torch.empty(q.size, dtype=torch.int32, device=cuda) for q in q_batches]
+        sh.get_grouped([(tdev(q, cuda), o) for q, o in zip(q_batches, outs)])
+        torch.cuda.synchronize()
+        for j, (o, w) in enumerate(zip(outs, wants)):
+            assert_bits_equal(o.cpu().numpy(), w, f"{mode} batch {j}")
+
+
 def test_radix_accumulate_full_key_space_edges(cuda):
     """K5 accumulate on the reference's argument-less storage (the whole uint32
     key space in one shard, 16 GiB of int32 in HBM): the K5b -> K5c pair
