@@ -766,14 +766,23 @@ int stage_host_batches(pskv_shard* s, const std::vector<pskv_batch>& in,
     } else {
       // pageable (PSKV_PAGEABLE_DMA): the runtime's copies block the issuing
       // thread, so they are issued from a helper while the pool checks
-      std::thread t([&]() {
-        (void)hipSetDevice(s->device);
-        e = issue();
-      });
+      std::thread t;
+      try {
+        t = std::thread([&]() {
+          (void)hipSetDevice(s->device);
+          e = issue();
+        });
+      } catch (...) {  // no helper thread: issue, then check
+      }
+      if (!t.joinable()) e = issue();
       check();
-      t.join();
+      if (t.joinable()) t.join();
     }
-    PSKV_HIP(e);
+    if (e != hipSuccess) {
+      // copies queued before the failure may still read the caller's buffers
+      (void)hipStreamSynchronize(s->stream);
+      PSKV_HIP(e);
+    }
     // the caller may reuse its buffers once this returns
     PSKV_HIP(hipEventSynchronize(s->h2d_done));
   } else {
