@@ -29,6 +29,13 @@
  * Keys outside [key_begin, key_end) are legal (the reference's last range
  * server receives every out-of-range key, range_partition_manager.hpp:26-27):
  * they live in a device-side overflow hash table with the same semantics.
+ * Host inputs are counted while they are checked, and the table grows before
+ * the kernels run, so host calls (the reference's case) never run out of room.
+ * For PSKV_DEVICE inputs the keys are not read on the host: the table grows at
+ * pskv_sync (to keep its load <= 1/2), and one device call may add at most
+ * (capacity - stored) new out-of-range keys; beyond that keys are dropped and
+ * the next pskv_sync returns PSKV_ESTATE.  Size the table for the largest
+ * out-of-range burst a device caller expects (pskv_shard_create_ex).
  *
  * Threading: one shard handle is used by one host thread at a time (the
  * reference calls a storage only from its ServerThread, server_thread.cpp:20-50);
