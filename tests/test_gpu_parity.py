@@ -440,6 +440,29 @@ def test_overflow_table_growth_and_edges(cuda, oracle_mod):
     assert_bits_equal(got, ref.get(q), "overflow")
 
 
+@pytest.mark.parametrize("path", ["sorted_hint", "unsorted"])
+def test_device_overflow_burst_fails_loudly(cuda, path):
+    """PSKV_DEVICE inputs are not counted on the host: a burst of new
+    out-of-range keys larger than the overflow table is reported by the next
+    sync (PSKV_ESTATE), never silently; a burst that fits, followed by a sync,
+    grows the table for the next one."""
+    import parameter_server_amd as ps
+    from parameter_server_amd import PskvError, _lib
+
+    hint = path == "sorted_hint"
+    small = np.arange(10_000, 10_020, dtype=np.uint32)          # 20 new keys: fits 64 slots
+    with ps.Shard(0, 1000, np.float32, overflow_slots=64) as sh:
+        sh.add(tdev(small, cuda), tdev(np.ones(small.size, np.float32), cuda), sorted_hint=hint)
+        sh.sync()
+        assert sh.info()["overflow_capacity"] >= 2 * sh.info()["overflow_count"]
+        assert np.all(sh.get(small) == 1.0)
+        burst = np.arange(20_000, 25_000, dtype=np.uint32)      # 5000 new keys: cannot fit
+        sh.add(tdev(burst, cuda), tdev(np.full(burst.size, 2.0, np.float32), cuda), sorted_hint=hint)
+        with pytest.raises(PskvError) as ei:
+            sh.sync()
+        assert ei.value.code == _lib.PSKV_ESTATE
+
+
 def test_size_mismatch_is_rejected(cuda):
     from parameter_server_amd import CheckError, HipStorage, Message
 
