@@ -1056,7 +1056,7 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
   // f64 sums take 8 B per slot: half the slots in the same LDS
   constexpr int SLOTS = (MODE == 1 && sizeof(AT) == 8) ? (1 << LOGS) / 2 : (1 << LOGS);
   constexpr uint32_t CAP = (uint32_t)SLOTS / 8 * 7;  // entries per round (load <= 7/8)
-  constexpr int RPT = 12;                             // run entries held in registers
+  constexpr int RPT = 10;                             // run entries held in registers (10: no spills for 4-byte values)
   constexpr uint32_t LONG = 4 * RPT;                  // longer runs: the strided path
   static_assert(LONG <= 64, "a run's winners fit one 64-bit mask");
   constexpr uint32_t SC = rb_sc<BT>();
@@ -1174,16 +1174,17 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
   const uint32_t per_xcd = (gridDim.x + 7u - xcd) >> 3;  // workgroups in this XCD group
   const uint32_t b_hi = (uint32_t)((uint64_t)nbk * (xcd + 1) / 8);
   uint32_t b = (uint32_t)((uint64_t)nbk * xcd / 8) + (blockIdx.x >> 3);
-  const uint16_t* myrow = loff + (size_t)tid * (nbk + 1);
   const bool has_run = (uint32_t)tid < nsc;
+  const uint32_t rowo = has_run ? (uint32_t)tid * (nbk + 1) : 0u;  // this thread's loff row
   // software pipeline: the run of bucket b in registers, the run bounds of the
-  // bucket after it in flight
+  // bucket after it in flight.  The bounds loads are unconditional (a thread
+  // without a run, or past the last bucket, reads a valid word it then
+  // ignores) so nothing waits for them until the next bucket uses them.
+  auto bounds_ok = [&](uint32_t bb) { return bb < b_hi && has_run; };
   auto bounds = [&](uint32_t bb, uint32_t& a, uint32_t& e) {
-    a = e = 0;
-    if (bb < b_hi && has_run) {
-      a = myrow[bb];
-      e = myrow[bb + 1];
-    }
+    const uint32_t i = rowo + (bb < b_hi ? bb : 0u);
+    a = loff[i];
+    e = loff[i + 1];
   };
   auto load_run = [&](uint32_t a, uint32_t e, Ent (&x)[RPT]) {
 #pragma unroll
@@ -1201,6 +1202,7 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
   };
   uint32_t ra, re, na, ne_;
   bounds(b, ra, re);
+  if (!bounds_ok(b)) ra = re = 0;
   bounds(b + per_xcd, na, ne_);
   Ent xn[RPT];
   load_run(ra, re, xn);
@@ -1210,8 +1212,8 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
 #pragma unroll
     for (int q = 0; q < RPT; ++q) x[q] = xn[q];
     // next bucket: its run loads now, the bounds of the one after
-    ra = na;
-    re = ne_;
+    ra = bounds_ok(b + per_xcd) ? na : 0u;
+    re = bounds_ok(b + per_xcd) ? ne_ : 0u;
     load_run(ra, re, xn);
     bounds(b + 2 * per_xcd, na, ne_);
     pre[tid] = len;
