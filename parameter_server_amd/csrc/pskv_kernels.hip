@@ -61,6 +61,33 @@ __device__ __forceinline__ void st16(void* p, u32x4 v) {
     *reinterpret_cast<u32x4*>(p) = v;
 }
 
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+template <bool NT>
+__device__ __forceinline__ void ld8_keys(const uint32_t* p, uint32_t (&k)[2]) {
+  const u32x2 t = NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(p))
+                     : *reinterpret_cast<const u32x2*>(p);
+  k[0] = t.x;
+  k[1] = t.y;
+}
+
+// Two 8-byte values as one 16-byte access.  Streams of 8-byte values go two
+// per lane (a wave covers 1 KiB contiguously per instruction) rather than four
+// per lane as two 16-byte accesses 32 bytes apart (each instruction then
+// touches every line of a 2 KiB span for half its bytes).
+struct Vec2x8 {
+  using T = unsigned long long;
+  template <bool NT = false>
+  static __device__ __forceinline__ void load(const T* p, T (&v)[2]) {
+    const u32x4 a = ld16<NT>(p);
+    v[0] = (T)a.x | ((T)a.y << 32);
+    v[1] = (T)a.z | ((T)a.w << 32);
+  }
+  template <bool NT = false>
+  static __device__ __forceinline__ void store(T* p, const T (&v)[2]) {
+    st16<NT>(p, u32x4{(uint32_t)v[0], (uint32_t)(v[0] >> 32), (uint32_t)v[1], (uint32_t)(v[1] >> 32)});
+  }
+};
+
 template <typename VT>
 struct Vec4;
 
@@ -163,6 +190,21 @@ __device__ __forceinline__ void gather4(const DenseView& d, const Ovf& o, const 
   }
 }
 
+// Two keys of one lane, 8-byte values: one 16-byte load when they are two
+// consecutive in-range keys on an even offset.
+__device__ __forceinline__ void gather2(const DenseView& d, const Ovf& o, const uint32_t (&k)[2],
+                                        unsigned long long (&v)[2]) {
+  using T = unsigned long long;
+  const uint32_t off0 = k[0] - d.key_begin;
+  const bool run = (k[1] == k[0] + 1u) & ((off0 & 1u) == 0u) & ((uint64_t)off0 + 1u < d.range);
+  if (run) {
+    Vec2x8::load(reinterpret_cast<const T*>(d.param) + off0, v);
+  } else {
+    v[0] = load_one<T>(d, o, k[0]);
+    v[1] = load_one<T>(d, o, k[1]);
+  }
+}
+
 template <typename VT, bool VEC, int U, bool NT>
 __global__ __launch_bounds__(kBlock) void k_gather(GroupArgs ga, DenseView d, Ovf o) {
   constexpr int CH = kBlock * 4 * U;
@@ -173,6 +215,22 @@ __global__ __launch_bounds__(kBlock) void k_gather(GroupArgs ga, DenseView d, Ov
   const uint64_t n = ga.b[j].n;
   const uint64_t base = (uint64_t)(wg - ga.wg_prefix[j]) * CH;
   const int tid = threadIdx.x;
+  if constexpr (sizeof(VT) == 8) {
+    if (VEC && base + CH <= n) {
+      // two keys per lane per step (see Vec2x8): 8-byte key loads, 16-byte
+      // value loads and stores, every instruction one contiguous span
+      constexpr int UU = 2 * U;
+      uint32_t k[UU][2];
+#pragma unroll
+      for (int u = 0; u < UU; ++u) ld8_keys<NT>(keys + base + (uint64_t)(u * kBlock + tid) * 2, k[u]);
+      VT v[UU][2];
+#pragma unroll
+      for (int u = 0; u < UU; ++u) gather2(d, o, k[u], v[u]);
+#pragma unroll
+      for (int u = 0; u < UU; ++u) Vec2x8::store<NT>(out + base + (uint64_t)(u * kBlock + tid) * 2, v[u]);
+      return;
+    }
+  }
   if (VEC && base + CH <= n) {
     uint32_t k[U][4];
 #pragma unroll
@@ -396,6 +454,33 @@ __device__ __forceinline__ bool dense_chunk(const GroupArgs& ga, const DenseView
       Vec4<uint32_t>::load<NT>(keys + i, k);
       const uint32_t k0 = first + (uint32_t)i;
       bad |= (k[0] != k0) | (k[1] != k0 + 1u) | (k[2] != k0 + 2u) | (k[3] != k0 + 3u);
+    }
+  } else if (sizeof(VT) == 8 && VEC && end - base == CH) {
+    // 8-byte values two keys per lane per step (see Vec2x8)
+    using T = unsigned long long;
+    constexpr int UU = 2 * U;
+    uint32_t k[UU][2];
+    T v[UU][2];
+#pragma unroll
+    for (int u = 0; u < UU; ++u) {
+      const uint64_t i = base + (uint64_t)(u * kBlock + tid) * 2;
+      ld8_keys<NT>(keys + i, k[u]);
+      Vec2x8::load<NT>(reinterpret_cast<const T*>(vals) + i, v[u]);
+    }
+    T* __restrict__ p8 = reinterpret_cast<T*>(param);
+#pragma unroll
+    for (int u = 0; u < UU; ++u) {
+      const uint64_t i = base + (uint64_t)(u * kBlock + tid) * 2;
+      const uint32_t k0 = first + (uint32_t)i;
+      bad |= (k[u][0] != k0) | (k[u][1] != k0 + 1u);
+      const uint32_t off0 = k0 - d.key_begin;
+      if (later == 0 && (off0 & 1u) == 0u) {
+        Vec2x8::store<NTP>(p8 + off0, v[u]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+          if (!shadowed(k0 + e)) p8[off0 + e] = v[u][e];
+      }
     }
   } else if (VEC && end - base == CH) {
     uint32_t k[U][4];

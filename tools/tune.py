@@ -24,16 +24,19 @@ def main():
     variants = sys.argv[1:] or [""]
     rounds = int(os.environ.get("TUNE_ROUNDS", "8"))
     J = int(os.environ.get("TUNE_J", "64"))
+    f64 = os.environ.get("TUNE_DTYPE", "f32") == "f64"  # TUNE_DTYPE=f64: 8-byte values
+    V = 8 if f64 else 4
     space = 100_000_000
     dev = torch.device("cuda:0")
-    batches = workload.dense_batches(J, space, device=dev)
+    batches = workload.dense_batches(J, space, device=dev,
+                                     dtype=torch.float64 if f64 else torch.float32)
     outs = [torch.empty_like(v) for _, v in batches]
     shards = []
     for v in variants:
         env = dict(kv.split("=") for kv in v.split(",") if kv)
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
-        sh = ps.Shard(0, space, np.float32)
+        sh = ps.Shard(0, space, np.float64 if f64 else np.float32)
         for k, o in old.items():
             if o is None:
                 os.environ.pop(k)
@@ -82,16 +85,16 @@ def main():
         torch.cuda.synchronize()
         ct.append((time.perf_counter() - t0) * 1e3)
     med = statistics.median(ct)
-    print(f"{'torch copy_ (8 B/key)':40s}  {med:.4f}ms ({J * 1e6 * 8 / (med / 1e3) / 1e9:.0f} GB/s)")
+    print(f"{f'torch copy_ ({2 * V} B/key)':40s}  {med:.4f}ms ({J * 1e6 * 2 * V / (med / 1e3) / 1e9:.0f} GB/s)")
     for name, d in res.items():
         line = [f"{name:40s}"]
         for k, v in d.items():
             med = statistics.median(v)
             extra = ""
             if k in ("k_gather", "k_assign_group"):
-                extra = f" ({J * 1e6 * 12 / (med / 1e3) / 1e9:.0f} GB/s)"
+                extra = f" ({J * 1e6 * (4 + 2 * V) / (med / 1e3) / 1e9:.0f} GB/s)"
             if k in ("step", "step_untimed"):
-                extra = f" ({J * 1e6 * 24 / (med / 1e3) / 1e9:.0f} GB/s)"
+                extra = f" ({J * 1e6 * (8 + 4 * V) / (med / 1e3) / 1e9:.0f} GB/s)"
             line.append(f"{k}={med:.4f}ms{extra}")
         print("  ".join(line), flush=True)
 
