@@ -120,6 +120,18 @@ struct Vec4<unsigned long long> {
   }
 };
 
+// The widest lane layout of a value stream: N values per 16-byte access.
+template <typename BT>
+struct VecN;
+template <>
+struct VecN<uint32_t> : Vec4<uint32_t> {
+  static constexpr int N = 4;
+};
+template <>
+struct VecN<unsigned long long> : Vec2x8 {
+  static constexpr int N = 2;
+};
+
 // Which batch of a grouped launch this workgroup serves (wave-uniform scan of
 // the kernarg prefix table; nb <= 64).
 __device__ __forceinline__ int batch_of(const GroupArgs& ga, uint32_t wg) {
@@ -1548,23 +1560,27 @@ __global__ __launch_bounds__(kBlock) void k_acc_dense(GroupArgs ga, DenseView d,
     };
     const bool vec_ok = ((reinterpret_cast<uintptr_t>(vals) & 15u) == 0) && end - base == CH;
     if (vec_ok) {
-      BT v[U][4];
+      // N values per lane per 16-byte access: 4 (4-byte values) or 2 (8-byte,
+      // see Vec2x8); UU steps keep the chunk at CH keys
+      constexpr int N = VecN<BT>::N;
+      constexpr int UU = U * 4 / N;
+      BT v[UU][N];
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-        Vec4<BT>::template load<NT>(reinterpret_cast<const BT*>(vals) + base +
-                                        (uint64_t)(u * kBlock + tid) * 4,
+      for (int u = 0; u < UU; ++u)
+        VecN<BT>::template load<NT>(reinterpret_cast<const BT*>(vals) + base +
+                                        (uint64_t)(u * kBlock + tid) * N,
                                     v[u]);
-      if (earlier == 0 && ((first - d.key_begin) & 3u) == 0) {
+      if (earlier == 0 && ((first - d.key_begin) & (uint32_t)(N - 1)) == 0) {
         // no earlier batch meets this chunk (the common case), aligned: 16-B
         // RMW; later batches meeting it add their values in call order
-        BT p[U][4];
+        BT p[UU][N];
         BT* pb = reinterpret_cast<BT*>(param) + (first - d.key_begin) + base;
 #pragma unroll
-        for (int u = 0; u < U; ++u) Vec4<BT>::load(pb + (uint64_t)(u * kBlock + tid) * 4, p[u]);
+        for (int u = 0; u < UU; ++u) VecN<BT>::load(pb + (uint64_t)(u * kBlock + tid) * N, p[u]);
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
+        for (int u = 0; u < UU; ++u) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
+          for (int e = 0; e < N; ++e)
             p[u][e] = to_bits<AT>(add_wrap<AT>(from_bits<AT>(p[u][e]), from_bits<AT>(v[u][e])));
         }
         unsigned long long m = later;
@@ -1574,30 +1590,31 @@ __global__ __launch_bounds__(kBlock) void k_acc_dense(GroupArgs ga, DenseView d,
           const uint32_t fq = s_first[q], lq = s_last[q];
           const BT* __restrict__ vq = reinterpret_cast<const BT*>(ga.b[q].vals);
 #pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const uint32_t k0 = first + (uint32_t)(base + (uint64_t)(u * kBlock + tid) * 4);
-            BT w[4];
-            if (k0 >= fq && k0 + 3u <= lq && (((k0 - fq) & 3u) | (reinterpret_cast<uintptr_t>(vq) & 15u)) == 0) {
-              Vec4<BT>::template load<NT>(vq + (k0 - fq), w);
+          for (int u = 0; u < UU; ++u) {
+            const uint32_t k0 = first + (uint32_t)(base + (uint64_t)(u * kBlock + tid) * N);
+            BT w[N];
+            if (k0 >= fq && k0 + (uint32_t)(N - 1) <= lq &&
+                (((k0 - fq) & (uint32_t)(N - 1)) | (reinterpret_cast<uintptr_t>(vq) & 15u)) == 0) {
+              VecN<BT>::template load<NT>(vq + (k0 - fq), w);
 #pragma unroll
-              for (int e = 0; e < 4; ++e)
+              for (int e = 0; e < N; ++e)
                 p[u][e] = to_bits<AT>(add_wrap<AT>(from_bits<AT>(p[u][e]), from_bits<AT>(w[e])));
             } else {
 #pragma unroll
-              for (int e = 0; e < 4; ++e)
+              for (int e = 0; e < N; ++e)
                 if (k0 + e >= fq && k0 + e <= lq)
                   p[u][e] = to_bits<AT>(add_wrap<AT>(from_bits<AT>(p[u][e]), from_bits<AT>(vq[k0 + e - fq])));
             }
           }
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) Vec4<BT>::store(pb + (uint64_t)(u * kBlock + tid) * 4, p[u]);
+        for (int u = 0; u < UU; ++u) VecN<BT>::store(pb + (uint64_t)(u * kBlock + tid) * N, p[u]);
       } else {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const uint32_t k0 = first + (uint32_t)(base + (uint64_t)(u * kBlock + tid) * 4);
+        for (int u = 0; u < UU; ++u) {
+          const uint32_t k0 = first + (uint32_t)(base + (uint64_t)(u * kBlock + tid) * N);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) rmw(k0 + e, from_bits<AT>(v[u][e]));
+          for (int e = 0; e < N; ++e) rmw(k0 + e, from_bits<AT>(v[u][e]));
         }
       }
     } else {

@@ -36,7 +36,8 @@ def main():
         env = dict(kv.split("=") for kv in v.split(",") if kv)
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
-        sh = ps.Shard(0, space, np.float64 if f64 else np.float32)
+        sh = ps.Shard(0, space, np.float64 if f64 else np.float32,
+                      mode=os.environ.get("TUNE_MODE", "assign"))  # TUNE_MODE=accumulate: K6 + K7
         for k, o in old.items():
             if o is None:
                 os.environ.pop(k)
