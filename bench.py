@@ -48,8 +48,8 @@ def step_bytes(n_push, u_push, n_pull):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--batches", type=int, default=64, help="push/pull batches per step per GPU")
     p.add_argument("--batch-keys", type=int, default=1_000_000)
     p.add_argument("--no-cpu-baseline", action="store_true")
