@@ -593,6 +593,7 @@ int known_answers(MakeStorage make, const char* label) {
 }  // namespace
 
 int main(int argc, char** argv) {
+  std::setvbuf(stdout, nullptr, _IOLBF, 0);  // each line out as printed (logs survive an abort)
   Config c;
   bool ka = false;
   for (int i = 1; i < argc; ++i) {
