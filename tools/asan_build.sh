@@ -7,11 +7,12 @@
 #   bash tools/asan_build.sh && ASAN_OPTIONS=detect_leaks=0 scratch/asan/hip_storage_test
 set -euo pipefail
 R=$(cd "$(dirname "$0")/.." && pwd)
+SAN=${SAN:-address}  # e.g. SAN=address,undefined
 O=$R/scratch/asan
 mkdir -p "$O"
 CXX=/opt/rocm/llvm/bin/clang++
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -shared \
-  -Xarch_host -fsanitize=address -Xarch_host -fno-omit-frame-pointer \
+  -Xarch_host -fsanitize=$SAN -Xarch_host -fno-omit-frame-pointer \
   -I "$R/include" -I "$R/parameter_server_amd/csrc" \
   "$R/parameter_server_amd/csrc/pskv_kernels.hip" "$R/parameter_server_amd/csrc/pskv_shard.cpp" \
   -o "$O/libpskv.so"
@@ -20,7 +21,7 @@ for p in hip_storage_test kv_client_table_test ssp_replay; do
   if [ "$p" = ssp_replay ]; then
     extra=(-L "$R/oracle" -loracle "-Wl,-rpath,$R/oracle")
   fi
-  $CXX -O1 -g -std=c++11 -pthread -fsanitize=address -fno-omit-frame-pointer \
+  $CXX -O1 -g -std=c++11 -pthread -fsanitize=$SAN -fno-omit-frame-pointer \
     -I "$R/include" "$R/tests/cpp/$p.cpp" -o "$O/$p" \
     -L "$O" -lpskv '-Wl,-rpath,$ORIGIN' "${extra[@]}"
 done
