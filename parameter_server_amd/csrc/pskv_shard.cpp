@@ -459,17 +459,16 @@ int radix_launch(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size
   const uint32_t nsc = build_group(v, b, e, rb_superchunk(s->vb), &ga);
   uint64_t elems = 0;
   for (size_t i = b; i < e; ++i) elems += v[i].n;
-  // bucket = key offset >> bshift: about one bucket per 4 Ki pushed keys, at
-  // most 2048 dense buckets (more buckets: longer loff rows, shorter runs).
-  // The resolve workgroup handles a bucket from registers when its entries fit
-  // its LDS table: 2^13 slots (two workgroups per CU) while buckets average
+  // bucket = key offset >> bshift (more buckets: longer loff rows, shorter
+  // runs).  Per mode: assign takes one bucket per 2 Ki pushed keys, at most
+  // 2^11 bucket bits; accumulate, whose resolve also reads the parameters, one
+  // per 4 Ki, at most 2^10.  The sweep behind the rule (tools/zipf_probe.py,
+  // 4/8/16 x 1M Zipf keys) and its timings: DESIGN.md §7 "K5 bucket count",
+  // logs in profiles/r01_probes/probe_tb*.log and probe_new_*.log.
+  // The resolve workgroup uses a 2^13-slot LDS table while buckets average
   // <= 2 Ki pushed keys, else 2^14.
   uint32_t bits = 0;
   while (bits < 32 && ((s->range - 1) >> bits) != 0) ++bits;
-  // Measured on cfg-3 Zipf pushes (tools/zipf_probe.py, 4/8/16 x 1M keys):
-  // assign resolves fastest with the most buckets (one per 2 Ki pushed keys:
-  // 4 M keys 107 -> 87 us against one per 4 Ki); accumulate, whose resolve
-  // also reads the parameters, with at most 1024 (8 M keys 203 -> 194 us).
   const uint32_t per = s->mode == PSKV_ASSIGN ? 11 : 12, tmax = s->mode == PSKV_ASSIGN ? 11 : 10;
   uint32_t tb = 6;
   while (tb < tmax && (elems >> (per + tb)) != 0) ++tb;
