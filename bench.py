@@ -3,9 +3,15 @@
 One step = one pass of the hot path over one batch set: a grouped Add of J
 push batches (1M keys each) followed by a grouped Get of the same J pull
 batches, on every rank's shard.  Inputs are resident in HBM before timing.
+Consecutive steps rotate over R window sets (--sets, default 4; set r drawn
+with seed set_seed(r), set 0 being the config's own seed), so a step never
+re-pushes the windows of the step before it: the parameters a step touches are
+not left in the 256 MB Infinity Cache by the previous step.  (The round-1 form,
+the same set every step, is kept as extra.fixed_set_step, labelled cache-warm.)
 
   N = 1: configs[1] (cfg 2) — 1e8-key float shard, J x 1M contiguous-key
-         windows at seed-42 uniform 1M-aligned bases, vals U(-1,1), assign mode.
+         windows at uniform 1M-aligned bases (seed 42 for set 0), vals U(-1,1),
+         assign mode.
   N > 1: configs[3] (cfg 4) — 1e9 keys range-partitioned over N GPUs (one
          shard per rank, base/range_partition_manager.hpp's map); each rank's
          producers push J x 1M windows routed to it by the range map
@@ -52,9 +58,11 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--batches", type=int, default=64, help="push/pull batches per step per GPU")
     p.add_argument("--batch-keys", type=int, default=1_000_000)
+    p.add_argument("--sets", type=int, default=4, help="window sets rotated over the steps")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extra", action="store_true", help="skip the zipf / e2e side measurements")
-    p.add_argument("--cpu-batches", type=int, default=12)
+    p.add_argument("--cpu-batches", type=int, default=64,
+                   help="1M-key windows in the 1-thread CPU baseline sample (~10 s)")
     return p.parse_args()
 
 
@@ -119,20 +127,22 @@ def sum_over_ranks(x, world, dev):
     return float(t.item())
 
 
-def plan_rank(rank, world, J, B):
-    """Key range and push-window bases of one rank (pure host logic; tested with
-    gloo in tests/test_dist.py).  N = 1: cfg 2.  N > 1: cfg 4 weak scaling."""
+def plan_rank(rank, world, J, B, r=0):
+    """Key range and push-window bases (window set r) of one rank (pure host
+    logic; tested with gloo in tests/test_dist.py).  N = 1: cfg 2.  N > 1: cfg 4
+    weak scaling."""
     from parameter_server_amd import workload
 
+    seed = workload.set_seed(r, world)
     if world == 1:
         key_space = 100_000_000
         lo, hi = 0, key_space
-        bases = workload.dense_bases(J, key_space, B)
+        bases = workload.dense_bases(J, key_space, B, seed=seed)
     else:
         key_space = 1_000_000_000
         ranges = workload.rank_ranges(key_space, world)
         lo, hi = ranges[rank]
-        bases = workload.rank_windows(rank, world, key_space, J, B)
+        bases = workload.rank_windows(rank, world, key_space, J, B, seed=seed)
         routed = workload.route_windows(bases, B, ranges)
         # every window of this rank's producers is routed to this rank, whole
         assert all(len(routed[r]) == 0 for r in range(world) if r != rank)
@@ -140,19 +150,19 @@ def plan_rank(rank, world, J, B):
     return key_space, lo, hi, bases
 
 
-def make_workload(rank, world, J, B, dev):
+def make_workload(rank, world, J, B, dev, r=0):
+    """Window set r of this rank: J (keys, vals) push batches in HBM."""
     import torch
 
-    key_space, lo, hi, bases = plan_rank(rank, world, J, B)
+    key_space, lo, hi, bases = plan_rank(rank, world, J, B, r)
     batches = []
     for j, b in enumerate(bases):
         keys = torch.arange(int(b), int(b) + B, dtype=torch.int64, device=dev).to(torch.int32)
         g = torch.Generator(device=dev)
-        g.manual_seed(42 + j + 1000 * rank)
+        g.manual_seed(42 + j + 1000 * rank + 100_000 * r)
         vals = torch.rand(B, generator=g, device=dev, dtype=torch.float32) * 2 - 1
         batches.append((keys, vals))
-    outs = [torch.empty(B, dtype=torch.float32, device=dev) for _ in range(J)]
-    return key_space, lo, hi, bases, batches, outs
+    return key_space, lo, hi, bases, batches
 
 
 def cpu_baseline(bases, B, n_batches):
@@ -186,9 +196,9 @@ def cpu_baseline(bases, B, n_batches):
     # storage per server thread); ctypes drops the GIL inside the oracle calls
     import threading
 
-    T = 8
+    T, mt_batches = 8, min(12, len(ks))  # 8 threads x 12 windows each (~3 s)
     shards = [oracle.MapStorageRef(np.float32) for _ in range(T)]
-    work = [[(k, v) for k, v in zip(ks, vs)] for _ in range(T)]
+    work = [[(k, v) for k, v in zip(ks[:mt_batches], vs[:mt_batches])] for _ in range(T)]
     barrier_t = threading.Barrier(T + 1)
 
     def serve(t):
@@ -206,8 +216,10 @@ def cpu_baseline(bases, B, n_batches):
     for x in th:
         x.join()
     t_mt = time.perf_counter() - t0
+    # same byte accounting as the GPU value (u = distinct keys pushed)
+    add_b, get_b = step_bytes(B * len(ks), B * len(set(int(b) for b in bases[:n_batches])), B * len(ks))
     return {
-        "value": 24.0 * B * len(ks) / t_map / 1e9,
+        "value": (add_b + get_b) / t_map / 1e9,
         "unit": "GB/s",
         "cores": 1,
         "kind": "port",
@@ -219,8 +231,9 @@ def cpu_baseline(bases, B, n_batches):
                       f"keys (config 1 at 1/10 size; the 1e6 case is ~100x longer, quadratic)",
         },
         "eight_threads": {
-            "value": 24.0 * B * len(ks) * T / t_mt / 1e9, "unit": "GB/s", "cores": T, "seconds": t_mt,
-            "sample": f"{T} threads x one MapStorage restatement each, {len(ks)} x {B} keys per thread"},
+            "value": sum(step_bytes(B * mt_batches, B * len(set(int(b) for b in bases[:mt_batches])),
+                                    B * mt_batches)) * T / t_mt / 1e9, "unit": "GB/s", "cores": T, "seconds": t_mt,
+            "sample": f"{T} threads x one MapStorage restatement each, {mt_batches} x {B} keys per thread"},
         "host_cpu": _cpu_model(),
     }
 
@@ -479,6 +492,42 @@ def cold_get_step(shard, adds, bases, J, B, dev, steps):
             "k_assign_group_ms": a["total_ms"] / max(1, a["launches"])}
 
 
+def fixed_set_step(shard, adds, gets, bases, J, B, steps):
+    """The round-1 headline form: the SAME window set every step.  The 48
+    distinct windows (192 MB of parameters) then stay largely resident in the
+    256 MB Infinity Cache from one step to the next, so this is the cache-warm
+    figure, reported apart from the rotating-set `value`."""
+    import torch
+
+    from parameter_server_amd import _lib
+
+    for _ in range(2):
+        shard.add_grouped(adds, sorted_hint=True)
+        shard.get_grouped(gets)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        shard.add_grouped(adds, sorted_hint=True)
+        shard.get_grouped(gets)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    shard.reset_timing()
+    shard.set_timing(True, kernels=[_lib.PSKV_K_GATHER, _lib.PSKV_K_ASSIGN_TILES])
+    for _ in range(steps):
+        shard.add_grouped(adds, sorted_hint=True)
+        shard.get_grouped(gets)
+    torch.cuda.synchronize()
+    shard.set_timing(False)
+    g = shard.kernel_time(_lib.PSKV_K_GATHER)
+    a = shard.kernel_time(_lib.PSKV_K_ASSIGN_TILES)
+    add_b, get_b = step_bytes(J * B, len(set(int(b) for b in bases)) * B, J * B)
+    return {"workload": f"cfg 2 step over ONE window set ({J} x {B}, seed 42) every step: cache-warm "
+                        "(the step's parameters stay in the Infinity Cache between steps)",
+            "GB/s": (add_b + get_b) * steps / dt / 1e9, "ms_per_step": dt / steps * 1e3,
+            "k_gather_ms": g["total_ms"] / max(1, g["launches"]),
+            "k_assign_group_ms": a["total_ms"] / max(1, a["launches"])}
+
+
 def main():
     args = parse()
     # the JSON line is the only thing on stdout: everything else the run prints
@@ -489,29 +538,44 @@ def main():
     import torch
 
     import parameter_server_amd as ps
-    from parameter_server_amd import _lib
+    from parameter_server_amd import _lib, workload
 
     rank, world, local = dist_init(args)
     dev = torch.device(f"cuda:{local}")
-    J, B = args.batches, args.batch_keys
-    key_space, lo, hi, bases, batches, outs = make_workload(rank, world, J, B, dev)
+    J, B, R = args.batches, args.batch_keys, max(1, args.sets)
+    sets = [make_workload(rank, world, J, B, dev, r) for r in range(R)]
+    key_space, lo, hi = sets[0][:3]
+    outs = [torch.empty(B, dtype=torch.float32, device=dev) for _ in range(J)]  # shared by the sets
     stream = torch.cuda.current_stream()
     shard = ps.Shard(lo, hi, np.float32, device=local)
     shard.set_stream(stream.cuda_stream)  # torch events and the kernels share one stream
-    adds = shard.prepare(batches)
-    gets = shard.prepare([(k, o) for (k, _), o in zip(batches, outs)], is_get=True)
+    plans = []  # per set: (bases, batches, prepared adds, prepared gets, step bytes)
+    for _, _, _, bases_r, batches_r in sets:
+        u_r = len(set(int(b) for b in bases_r)) * B  # distinct keys pushed by the set
+        plans.append((bases_r, batches_r, shard.prepare(batches_r),
+                      shard.prepare([(k, o) for (k, _), o in zip(batches_r, outs)], is_get=True),
+                      sum(step_bytes(J * B, u_r, J * B)), u_r))
+    bases, batches, adds, gets = plans[0][:4]
 
-    def step():
-        shard.add_grouped(adds, sorted_hint=True)
-        shard.get_grouped(gets)
+    def step(i):
+        p = plans[i % R]
+        shard.add_grouped(p[2], sorted_hint=True)
+        shard.get_grouped(p[3])
 
-    for _ in range(args.warmup):
-        step()
+    def bytes_of(k):  # algorithmic bytes of steps 0..k-1
+        return sum(plans[i % R][4] for i in range(k))
+
+    for i in range(max(args.warmup, R)):
+        step(i)
     torch.cuda.synchronize()
-    # correctness guard on the benchmarked state: every pull returns the last push of its window
-    last = {int(b): j for j, b in enumerate(bases)}
-    for j, b in enumerate(bases):
-        assert torch.equal(outs[j], batches[last[int(b)]][1]), "bench self-check failed"
+    # correctness guard on the benchmarked state: every pull returns the last
+    # push of its window, for every window set
+    for r, (bases_r, batches_r, *_rest) in enumerate(plans):
+        step(r)
+        torch.cuda.synchronize()
+        last = {int(b): j for j, b in enumerate(bases_r)}
+        for j, b in enumerate(bases_r):
+            assert torch.equal(outs[j], batches_r[last[int(b)]][1]), "bench self-check failed"
 
     # timed region: exactly K steps, barrier + synchronize on both sides, no
     # instrumentation inside (each HIP event record on the stream costs ~4.6 us
@@ -519,8 +583,8 @@ def main():
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for i in range(args.steps):
+        step(i)
     torch.cuda.synchronize()
     t_own = time.perf_counter()  # this rank's own work done
     barrier(world)
@@ -533,8 +597,8 @@ def main():
     shard.set_timing(True, kernels=[_lib.PSKV_K_GATHER, _lib.PSKV_K_ASSIGN_TILES])
     torch.cuda.synchronize()
     t2 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for i in range(args.steps):
+        step(i)
     torch.cuda.synchronize()
     t3 = time.perf_counter()
     shard.set_timing(False)
@@ -547,11 +611,13 @@ def main():
             ktimes[name] = {"launches": t["launches"], "avg_ms": t["total_ms"] / t["launches"],
                             "keys_per_launch": t["elements"] / t["launches"]}
     shard.sync()
-    u_push = len(set(int(b) for b in bases)) * B  # distinct keys pushed per step
+    # per-step bytes, averaged over the rotation as the steps ran it
+    u_push = sum(plans[i % R][5] for i in range(args.steps)) / args.steps  # distinct keys pushed per step
     add_b, get_b = step_bytes(J * B, u_push, J * B)
-    total_bytes = sum_over_ranks(float((add_b + get_b) * args.steps), world, dev)
+    own_bytes = float(bytes_of(args.steps))
+    total_bytes = sum_over_ranks(own_bytes, world, dev)
     value = total_bytes / elapsed / 1e9
-    own = (add_b + get_b) * args.steps / (t_own - t0) / 1e9
+    own = own_bytes / (t_own - t0) / 1e9
     per_gpu = {"mean_GB/s": value / world, "min_GB/s": -max_over_ranks(-own, world, dev),
                "max_GB/s": max_over_ranks(own, world, dev)}
 
@@ -559,7 +625,7 @@ def main():
     dom = max(ktimes.items(), key=lambda kv: kv[1]["avg_ms"] * kv[1]["launches"])
     launch_bytes = get_b if dom[0] == "k_gather" else add_b  # one launch = one step's Add or Get
     achieved = launch_bytes / (dom[1]["avg_ms"] / 1e3) / 1e9
-    traffic, traffic_src = load_pmc(dom[0], {"n_gpus": world, "batches": J, "batch_keys": B})
+    traffic, traffic_src = load_pmc(dom[0], {"n_gpus": world, "batches": J, "batch_keys": B, "sets": R})
     for name, kt in ktimes.items():
         kt["algorithmic_bytes"] = get_b if name == "k_gather" else add_b
         kt["GB/s"] = kt["algorithmic_bytes"] / (kt["avg_ms"] / 1e3) / 1e9
@@ -592,11 +658,13 @@ def main():
             "workload": ("cfg 2 dense: 1e8-key float shard" if world == 1 else
                          f"cfg 4 ranges: 1e9 keys over {world} range shards") +
                         f", {J} x {B} contiguous-key push batches then the same pulls per step per GPU, "
-                        "assign (last-write-wins) mode, grouped launches",
+                        f"assign (last-write-wins) mode, grouped launches, {R} window sets rotated over the steps",
             "key_space": key_space,
             "shard_keys_per_gpu": hi - lo,
             "batches_per_step_per_gpu": J,
             "batch_keys": B,
+            "window_sets": R,
+            "window_set_seeds": [workload.set_seed(r, world) for r in range(R)],
             "bytes_per_step_per_gpu": add_b + get_b,
             "distinct_pushed_keys_per_step": u_push,
             "parallelism": f"range-sharded x{world} (no collective)",
@@ -610,9 +678,11 @@ def main():
         result["cpu_baseline"] = cpu_baseline(bases, B, args.cpu_batches)
     if rank == 0 and world == 1 and not args.no_extra:
         cold = cold_get_step(shard, adds, bases, J, B, dev, args.steps)
+        fixed = fixed_set_step(shard, adds, gets, bases, J, B, args.steps)
         shard.set_stream(None)
         result["extra"] = side_measurements(dev, B)
         result["extra"]["cold_get_step"] = cold
+        result["extra"]["fixed_set_step"] = fixed
         result["extra"]["dense_f64_step"] = dense_f64_step(batches, bases, J, B, dev, args.steps)
     shard.close()
     if rank == 0:

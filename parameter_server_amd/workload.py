@@ -80,17 +80,25 @@ def rank_ranges(key_space: int, world: int):
     return [(r * step, (r + 1) * step if r + 1 < world else key_space) for r in range(world)]
 
 
-def rank_windows(rank: int, world: int, key_space: int, n_windows: int, batch: int = MILLION):
+def rank_windows(rank: int, world: int, key_space: int, n_windows: int, batch: int = MILLION,
+                 seed: int = 1000):
     """cfg 4 producer windows for one rank: stream s of rank r draws its base with
-    seed 1000 + (r * n_windows + s), a uniform multiple of `batch` inside the rank's
-    range.  Returns base offsets (int64)."""
+    seed `seed` + (r * n_windows + s) (default 1000), a uniform multiple of `batch`
+    inside the rank's range.  Returns base offsets (int64)."""
     lo, hi = rank_ranges(key_space, world)[rank]
     slots = (hi - lo) // batch
     bases = []
     for s in range(n_windows):
-        rng = np.random.default_rng(1000 + rank * n_windows + s)
+        rng = np.random.default_rng(seed + rank * n_windows + s)
         bases.append(lo + int(rng.integers(0, slots)) * batch)
     return np.asarray(bases, dtype=np.int64)
+
+
+def set_seed(r: int, world: int) -> int:
+    """Base seed of window set r (the bench rotates R sets of windows over its
+    steps, so no step re-pushes the windows the step before it touched).  Set 0
+    is the config's own seed: 42 (cfg 2) / 1000 (cfg 4)."""
+    return (42 if world == 1 else 1000) + 100_000 * r
 
 
 def route_windows(bases, batch, ranges):

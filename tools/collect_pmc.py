@@ -40,7 +40,8 @@ def short(name):
 def main():
     fetch_csv, write_csv, out = sys.argv[1:4]
     # the bench configuration profiled (bench.py uses the traffic only for the same one)
-    config = json.loads(sys.argv[4]) if len(sys.argv) > 4 else {"n_gpus": 1, "batches": 64, "batch_keys": 1000000}
+    config = json.loads(sys.argv[4]) if len(sys.argv) > 4 else {"n_gpus": 1, "batches": 64, "batch_keys": 1000000,
+                                                                "sets": 4}
     fe = per_dispatch(fetch_csv, "FETCH_SIZE")
     wr = per_dispatch(write_csv, "WRITE_SIZE")
     res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of bench.py; "
