@@ -122,7 +122,9 @@ enum pskv_kernel {
   PSKV_K_RADIX = 5,         /* K5a-d: radix-bucket general Add (timed as one operation) */
   PSKV_K_DENSE_CHECK = 6,   /* K6: accumulate, prove the batches dense windows */
   PSKV_K_ACC_DENSE = 7,     /* K7: accumulate dense windows, one RMW per key */
-  PSKV_K_COUNT = 8
+  PSKV_K_INLINE_ADD = 8,    /* K8: small host Add carried in the kernel arguments */
+  PSKV_K_INLINE_GET = 9,    /* K8: small host Get, reply written to page-locked memory */
+  PSKV_K_COUNT = 10
 };
 
 /* Create a shard owning keys [key_begin, key_end) on `device`.  The dense
@@ -138,7 +140,11 @@ int pskv_shard_destroy(pskv_shard* s);
 
 /* Push: apply n (key, value) pairs.  Asynchronous on the shard's stream for
  * PSKV_DEVICE inputs (the caller keeps them alive until the stream passes the
- * call); host inputs are staged before return and may be reused immediately. */
+ * call); host inputs are staged before return and may be reused immediately.
+ * A host call of at most 256 keys in all (grouped: summed over its batches)
+ * travels inside the kernel arguments (no staging copy) and returns once the
+ * launch is enqueued; a host Get of at most 512 keys likewise, its reply
+ * written by the kernel into page-locked memory (PSKV_INLINE=0 disables). */
 int pskv_add(pskv_shard* s, const uint32_t* keys, const void* vals, uint64_t n, int flags);
 /* Pull: out[i] = value of keys[i] (0 if never written).  Synchronous for host
  * `out` (PSKV_HOST), stream-ordered for device `out` (PSKV_DEVICE). */

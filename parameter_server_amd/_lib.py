@@ -32,7 +32,9 @@ PSKV_K_GENERAL_COMMIT = 4
 PSKV_K_RADIX = 5
 PSKV_K_DENSE_CHECK = 6
 PSKV_K_ACC_DENSE = 7
-PSKV_K_COUNT = 8
+PSKV_K_INLINE_ADD = 8
+PSKV_K_INLINE_GET = 9
+PSKV_K_COUNT = 10
 KERNEL_NAMES = {
     PSKV_K_GATHER: "k_gather",
     PSKV_K_ASSIGN_SORTED: "k_assign_sorted",
@@ -42,6 +44,8 @@ KERNEL_NAMES = {
     PSKV_K_RADIX: "k_radix_bucket",
     PSKV_K_DENSE_CHECK: "k_dense_check",
     PSKV_K_ACC_DENSE: "k_acc_dense",
+    PSKV_K_INLINE_ADD: "k_inline_add",
+    PSKV_K_INLINE_GET: "k_inline_get",
 }
 
 # Every symbol include/pskv.h declares (checked by tests/test_abi.py).

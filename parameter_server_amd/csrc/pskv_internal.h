@@ -24,6 +24,8 @@ constexpr int kGeneralChunk = 2048;  // keys per workgroup in the dedup path
 constexpr int kGeneralSlots = 4096;  // LDS hash slots (load factor <= 1/2)
 constexpr int kRbMaxBuckets = 2064;  // key buckets incl. the out-of-range bucket (>= 2049)
 constexpr uint32_t kRbMaxSc = 1024;  // K5 super-chunks per launch (one run per resolve thread)
+constexpr int kInlineMax = 256;      // keys of an inline (kernarg-carried) Add
+constexpr int kInlineGetMax = 512;   // keys of an inline Get
 constexpr unsigned long long kEmpty64 = ~0ull;
 constexpr uint32_t kEmpty32 = 0xFFFFFFFFu;
 
@@ -43,6 +45,19 @@ struct GroupArgs {
   uint64_t elem_prefix[kMaxBatches];    // group-wide index of each batch's first element
   DevBatch b[kMaxBatches];
 };
+
+// K8: a whole small message inside the kernel arguments (<= 4 KiB kernarg).
+struct InlineAdd {
+  uint32_t n;
+  uint32_t keys[kInlineMax];
+  unsigned long long vals[kInlineMax];  // value bits (4-byte values in the low word)
+};
+struct InlineGet {
+  uint32_t n;
+  uint32_t keys[kInlineGetMax];
+};
+static_assert(sizeof(InlineAdd) + 128 <= 4096 && sizeof(InlineGet) + 128 <= 4096,
+              "inline messages must fit the kernarg segment with the other arguments");
 
 struct DenseView {
   void* param;
@@ -92,6 +107,14 @@ hipError_t launch_rb_add(int dtype, int mode, const GroupArgs& ga, uint32_t nsc,
                          const DenseView& d, const Ovf& o, uint32_t bshift, uint32_t nbd,
                          int apply_log2, uint16_t* loff, void* tmp, hipStream_t st);
 uint32_t rb_superchunk(int vb);
+// K8: one small host message carried in the kernarg segment (one workgroup).
+// Get writes its n values to `out` (page-locked host memory or device memory);
+// with `done` non-null it then stores `seq` there (system-scope release) for a
+// host that polls instead of waiting on the stream.
+hipError_t launch_inline_add(int dtype, int mode, const InlineAdd& a, const DenseView& d,
+                             const Ovf& o, hipStream_t st);
+hipError_t launch_inline_get(int vb, const InlineGet& a, const DenseView& d, const Ovf& o,
+                             void* out, unsigned int* done, unsigned int seq, hipStream_t st);
 size_t rb_entry_bytes(int vb);
 // K6: tag `flag` with `epoch` unless every batch is a dense in-range window
 // (chunk = kBlock * 4 * 8 keys per workgroup).

@@ -1623,6 +1623,86 @@ __global__ __launch_bounds__(kBlock) void k_acc_dense(GroupArgs ga, DenseView d,
   }
 }
 
+
+// ------------------------------------------------ K8 inline small messages
+// The reference's live traffic is many small messages: a logistic-regression
+// worker pushes and pulls one sample's features at a time (tens of keys,
+// app/logistic_regression.cpp:411,490), sliced over the server threads.  For
+// those the cost of a call is latency, not bandwidth: staging DMAs (H2D of keys
+// and values, D2H of the reply) and their completion waits dominate.  Here the
+// keys (and an Add's values) travel INSIDE the kernel arguments — the launch
+// packet's kernarg segment is the only host->device transfer — and a Get writes
+// its reply straight into page-locked host memory.  One workgroup does the
+// whole message with the reference's sequential semantics:
+//   assign      element i stores iff no later element has its key (last wins,
+//               map_storage.hpp:22-23)
+//   accumulate  the FIRST occurrence of a key adds every occurrence's value in
+//               index order: ((p + v_a) + v_b) + ..., bit-identical to the
+//               sequential loop
+// Distinct threads write distinct keys, and calls are stream-ordered, so no
+// atomics are needed on the dense array (the overflow table's insert uses its
+// usual CAS).
+
+template <typename VT, int MODE>
+__global__ __launch_bounds__(kInlineMax) void k_inline_add(InlineAdd a, DenseView d, Ovf o) {
+  // Every lane walks the whole message with a wave-UNIFORM index, so each key
+  // and value is one scalar load from the kernarg segment shared by the wave
+  // (a per-lane start index would turn the walk into dependent vector loads,
+  // ~10 us at 256 keys).
+  const int tid = threadIdx.x;
+  const int n = (int)a.n;
+  const uint32_t k = tid < n ? a.keys[tid] : 0u;
+  using BT = typename std::conditional<sizeof(VT) == 8, unsigned long long, uint32_t>::type;
+  if (MODE == 0) {
+    bool later = false;
+#pragma unroll 16
+    for (int j = 0; j < n; ++j) later |= (j > tid) & (a.keys[j] == k);
+    if (tid >= n || later) return;  // a later occurrence wins
+    const BT v = (BT)a.vals[tid];
+    const uint32_t off = k - d.key_begin;
+    if ((uint64_t)off < d.range) {
+      reinterpret_cast<BT*>(d.param)[off] = v;
+    } else {
+      const long long slot = ovf_insert(o, k);
+      if (slot >= 0) reinterpret_cast<BT*>(o.vals)[slot] = v;
+    }
+  } else {
+    bool earlier = false;
+#pragma unroll 16
+    for (int j = 0; j < n; ++j) earlier |= (j < tid) & (a.keys[j] == k);
+    if (tid >= n || earlier) return;  // the first occurrence sums them all
+    const uint32_t off = k - d.key_begin;
+    VT* p;
+    if ((uint64_t)off < d.range) {
+      p = reinterpret_cast<VT*>(d.param) + off;
+    } else {
+      const long long slot = ovf_insert(o, k);
+      if (slot < 0) return;
+      p = reinterpret_cast<VT*>(o.vals) + slot;
+    }
+    VT acc = *p;
+#pragma unroll 16
+    for (int j = 0; j < n; ++j)  // index order: the sequential loop's sum, bit for bit
+      if ((j >= tid) & (a.keys[j] == k)) acc = add_wrap<VT>(acc, from_bits<VT>(a.vals[j]));
+    *p = acc;
+  }
+}
+
+// One wave: its own stores are the whole reply, so when `done` is given (the
+// spin-wait reply) lane 0 can publish it with a system-scope release and a
+// sequence number the host polls — no cross-wave hand-off to order.
+template <typename VT>
+__global__ __launch_bounds__(64) void k_inline_get(InlineGet a, DenseView d, Ovf o, VT* out,
+                                                   unsigned int* done, unsigned int seq) {
+  for (uint32_t i = threadIdx.x; i < a.n; i += 64) out[i] = load_one<VT>(d, o, a.keys[i]);
+  if (done) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the reply before the flag
+    // MI355X_MICROARCH.md "Compiler hazard": keep the wait after the write-back
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x == 0) __hip_atomic_store(done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 }  // namespace
 
 // ------------------------------------------------------- launch wrappers
@@ -1834,5 +1914,35 @@ hipError_t launch_acc_dense(int dtype, const GroupArgs& ga, uint32_t grid, const
 uint32_t rb_superchunk(int vb) { return vb == 8 ? rb_sc<unsigned long long>() : rb_sc<uint32_t>(); }
 size_t rb_entry_bytes(int vb) { return vb == 8 ? sizeof(RbEnt<8>) : sizeof(RbEnt<4>); }
 
+
+hipError_t launch_inline_add(int dtype, int mode, const InlineAdd& a, const DenseView& d,
+                             const Ovf& o, hipStream_t st) {
+  if (a.n == 0) return hipSuccess;
+  if (mode == 0) {
+    // assign moves value bits only: int32 and float share the 4-byte form
+    if (dtype == 2)
+      k_inline_add<double, 0><<<1, kInlineMax, 0, st>>>(a, d, o);
+    else
+      k_inline_add<float, 0><<<1, kInlineMax, 0, st>>>(a, d, o);
+  } else if (dtype == 0) {
+    k_inline_add<int, 1><<<1, kInlineMax, 0, st>>>(a, d, o);
+  } else if (dtype == 1) {
+    k_inline_add<float, 1><<<1, kInlineMax, 0, st>>>(a, d, o);
+  } else {
+    k_inline_add<double, 1><<<1, kInlineMax, 0, st>>>(a, d, o);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_inline_get(int vb, const InlineGet& a, const DenseView& d, const Ovf& o,
+                             void* out, unsigned int* done, unsigned int seq, hipStream_t st) {
+  if (a.n == 0) return hipSuccess;
+  if (vb == 8)
+    k_inline_get<unsigned long long><<<1, 64, 0, st>>>(a, d, o, static_cast<unsigned long long*>(out),
+                                                       done, seq);
+  else
+    k_inline_get<uint32_t><<<1, 64, 0, st>>>(a, d, o, static_cast<uint32_t*>(out), done, seq);
+  return hipGetLastError();
+}
 
 }  // namespace pskv

@@ -233,6 +233,12 @@ struct pskv_shard {
   // 8 x 1M keys: 1.43 ms against 1.75 ms staged, Get 1.37 against 1.44 ms.
   bool tune_pageable_dma = true;
   uint32_t tune_rb_tb = 0; // PSKV_RB_TB: K5 bucket bits (0 = by element count)
+  // PSKV_INLINE: host calls of <= kInlineMax (Add) / kInlineGetMax (Get) keys in
+  // all travel inside the kernel arguments (K8); 0 sends them through staging
+  bool tune_inline = true;
+  void* ireply = nullptr;  // page-locked reply buffer of inline Gets (kInlineGetMax values)
+  bool tune_ispin = true;  // PSKV_ISPIN: poll the reply's sequence word instead of a stream wait
+  unsigned int ireply_seq = 0;
   int tune_rb_apply_log2 = 0; // PSKV_RB_APPLY_LOG2: 13 or 14 (0 = by bucket size)
 
   DenseView dview() const { return DenseView{dense, key_begin, range}; }
@@ -819,6 +825,101 @@ int stage_host_batches(pskv_shard* s, const std::vector<pskv_batch>& in,
   return PSKV_OK;
 }
 
+// K8: a host Add of at most kInlineMax keys in all (the reference's per-sample
+// messages).  The grouped form equals the concatenation of its batches in
+// order (last-wins / sums follow index order across batches), so the batches
+// are packed into one kernel-argument message; the caller's buffers are free
+// once the launch is enqueued (the runtime copies the arguments).
+int inline_add(pskv_shard* s, const std::vector<pskv_batch>& v, uint64_t total) {
+  InlineAdd a;
+  a.n = (uint32_t)total;
+  uint32_t i = 0;
+  uint64_t outside = 0;
+  for (const auto& b : v) {
+    for (uint64_t e = 0; e < b.n; ++e, ++i) {
+      const uint32_t k = b.keys[e];
+      a.keys[i] = k;
+      outside += (uint64_t)(uint32_t)(k - s->key_begin) >= s->range;
+      if (s->vb == 8) {
+        std::memcpy(&a.vals[i], static_cast<const char*>(b.vals) + e * 8, 8);
+      } else {
+        uint32_t w;
+        std::memcpy(&w, static_cast<const char*>(b.vals) + e * 4, 4);
+        a.vals[i] = w;
+      }
+    }
+  }
+  if (outside) {
+    // exact bound on new overflow keys, as for staged host inputs
+    if (2 * (s->ocount_known + outside) > s->ocap) {
+      uint32_t cnt, err;
+      int rc = read_overflow_stat(s, &cnt, &err);
+      if (!rc) rc = grow_overflow(s, cnt + outside);
+      if (rc) return rc;
+    }
+    s->ocount_known += outside;
+  }
+  LaunchTimer t(s, PSKV_K_INLINE_ADD, total);
+  PSKV_HIP(launch_inline_add(s->dtype, s->mode, a, s->dview(), s->ovf, s->stream));
+  t.done();
+  return PSKV_OK;
+}
+
+// K8 Get: keys in the kernel arguments, the reply written by the kernel into a
+// page-locked buffer, copied out to the caller after the stream completes.
+int inline_get(pskv_shard* s, const std::vector<pskv_batch>& v, uint64_t total) {
+  if (!s->ireply) {
+    // kInlineGetMax values, then the reply's sequence word on its own line.
+    // Coherent (fine-grained) memory: the kernel's stores go straight to the
+    // host.  Measured alternatives (tools/micro/small_latency.cpp, DESIGN.md
+    // §5): non-coherent pinned memory the same, a device reply + D2H copy
+    // 3 us slower.
+    if (hipHostMalloc(&s->ireply, (size_t)kInlineGetMax * 8 + 128, hipHostMallocCoherent) != hipSuccess) {
+      s->ireply = nullptr;
+      return fail(PSKV_ENOMEM, "inline reply buffer allocation failed");
+    }
+  }
+  InlineGet a;
+  a.n = (uint32_t)total;
+  uint32_t i = 0;
+  for (const auto& b : v) {
+    std::memcpy(&a.keys[i], b.keys, b.n * 4);
+    i += (uint32_t)b.n;
+  }
+  LaunchTimer t(s, PSKV_K_INLINE_GET, total);
+  // spin-wait reply (coherent host buffer, no timing events to drain): the
+  // kernel publishes a sequence number after the values and the host polls it
+  const bool spin = s->tune_ispin && !t.a;
+  unsigned int* done = reinterpret_cast<unsigned int*>(static_cast<char*>(s->ireply) + (size_t)kInlineGetMax * 8);
+  const unsigned int seq = ++s->ireply_seq;
+  PSKV_HIP(launch_inline_get(s->vb, a, s->dview(), s->ovf, s->ireply, spin ? done : nullptr, seq,
+                             s->stream));
+  t.done();
+  if (spin) {
+    // poll the sequence word; every 1024 polls ask the stream whether it
+    // finished (or failed) without publishing, so a fault cannot hang the host
+    for (uint32_t it = 1;; ++it) {
+      if (__atomic_load_n(done, __ATOMIC_ACQUIRE) == seq) break;
+      if ((it & 1023u) == 0) {
+        const hipError_t e = hipStreamQuery(s->stream);
+        if (e == hipSuccess) {
+          if (__atomic_load_n(done, __ATOMIC_ACQUIRE) == seq) break;
+          return fail(PSKV_EHIP, "inline get: kernel finished without publishing its reply");
+        }
+        if (e != hipErrorNotReady) PSKV_HIP(e);
+      }
+    }
+  } else {
+    PSKV_HIP(hipStreamSynchronize(s->stream));
+  }
+  const char* r = static_cast<const char*>(s->ireply);
+  for (const auto& b : v) {
+    std::memcpy(b.vals, r, b.n * (size_t)s->vb);
+    r += b.n * (size_t)s->vb;
+  }
+  return PSKV_OK;
+}
+
 int add_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
   std::vector<pskv_batch> v;
   for (auto& b : in) {
@@ -831,6 +932,11 @@ int add_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
   int rc = use_device(s);
   if (rc) return rc;
   const bool device = (flags & PSKV_DEVICE) != 0;
+  if (!device && s->tune_inline) {
+    uint64_t total = 0;
+    for (const auto& b : v) total += b.n;
+    if (total <= (uint64_t)kInlineMax) return inline_add(s, v, total);
+  }
   bool host_verified = false, host_dense = false;
   if (!device) {
     std::vector<pskv_batch> staged;
@@ -891,6 +997,11 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
   int rc = use_device(s);
   if (rc) return rc;
   const bool device = (flags & PSKV_DEVICE) != 0;
+  if (!device && s->tune_inline) {
+    uint64_t total = 0;
+    for (const auto& b : v) total += b.n;
+    if (total <= (uint64_t)kInlineGetMax) return inline_get(s, v, total);
+  }
   std::vector<pskv_batch> dv = v;
   size_t out_off = 0;
   bool pinned = !device;
@@ -1048,6 +1159,8 @@ int pskv_shard_create_ex(int device, uint32_t key_begin, uint64_t key_end, int d
   if (const char* e = std::getenv("PSKV_NT")) s->tune_nt = std::atoi(e) != 0;
   if (const char* e = std::getenv("PSKV_NTP")) s->tune_ntp = std::atoi(e) != 0;
   if (const char* e = std::getenv("PSKV_PAGEABLE_DMA")) s->tune_pageable_dma = std::atoi(e) != 0;
+  if (const char* e = std::getenv("PSKV_INLINE")) s->tune_inline = std::atoi(e) != 0;
+  if (const char* e = std::getenv("PSKV_ISPIN")) s->tune_ispin = std::atoi(e) != 0;
   if (const char* e = std::getenv("PSKV_TILE_GRID")) {
     const int v = std::atoi(e);
     if (v >= 1 && v <= 65536) s->tune_tile_grid = (uint32_t)v;
@@ -1114,6 +1227,7 @@ int pskv_shard_destroy(pskv_shard* s) {
   if (s->rb_loff) (void)hipFree(s->rb_loff);
   if (s->rb_ent) (void)hipFree(s->rb_ent);
   if (s->hstage) (void)hipHostFree(s->hstage);
+  if (s->ireply) (void)hipHostFree(s->ireply);
   if (s->hstage_free) (void)hipEventDestroy(s->hstage_free);
   if (s->h2d_done) (void)hipEventDestroy(s->h2d_done);
   for (auto e : s->win_events) (void)hipEventDestroy(e);

@@ -906,3 +906,153 @@ def test_pinned_host_buffers_direct_dma(cuda, oracle_mod, mode, pageable_path, m
         for k, v in batches:
             ref.add(k, v)
         assert_bits_equal(outs["pinned"], ref.get(q), "pinned vs oracle")
+
+
+# ---------------------------------------------------------------- K8 inline
+# Small host messages (<= 256 keys per Add, <= 512 per Get) travel inside the
+# kernel arguments.  They are the reference's live traffic shape (one LR
+# sample's features per message, app/logistic_regression.cpp:411,490).
+
+def _small_messages(rng, kb, ke, count, max_n=256):
+    """Host messages of 0..max_n keys: duplicates, out-of-range keys on both
+    sides, the overflow sentinel 0xFFFFFFFF."""
+    out = []
+    for i in range(count):
+        n = int(rng.integers(0, max_n + 1)) if i % 5 else max_n
+        k = rng.integers(kb - 50, ke + 50, size=n).astype(np.uint32)
+        if n > 4 and i % 3 == 0:
+            k[: n // 4] = k[0]                   # a hot key, repeated
+        if n > 2 and i % 7 == 0:
+            k[-1] = 0xFFFFFFFF
+            k[-2] = int(rng.integers(0, 2**32))
+        out.append(k)
+    return out
+
+
+@pytest.mark.parametrize("dt", [np.int32, np.float32, np.float64])
+def test_inline_small_messages_assign(cuda, oracle_mod, dt, monkeypatch):
+    """K8 assign: last write wins within and across messages, missing keys 0,
+    overflow keys kept; the same message stream through the staged path
+    (PSKV_INLINE=0) gives the same bits."""
+    import parameter_server_amd as ps
+    from parameter_server_amd import _lib
+
+    rng = np.random.default_rng(808)
+    kb, ke = 1000, 1000 + 4096
+    msgs = _small_messages(rng, kb, ke, 120)
+    vals = [(rng.standard_normal(k.size) * 100).astype(dt) for k in msgs]
+    ref = oracle_mod.MapStorageRef(dt)
+    monkeypatch.setenv("PSKV_INLINE", "0")
+    staged = ps.Shard(kb, ke, dt, overflow_slots=64)
+    staged.set_timing(True)
+    monkeypatch.delenv("PSKV_INLINE")
+    try:
+        with ps.Shard(kb, ke, dt, overflow_slots=64) as sh:
+            sh.set_timing(True)
+            replies = []
+            for i, (k, v) in enumerate(zip(msgs, vals)):
+                sh.add(k, v)
+                staged.add(k, v)
+                ref.add(k, v)
+                if i % 10 == 9:                       # interleaved small Gets
+                    q = np.concatenate([k[:40], rng.integers(kb - 60, ke + 60, size=40)]).astype(np.uint32)
+                    replies.append((sh.get(q), staged.get(q), ref.get(q)))
+            q = np.concatenate([np.arange(kb - 60, ke + 60), [0xFFFFFFFF]]).astype(np.uint32)
+            big = sh.get(q)                             # > 512 keys: staged Get
+            assert sh.kernel_time(_lib.PSKV_K_INLINE_ADD)["launches"] == sum(1 for k in msgs if k.size)
+            assert sh.kernel_time(_lib.PSKV_K_INLINE_GET)["launches"] == len(replies)
+            sh.sync()
+        assert staged.kernel_time(_lib.PSKV_K_INLINE_ADD)["launches"] == 0
+        big_staged = staged.get(q)
+    finally:
+        staged.close()
+    for a, b, w in replies:
+        assert_bits_equal(a, w, "inline get")
+        assert_bits_equal(b, w, "staged get")
+    assert_bits_equal(big, ref.get(q), "full read after inline adds")
+    assert_bits_equal(big_staged, ref.get(q), "full read after staged adds")
+
+
+@pytest.mark.parametrize("dt", [np.int32, np.float32, np.float64])
+def test_inline_accumulate_sequential_bits(cuda, dt):
+    """K8 accumulate: the first occurrence of a key adds every occurrence in
+    index order, so the result equals sequential accumulation in the value
+    dtype BIT FOR BIT (np.add.at), overflow keys included."""
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(909)
+    kb, ke = 0, 2048
+    msgs = _small_messages(rng, kb, ke, 80)
+    want = np.zeros(ke - kb, dt)
+    want_ovf = {}
+    with ps.Shard(kb, ke, dt, mode="accumulate", overflow_slots=64) as sh:
+        for k in msgs:
+            v = (rng.integers(-2**31, 2**31 - 1, size=k.size, dtype=np.int64).astype(np.int32)
+                 if dt is np.int32 else rng.standard_normal(k.size).astype(dt))
+            sh.add(k, v)
+            inr = k < ke
+            np.add.at(want, k[inr].astype(np.int64) - kb, v[inr])
+            for key, val in zip(k[~inr], v[~inr]):
+                with np.errstate(over="ignore"):
+                    want_ovf[int(key)] = dt(want_ovf.get(int(key), dt(0)) + val)
+        got = sh.get(np.arange(kb, ke, dtype=np.uint32))
+        ok = np.array(sorted(want_ovf), np.uint32)
+        got_ovf = sh.get(ok)
+    assert_bits_equal(got, want, "inline accumulate (dense)")
+    assert_bits_equal(got_ovf, np.array([want_ovf[int(x)] for x in ok], dt), "inline accumulate (overflow)")
+
+
+@pytest.mark.parametrize("n", [255, 256, 257, 511, 512, 513])
+def test_inline_size_boundaries(cuda, oracle_mod, n):
+    """Messages at and beyond the inline limits (256 keys per Add, 512 per
+    Get; grouped calls count their batches together) agree with the oracle."""
+    import parameter_server_amd as ps
+    from parameter_server_amd import _lib
+
+    rng = np.random.default_rng(n)
+    ref = oracle_mod.MapStorageRef(np.float64)
+    with ps.Shard(0, 3000, np.float64) as sh:
+        sh.set_timing(True)
+        k = rng.integers(0, 3100, size=n).astype(np.uint32)
+        v = rng.standard_normal(n)
+        sh.add(k, v)
+        ref.add(k, v)
+        # grouped: three batches, n keys in all
+        parts = np.split(np.arange(n), [n // 3, 2 * n // 3])
+        k2 = rng.integers(0, 3100, size=n).astype(np.uint32)
+        v2 = rng.standard_normal(n)
+        sh.add_grouped([(k2[p], v2[p]) for p in parts])
+        for p in parts:
+            ref.add(k2[p], v2[p])
+        outs = [np.empty(p.size) for p in parts]
+        sh.get_grouped([(k2[p], o) for p, o in zip(parts, outs)])
+        got = sh.get(k)
+        adds = sh.kernel_time(_lib.PSKV_K_INLINE_ADD)["launches"]
+        gets = sh.kernel_time(_lib.PSKV_K_INLINE_GET)["launches"]
+    assert adds == (2 if n <= 256 else 0)
+    assert gets == (2 if n <= 512 else 0)
+    assert_bits_equal(got, ref.get(k), "single")
+    for p, o in zip(parts, outs):
+        assert_bits_equal(o, ref.get(k2[p]), "grouped")
+
+
+@pytest.mark.parametrize("spin", ["1", "0"])
+def test_inline_get_reply_paths(cuda, oracle_mod, spin, monkeypatch):
+    """The inline Get's two completion forms: the polled sequence word the
+    kernel publishes after its reply (default) and a plain stream wait
+    (PSKV_ISPIN=0); with timing on, the polled form is bypassed too."""
+    import parameter_server_amd as ps
+
+    monkeypatch.setenv("PSKV_ISPIN", spin)
+    rng = np.random.default_rng(11)
+    ref = oracle_mod.MapStorageRef(np.float32)
+    with ps.Shard(0, 1 << 16, np.float32) as sh:
+        for i in range(300):
+            k = rng.integers(0, 1 << 17, size=int(rng.integers(1, 300))).astype(np.uint32)
+            v = rng.standard_normal(k.size).astype(np.float32)
+            sh.add(k, v)
+            ref.add(k, v)
+            if i == 150:
+                sh.set_timing(True)
+            q = rng.integers(0, 1 << 17, size=int(rng.integers(1, 513))).astype(np.uint32)
+            assert_bits_equal(sh.get(q), ref.get(q), f"get {i}")

@@ -1,0 +1,84 @@
+// small_latency.cpp — per-call latency of small host messages through the C ABI
+// (the reference's live traffic: one LR sample's keys per message,
+// app/logistic_regression.cpp:411,490).  Compares the K8 inline path (keys and
+// values in the kernel arguments, reply written to page-locked memory and
+// published by a polled sequence word) with the same path waiting on the stream
+// (PSKV_ISPIN=0) and with the staged path (PSKV_INLINE=0: H2D / D2H DMAs).
+//   g++ -O2 -std=c++11 -I include tools/micro/small_latency.cpp \
+//       -L parameter_server_amd -lpskv -Wl,-rpath,$PWD/parameter_server_amd -o /tmp/small_latency
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "pskv.h"
+
+static double now_us() {
+  using namespace std::chrono;
+  return duration<double, std::micro>(steady_clock::now().time_since_epoch()).count();
+}
+
+static void die(int rc, const char* what) {
+  if (rc) {
+    std::fprintf(stderr, "%s: %d %s\n", what, rc, pskv_last_error());
+    std::exit(1);
+  }
+}
+
+int main() {
+  const int sizes[] = {1, 16, 64, 256};
+  const int reps = 2000;
+  std::mt19937 rng(7);
+  std::printf("%-10s %6s %10s %10s %12s %12s\n", "path", "keys", "add_us", "get_us", "add+get_us",
+              "get_only_us");
+  // variants: inline with the polled reply, inline with a stream wait
+  // (PSKV_ISPIN=0), staged (PSKV_INLINE=0)
+  const char* names[] = {"inline", "inline-sync", "staged"};
+  for (int var = 0; var < 3; ++var) {
+    setenv("PSKV_INLINE", var < 2 ? "1" : "0", 1);
+    setenv("PSKV_ISPIN", var == 0 ? "1" : "0", 1);
+    pskv_shard* s = nullptr;
+    die(pskv_shard_create(0, 0, 1000000, PSKV_F64, PSKV_ASSIGN, &s), "create");
+    for (int n : sizes) {
+      std::vector<uint32_t> k(n);
+      std::vector<double> v(n), out(n);
+      std::vector<double> ta, tg, tb, to;
+      for (int r = 0; r < reps + 50; ++r) {
+        for (int i = 0; i < n; ++i) {
+          k[i] = rng() % 1000000;
+          v[i] = (double)r + i;
+        }
+        std::sort(k.begin(), k.end());  // LR pushes [0] + sorted feature ids
+        const double t0 = now_us();
+        die(pskv_add(s, k.data(), v.data(), n, PSKV_HOST), "add");
+        const double t1 = now_us();
+        die(pskv_get(s, k.data(), n, out.data(), PSKV_HOST), "get");
+        const double t2 = now_us();
+        die(pskv_get(s, k.data(), n, out.data(), PSKV_HOST), "get");  // nothing queued before it
+        const double t3 = now_us();
+        if (r >= 50) {
+          ta.push_back(t1 - t0);
+          tg.push_back(t2 - t1);
+          tb.push_back(t2 - t0);
+          to.push_back(t3 - t2);
+        }
+        for (int i = 0; i < n; ++i)  // read-your-writes (last duplicate wins)
+          if (i + 1 == n || k[i] != k[i + 1])
+            if (out[i] != v[i]) {
+              std::fprintf(stderr, "mismatch at %d\n", i);
+              return 1;
+            }
+      }
+      auto med = [](std::vector<double>& x) {
+        std::nth_element(x.begin(), x.begin() + x.size() / 2, x.end());
+        return x[x.size() / 2];
+      };
+      std::printf("%-10s %6d %10.2f %10.2f %12.2f %12.2f\n", names[var], n, med(ta), med(tg), med(tb),
+                  med(to));
+    }
+    die(pskv_shard_destroy(s), "destroy");
+  }
+  return 0;
+}
