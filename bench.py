@@ -60,7 +60,8 @@ def parse():
     p.add_argument("--batch-keys", type=int, default=1_000_000)
     p.add_argument("--sets", type=int, default=4, help="window sets rotated over the steps")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--no-extra", action="store_true", help="skip the zipf / e2e side measurements")
+    p.add_argument("--no-extra", action="store_true", help="skip the side measurements (e2e, f64, accumulate)")
+    p.add_argument("--no-zipf", action="store_true", help="skip the cfg-3 sparse (Zipf) measurement")
     p.add_argument("--cpu-batches", type=int, default=64,
                    help="1M-key windows in the 1-thread CPU baseline sample (~10 s)")
     return p.parse_args()
@@ -296,32 +297,11 @@ def side_measurements(dev, B):
 
     out = {}
     stream = torch.cuda.current_stream()
-    # cfg 3: Zipf(0.99) over 1e8 keys, unsorted, 8 x 1M pushes then pulls
+    # cfg 3 pushes: Zipf(0.99) over 1e8 keys, unsorted, 8 x 1M
     space, J = 100_000_000, 8
     zb = workload.zipf_batches(J, space, batch=B, device=dev)
-    zo = [torch.empty_like(v) for _, v in zb]
-    with ps.Shard(0, space, np.float32) as sh:
-        sh.set_stream(stream.cuda_stream)
-        for _ in range(2):
-            sh.add_grouped(zb)
-            sh.get_grouped([(k, o) for (k, _), o in zip(zb, zo)])
-        torch.cuda.synchronize()
-        reps = 5
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            sh.add_grouped(zb)
-            sh.get_grouped([(k, o) for (k, _), o in zip(zb, zo)])
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        uniq = int(torch.unique(zb[0][0]).numel())
-        u_all = int(torch.unique(torch.cat([k for k, _ in zb])).numel())
-        sh.set_stream(None)
-    add_b, get_b = step_bytes(J * B, u_all, J * B)
-    out["zipf"] = {"workload": "cfg 3: Zipf(0.99) over 1e8 keys, 8 x 1M unsorted pushes then pulls, assign "
-                               "(general path K5: LDS dedup + bucket-sorted super-chunks, no global atomics)",
-                   "GB/s": (add_b + get_b) * reps / dt / 1e9, "ms_per_step": dt / reps * 1e3,
-                   "unique_keys_per_batch": uniq, "distinct_keys_per_step": u_all,
-                   "cpu_map_storage": _zipf_cpu_sample(zb[:2], B)}
+    u_all = int(torch.unique(torch.cat([k for k, _ in zb])).numel())
+    reps = 5
     # cfg 3 in accumulate mode (the north star's LDS segmented-sum path): K5,
     # per-super-chunk LDS sums, key buckets, one owner workgroup per bucket
     with ps.Shard(0, space, np.float32, mode="accumulate") as sh:
@@ -339,7 +319,7 @@ def side_measurements(dev, B):
     out["zipf_accumulate_add"] = {"workload": "cfg 3 pushes (8 x 1M Zipf(0.99), unsorted), accumulate mode "
                                               "(K5: LDS super-chunk sums + key buckets, no global atomics)",
                                   "GB/s": acc_b * reps / dt / 1e9, "ms_per_call": dt / reps * 1e3}
-    del zb, zo
+    del zb
     # cfg 2 windows in accumulate mode (the north star's scatter-accumulate):
     # sorted hint -> K6 density proof + K7 one RMW per key (sums in call order)
     J = 64
@@ -492,6 +472,87 @@ def cold_get_step(shard, adds, bases, J, B, dev, steps):
             "k_assign_group_ms": a["total_ms"] / max(1, a["launches"])}
 
 
+def zipf_sparse(rank, world, dev, lo, hi, B, steps, J=8):
+    """cfg 3 on every rank: J x 1M unsorted Zipf(0.99) pushes then the same
+    pulls per step, assign mode, over this rank's range shard (N = 1: the 1e8-key
+    cfg-3 shard; N > 1: the rank's 1e9/N range, its own key permutation, so the
+    sparse path is weak-scaled like the dense one).  Barrier + synchronize around
+    exactly `steps` steps, max over ranks; bytes as SURVEY §8d with u = distinct
+    keys pushed in the step.  The K5 (Add) and K1 (Get) durations come from an
+    evented second pass."""
+    import torch
+
+    import parameter_server_amd as ps
+    from parameter_server_amd import _lib, workload
+
+    space = hi - lo
+    zb = workload.zipf_batches(J, space, batch=B, device=dev, perm_seed=7 + rank, seed=42 + 1000 * rank,
+                               lo=lo)
+    zo = [torch.empty_like(v) for _, v in zb]
+    uniq = int(torch.unique(zb[0][0]).numel())
+    u_all = int(torch.unique(torch.cat([k for k, _ in zb])).numel())
+    with ps.Shard(lo, hi, np.float32, device=dev.index) as sh:
+        sh.set_stream(torch.cuda.current_stream().cuda_stream)
+        adds = sh.prepare(zb)
+        gets = sh.prepare([(k, o) for (k, _), o in zip(zb, zo)], is_get=True)
+        for _ in range(2):
+            sh.add_grouped(adds)
+            sh.get_grouped(gets)
+        torch.cuda.synchronize()
+        # self-check: every key in the tail of the LAST batch was last written
+        # there (a later write would be later in that tail), so it reads its
+        # last occurrence's value
+        last = {}
+        kk, vv = zb[-1][0].cpu().numpy(), zb[-1][1].cpu().numpy()
+        last.update(zip(kk[-4096:].tolist(), vv[-4096:].tolist()))
+        probe = torch.tensor(list(last), dtype=torch.int32, device=dev)
+        got = sh.get(probe).cpu().numpy()
+        assert np.array_equal(got, np.array([last[int(x)] for x in probe.cpu().numpy()], np.float32)), \
+            "zipf self-check failed"
+        barrier(world)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            sh.add_grouped(adds)
+            sh.get_grouped(gets)
+        torch.cuda.synchronize()
+        t_own = time.perf_counter() - t0
+        barrier(world)
+        elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
+        sh.set_timing(True, kernels=[_lib.PSKV_K_RADIX, _lib.PSKV_K_GATHER])
+        for _ in range(steps):
+            sh.add_grouped(adds)
+            sh.get_grouped(gets)
+        torch.cuda.synchronize()
+        kt = {n: sh.kernel_time(k) for k, n in ((_lib.PSKV_K_RADIX, "k_rb_bin+k_rb_resolve (K5 Add)"),
+                                                 (_lib.PSKV_K_GATHER, "k_gather (K1 Get)"))}
+        sh.set_timing(False)
+        sh.set_stream(None)
+    add_b, get_b = step_bytes(J * B, u_all, J * B)
+    own = (add_b + get_b) * steps
+    total = sum_over_ranks(float(own), world, dev)
+    value = total / elapsed / 1e9
+    kernels = {}
+    for n, t in kt.items():
+        ms = t["total_ms"] / max(1, t["launches"])
+        b = add_b if n.startswith("k_rb") else get_b
+        kernels[n] = {"avg_ms": ms, "algorithmic_bytes": b, "GB/s": b / (ms * 1e-3) / 1e9,
+                      "frac": b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    return {
+        "workload": f"cfg 3 sparse: {J} x {B} unsorted Zipf(0.99) pushes then the same pulls per step per GPU "
+                    f"over a {space:.3g}-key range shard, assign mode (K5 key buckets + K1 gather)",
+        "value": value, "unit": "GB/s", "n_gpus": world, "steps": steps, "ms_per_step": elapsed / steps * 1e3,
+        "per_gpu": {"mean_GB/s": value / world, "min_GB/s": -max_over_ranks(-own / t_own / 1e9, world, dev),
+                    "max_GB/s": max_over_ranks(own / t_own / 1e9, world, dev)},
+        "roofline": {"bound": "hbm", "achieved": value / world, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": value / world / HBM_PEAK_GBS,
+                     "note": "algorithmic bytes (SURVEY §8d, u = distinct keys) per GPU per second; "
+                             "random single-value accesses fetch whole lines, so the line traffic is higher"},
+        "kernels": kernels,
+        "unique_keys_per_batch": uniq, "distinct_keys_per_step": u_all,
+        "bytes_per_step_per_gpu": add_b + get_b}, zb
+
+
 def fixed_set_step(shard, adds, gets, bases, J, B, steps):
     """The round-1 headline form: the SAME window set every step.  The 48
     distinct windows (192 MB of parameters) then stay largely resident in the
@@ -611,6 +672,9 @@ def main():
             ktimes[name] = {"launches": t["launches"], "avg_ms": t["total_ms"] / t["launches"],
                             "keys_per_launch": t["elements"] / t["launches"]}
     shard.sync()
+    zipf_res = None
+    if not args.no_zipf:
+        zipf_res, zb = zipf_sparse(rank, world, dev, lo, hi, B, args.steps)
     # per-step bytes, averaged over the rotation as the steps ran it
     u_push = sum(plans[i % R][5] for i in range(args.steps)) / args.steps  # distinct keys pushed per step
     add_b, get_b = step_bytes(J * B, u_push, J * B)
@@ -674,8 +738,14 @@ def main():
         # bytes over its own time, min / max over ranks
         "per_gpu": per_gpu,
     }
+    if zipf_res is not None:
+        result["zipf_sparse"] = zipf_res
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(bases, B, args.cpu_batches)
+        if zipf_res is not None:  # cfg 3's own CPU baseline: the same Zipf batches
+            result["cpu_baseline"]["zipf"] = _zipf_cpu_sample(zb[:2], B)
+    if zipf_res is not None:
+        del zb
     if rank == 0 and world == 1 and not args.no_extra:
         cold = cold_get_step(shard, adds, bases, J, B, dev, args.steps)
         fixed = fixed_set_step(shard, adds, gets, bases, J, B, args.steps)

@@ -45,9 +45,9 @@ def dense_batches(n_batches, key_space, batch=MILLION, device="cuda:0", dtype=No
 
 
 def zipf_batches(n_batches, key_space, batch=MILLION, s=0.99, device="cuda:0", dtype=None,
-                 perm_seed=7, seed=42):
+                 perm_seed=7, seed=42, lo=0):
     """cfg 3: exact discrete Zipf(s) ranks via an inverse CDF, mapped to keys
-    by a seeded permutation; order unsorted."""
+    lo + perm[rank] by a seeded permutation of [0, key_space); order unsorted."""
     import torch
 
     dtype = dtype or torch.float32
@@ -64,7 +64,7 @@ def zipf_batches(n_batches, key_space, batch=MILLION, s=0.99, device="cuda:0", d
         g.manual_seed(seed + j)
         u = torch.rand(batch, generator=g, device=device, dtype=torch.float64)
         ranks = torch.searchsorted(cdf, u).clamp_(max=key_space - 1)
-        keys = perm[ranks].to(torch.int32)
+        keys = (perm[ranks] + lo).to(torch.int32)
         if dtype in (torch.float32, torch.float64):
             vals = torch.rand(batch, generator=g, device=device, dtype=dtype) * 2 - 1
         else:
