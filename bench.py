@@ -431,6 +431,55 @@ def dense_f64_step(batches, bases, J, B, dev, steps):
             "GB/s": step_b * steps / dt / 1e9, "ms_per_step": dt / steps * 1e3}
 
 
+def dense_accumulate_step(plans, J, B, dev, steps):
+    """The headline step in ACCUMULATE mode (the north star's gradient push:
+    param[k] += v, then the pull of the updated parameters), over the same
+    rotating window sets: K6 density proof + K7 one read-modify-write per key
+    (sums in call order) + K1.  Bytes: Add n*(4+V) + 2*u*V (the RMW), Get
+    q*(4+2V).  A self-check compares one window with a float64 reference of
+    the sequential sums before timing."""
+    import torch
+
+    import parameter_server_amd as ps
+
+    R = len(plans)
+    outs = [torch.empty(B, dtype=torch.float32, device=dev) for _ in range(J)]
+    with ps.Shard(0, 100_000_000, np.float32, mode="accumulate") as sh:
+        sh.set_stream(torch.cuda.current_stream().cuda_stream)
+        prepared = [(sh.prepare(p[1]), sh.prepare([(k, o) for (k, _), o in zip(p[1], outs)], is_get=True))
+                    for p in plans]
+        # self-check on set 0, from a zeroed shard: window j's pulled values
+        # equal the sum of every push of that window in call order
+        sh.add_grouped(prepared[0][0], sorted_hint=True)
+        sh.get_grouped(prepared[0][1])
+        torch.cuda.synchronize()
+        bases0, batches0 = plans[0][0], plans[0][1]
+        b0 = int(bases0[0])
+        want = torch.zeros(B, dtype=torch.float32, device=dev)
+        for (k, v), b in zip(batches0, bases0):
+            if int(b) == b0:
+                want += v
+        assert torch.equal(outs[0], want), "accumulate self-check failed"
+        for i in range(2):
+            sh.add_grouped(prepared[i % R][0], sorted_hint=True)
+            sh.get_grouped(prepared[i % R][1])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            sh.add_grouped(prepared[i % R][0], sorted_hint=True)
+            sh.get_grouped(prepared[i % R][1])
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        sh.set_stream(None)
+    tot = 0
+    for i in range(steps):
+        u = len(set(int(b) for b in plans[i % R][0])) * B
+        tot += J * B * (4 + V) + 2 * u * V + J * B * (4 + 2 * V)
+    return {"workload": f"cfg 2 step in accumulate mode (gradient push += then pull), {J} x {B} windows, "
+                        f"{R} rotating window sets (K6 + K7 + K1)",
+            "GB/s": tot / dt / 1e9, "ms_per_step": dt / steps * 1e3}
+
+
 def cold_get_step(shard, adds, bases, J, B, dev, steps):
     """The headline step pulls the windows it just pushed: 48 distinct 4 MB
     windows = 192 MB of parameters, which the Infinity Cache (256 MB) can still
@@ -754,6 +803,7 @@ def main():
         result["extra"]["cold_get_step"] = cold
         result["extra"]["fixed_set_step"] = fixed
         result["extra"]["dense_f64_step"] = dense_f64_step(batches, bases, J, B, dev, args.steps)
+        result["extra"]["dense_accumulate_step"] = dense_accumulate_step(plans, J, B, dev, args.steps)
     shard.close()
     if rank == 0:
         json_out.write(json.dumps(result) + "\n")

@@ -61,15 +61,6 @@ __device__ __forceinline__ void st16(void* p, u32x4 v) {
     *reinterpret_cast<u32x4*>(p) = v;
 }
 
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-template <bool NT>
-__device__ __forceinline__ void ld8_keys(const uint32_t* p, uint32_t (&k)[2]) {
-  const u32x2 t = NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(p))
-                     : *reinterpret_cast<const u32x2*>(p);
-  k[0] = t.x;
-  k[1] = t.y;
-}
-
 // Two 8-byte values as one 16-byte access.  Streams of 8-byte values go two
 // per lane (a wave covers 1 KiB contiguously per instruction) rather than four
 // per lane as two 16-byte accesses 32 bytes apart (each instruction then
@@ -229,17 +220,49 @@ __global__ __launch_bounds__(kBlock) void k_gather(GroupArgs ga, DenseView d, Ov
   const int tid = threadIdx.x;
   if constexpr (sizeof(VT) == 8) {
     if (VEC && base + CH <= n) {
-      // two keys per lane per step (see Vec2x8): 8-byte key loads, 16-byte
-      // value loads and stores, every instruction one contiguous span
-      constexpr int UU = 2 * U;
-      uint32_t k[UU][2];
+      // 16-byte key loads, four keys per lane (a wave's 256 elements are
+      // contiguous).  When the wave's 256 keys are ONE contiguous in-range run
+      // on an even offset (a dense pull; wave-uniform test), the 8-byte values
+      // move as PAIRS: lane l takes elements 2l, 2l+1 and 128+2l, 128+2l+1 of
+      // the wave's span, so every value load and store instruction covers
+      // 1 KiB contiguously.  Otherwise each lane gathers its own four keys.
+      using T = unsigned long long;
+      const int lane = tid & 63;
+      uint32_t k[U][4];
 #pragma unroll
-      for (int u = 0; u < UU; ++u) ld8_keys<NT>(keys + base + (uint64_t)(u * kBlock + tid) * 2, k[u]);
-      VT v[UU][2];
+      for (int u = 0; u < U; ++u)
+        Vec4<uint32_t>::load<NT>(keys + base + (uint64_t)(u * kBlock + tid) * 4, k[u]);
+      T va[U][2], vb[U][2];
+      bool dense[U];
 #pragma unroll
-      for (int u = 0; u < UU; ++u) gather2(d, o, k[u], v[u]);
+      for (int u = 0; u < U; ++u) {
+        const uint32_t k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)k[u][0]);
+        const uint32_t e0 = k0 + 4u * (uint32_t)lane;
+        const bool ok = (k[u][0] == e0) & (k[u][1] == e0 + 1u) & (k[u][2] == e0 + 2u) & (k[u][3] == e0 + 3u);
+        const uint32_t off = k0 - d.key_begin;
+        dense[u] = __all(ok) && (off & 1u) == 0u && (uint64_t)off + 255u < d.range;  // wave-uniform
+        if (dense[u]) {
+          const T* p = reinterpret_cast<const T*>(d.param) + off;
+          Vec2x8::load(p + 2 * lane, va[u]);
+          Vec2x8::load(p + 128 + 2 * lane, vb[u]);
+        } else {
+          const uint32_t k01[2] = {k[u][0], k[u][1]}, k23[2] = {k[u][2], k[u][3]};
+          gather2(d, o, k01, va[u]);
+          gather2(d, o, k23, vb[u]);
+        }
+      }
 #pragma unroll
-      for (int u = 0; u < UU; ++u) Vec2x8::store<NT>(out + base + (uint64_t)(u * kBlock + tid) * 2, v[u]);
+      for (int u = 0; u < U; ++u) {
+        if (dense[u]) {
+          T* w = out + base + (uint64_t)(u * kBlock + (tid & ~63)) * 4;  // the wave's span
+          Vec2x8::store<NT>(w + 2 * lane, va[u]);
+          Vec2x8::store<NT>(w + 128 + 2 * lane, vb[u]);
+        } else {
+          T* w = out + base + (uint64_t)(u * kBlock + tid) * 4;  // this lane's four elements
+          Vec2x8::store<NT>(w, va[u]);
+          Vec2x8::store<NT>(w + 2, vb[u]);
+        }
+      }
       return;
     }
   }
@@ -468,30 +491,38 @@ __device__ __forceinline__ bool dense_chunk(const GroupArgs& ga, const DenseView
       bad |= (k[0] != k0) | (k[1] != k0 + 1u) | (k[2] != k0 + 2u) | (k[3] != k0 + 3u);
     }
   } else if (sizeof(VT) == 8 && VEC && end - base == CH) {
-    // 8-byte values two keys per lane per step (see Vec2x8)
+    // 8-byte values: keys four per lane (16-byte loads; each lane checks its
+    // own four against first + index), values and parameters as PAIRS over the
+    // wave's 256-element span (lane l: elements 2l, 2l+1 and 128+2l, 128+2l+1),
+    // so every access instruction covers one contiguous span
     using T = unsigned long long;
-    constexpr int UU = 2 * U;
-    uint32_t k[UU][2];
-    T v[UU][2];
+    uint32_t k[U][4];
+    T va[U][2], vb[U][2];
 #pragma unroll
-    for (int u = 0; u < UU; ++u) {
-      const uint64_t i = base + (uint64_t)(u * kBlock + tid) * 2;
-      ld8_keys<NT>(keys + i, k[u]);
-      Vec2x8::load<NT>(reinterpret_cast<const T*>(vals) + i, v[u]);
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = base + (uint64_t)(u * kBlock + tid) * 4;
+      const uint64_t ew = base + (uint64_t)(u * kBlock + (tid & ~63)) * 4;
+      Vec4<uint32_t>::load<NT>(keys + i, k[u]);
+      Vec2x8::load<NT>(reinterpret_cast<const T*>(vals) + ew + 2 * lane, va[u]);
+      Vec2x8::load<NT>(reinterpret_cast<const T*>(vals) + ew + 128 + 2 * lane, vb[u]);
     }
     T* __restrict__ p8 = reinterpret_cast<T*>(param);
 #pragma unroll
-    for (int u = 0; u < UU; ++u) {
-      const uint64_t i = base + (uint64_t)(u * kBlock + tid) * 2;
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = base + (uint64_t)(u * kBlock + tid) * 4;
       const uint32_t k0 = first + (uint32_t)i;
-      bad |= (k[u][0] != k0) | (k[u][1] != k0 + 1u);
-      const uint32_t off0 = k0 - d.key_begin;
-      if (later == 0 && (off0 & 1u) == 0u) {
-        Vec2x8::store<NTP>(p8 + off0, v[u]);
+      bad |= (k[u][0] != k0) | (k[u][1] != k0 + 1u) | (k[u][2] != k0 + 2u) | (k[u][3] != k0 + 3u);
+      const uint32_t ka = first + (uint32_t)(base + (uint64_t)(u * kBlock + (tid & ~63)) * 4) + 2u * lane;
+      const uint32_t offa = ka - d.key_begin;
+      if (later == 0 && (offa & 1u) == 0u) {
+        Vec2x8::store<NTP>(p8 + offa, va[u]);
+        Vec2x8::store<NTP>(p8 + offa + 128, vb[u]);
       } else {
 #pragma unroll
-        for (int e = 0; e < 2; ++e)
-          if (!shadowed(k0 + e)) p8[off0 + e] = v[u][e];
+        for (int e = 0; e < 2; ++e) {
+          if (!shadowed(ka + e)) p8[offa + e] = va[u][e];
+          if (!shadowed(ka + 128u + e)) p8[offa + 128 + e] = vb[u][e];
+        }
       }
     }
   } else if (VEC && end - base == CH) {
