@@ -47,6 +47,13 @@ def _worker(rank, world, port, q):
                 sample = np.array([b, b + 1, b + B // 2, b + B - 1], dtype=np.uint32)
                 sl = oracle.range_slice_ref(ranges, sample)
                 assert [s for s, _ in sl] == [r], (r, b, sl)
+        # every window set the bench rotates over routes to its rank too, and
+        # the sets differ (distinct seeds)
+        for r in (1, 3):
+            _, lo_r, hi_r, bases_r = bench.plan_rank(rank, world, J, B, r)
+            assert (lo_r, hi_r) == (lo, hi)
+            assert all(lo <= int(b) and int(b) + B <= hi for b in bases_r)
+            assert list(bases_r) != list(bases)
         # reductions as bench.py does them (device = cpu under gloo)
         t = bench.max_over_ranks(float(rank + 1), world, torch.device("cpu"))
         u = bench.sum_over_ranks(10.0, world, torch.device("cpu"))

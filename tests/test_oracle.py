@@ -6,6 +6,7 @@ import os
 import numpy as np
 import pytest
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 DT = {"int32": np.int32, "float32": np.float32, "float64": np.float64}
 
@@ -101,3 +102,25 @@ def test_oracle_rejects_mismatched_sizes(oracle_mod):
     ref = oracle_mod.MapStorageRef(np.float32)
     with pytest.raises(ValueError):
         ref.add(np.arange(3, dtype=np.uint32), np.zeros(2, np.float32))
+
+
+def test_bench_step_bytes_and_single_gpu_sets():
+    """bench.py's algorithmic byte accounting (Add n*(4+V) + u*V,
+    Get q*(4+2V)) and the N = 1 window sets: 1M-aligned bases inside the 1e8-key
+    shard, set 0 on the config's seed 42, the other sets on distinct seeds."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import bench
+    from parameter_server_amd import workload
+
+    add, get = bench.step_bytes(64_000_000, 48_000_000, 64_000_000)
+    assert add == 64_000_000 * 8 + 48_000_000 * 4 and get == 64_000_000 * 12
+    seen = []
+    for r in range(4):
+        ks, lo, hi, bases = bench.plan_rank(0, 1, 64, 1_000_000, r)
+        assert (ks, lo, hi) == (100_000_000, 0, 100_000_000)
+        assert all(b % 1_000_000 == 0 and 0 <= b <= 99_000_000 for b in bases)
+        seen.append(tuple(int(b) for b in bases))
+    assert len(set(seen)) == 4
+    assert seen[0] == tuple(int(b) for b in workload.dense_bases(64, 100_000_000, 1_000_000, seed=42))
