@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "ps/consistency.hpp"
+#include "ps/consistent_hashing_partition_manager.hpp"
 #include "ps/hip_storage.hpp"
 #include "ps/range_partition_manager.hpp"
 #include "ps/server_thread.hpp"
@@ -35,15 +36,17 @@ enum class ModelType { SSP, BSP, ASP };       // driver/engine.hpp:24
 
 using CpuStorageMaker = std::function<std::unique_ptr<AbstractStorage>(StorageType)>;
 
-// The storage of the i-th server of `map` (server order = range order).
+using KeyRange = std::pair<uint64_t, uint64_t>;  // [begin, end), end <= 2^32
+
+// The storage of the i-th server, owning key range r (server order = the
+// partition manager's server order).
 template <typename Val>
-std::unique_ptr<AbstractStorage> MakeStorage(StorageType type, const RangeShardMap& map, size_t i,
+std::unique_ptr<AbstractStorage> MakeStorage(StorageType type, const KeyRange& r, size_t i,
                                              int mode = PSKV_ASSIGN,
                                              const CpuStorageMaker& cpu = nullptr) {
   if (type == StorageType::Hip) {
     const int ndev = pskv_device_count();
     PS_CHECK(ndev > 0);
-    const auto r = map.GetRange(i);
     return std::unique_ptr<AbstractStorage>(
         new HipStorage<Val>((int)(i % (size_t)ndev), (uint32_t)r.first, r.second, mode));
   }
@@ -69,9 +72,27 @@ inline std::unique_ptr<AbstractModel> MakeModel(ModelType type, uint32_t model_i
   }
 }
 
-// Engine::CreateTable for a group of server threads, one per range of `map`
-// (threads[i] serves map range i).  Returns the storages (still owned by the
-// models) in server order, for inspection.
+// Engine::CreateTable for a group of server threads: threads[i] gets a storage
+// owning ranges[i] and a consistency model.  Returns the storages (still owned
+// by the models) in server order, for inspection.
+template <typename Val>
+std::vector<AbstractStorage*> CreateTable(std::vector<std::unique_ptr<ServerThread>>& threads,
+                                          const std::vector<KeyRange>& ranges, uint32_t model_id,
+                                          ModelType model_type, StorageType storage_type,
+                                          int staleness, ReplyQueue* replies,
+                                          int mode = PSKV_ASSIGN,
+                                          const CpuStorageMaker& cpu = nullptr) {
+  PS_CHECK(threads.size() == ranges.size());
+  std::vector<AbstractStorage*> out;
+  for (size_t i = 0; i < threads.size(); ++i) {
+    auto st = MakeStorage<Val>(storage_type, ranges[i], i, mode, cpu);
+    out.push_back(st.get());
+    threads[i]->RegisterModel(model_id, MakeModel(model_type, model_id, std::move(st), staleness, replies));
+  }
+  return out;
+}
+
+// Range partitioning (base/range_partition_manager.hpp): server i owns map range i.
 template <typename Val>
 std::vector<AbstractStorage*> CreateTable(std::vector<std::unique_ptr<ServerThread>>& threads,
                                           const RangeShardMap& map, uint32_t model_id,
@@ -80,13 +101,26 @@ std::vector<AbstractStorage*> CreateTable(std::vector<std::unique_ptr<ServerThre
                                           int mode = PSKV_ASSIGN,
                                           const CpuStorageMaker& cpu = nullptr) {
   PS_CHECK(threads.size() == map.GetNumServers());
-  std::vector<AbstractStorage*> out;
-  for (size_t i = 0; i < threads.size(); ++i) {
-    auto st = MakeStorage<Val>(storage_type, map, i, mode, cpu);
-    out.push_back(st.get());
-    threads[i]->RegisterModel(model_id, MakeModel(model_type, model_id, std::move(st), staleness, replies));
-  }
-  return out;
+  std::vector<KeyRange> ranges;
+  for (size_t i = 0; i < threads.size(); ++i) ranges.push_back(map.GetRange(i));
+  return CreateTable<Val>(threads, ranges, model_id, model_type, storage_type, staleness, replies, mode,
+                          cpu);
+}
+
+// Consistent hashing (the reference default, driver/engine.hpp:143-150): any
+// server may receive any key below key_end, so every storage covers
+// [0, key_end).
+template <typename Val>
+std::vector<AbstractStorage*> CreateTable(std::vector<std::unique_ptr<ServerThread>>& threads,
+                                          const ConsistentHashShardMap& map, uint64_t key_end,
+                                          uint32_t model_id, ModelType model_type,
+                                          StorageType storage_type, int staleness, ReplyQueue* replies,
+                                          int mode = PSKV_ASSIGN,
+                                          const CpuStorageMaker& cpu = nullptr) {
+  PS_CHECK(threads.size() == map.GetNumServers());
+  std::vector<KeyRange> ranges(threads.size(), KeyRange(0, key_end));
+  return CreateTable<Val>(threads, ranges, model_id, model_type, storage_type, staleness, replies, mode,
+                          cpu);
 }
 
 }  // namespace csci5570

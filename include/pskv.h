@@ -13,6 +13,8 @@
  *   VectorStorage<Val>()     server/vector_storage.hpp:14        pskv_shard_create(..., PSKV_ASSIGN)
  *   ~AbstractStorage (missing in the reference) pskv_shard_destroy
  *   RangePartitionManager::Slice base/range_partition_manager.hpp:19-46,48-77  pskv_range_slice
+ *   ConsistentHashingPartitionManager::JumpConsistentHash
+ *                     base/consistent_hashing_partition_manager.hpp:81-89       pskv_jump_hash
  *
  * Semantics (PSKV_ASSIGN, the reference semantics; map_storage.hpp:22-23,
  * vector_storage.hpp:21-43): a shard is a last-write-wins key/value store with
@@ -187,6 +189,14 @@ int pskv_reset_timing(pskv_shard* s);
 int pskv_range_slice(const uint64_t* range_begin, const uint64_t* range_end, int nranges,
                      const uint32_t* keys, uint64_t n, int32_t* slice_range,
                      uint64_t* slice_start, uint64_t* slice_len);
+
+/* Bucket of every key under jump consistent hashing over `nbuckets` servers:
+ * the bucket function of ConsistentHashingPartitionManager::Slice, the
+ * reference Engine's default partitioner
+ * (base/consistent_hashing_partition_manager.hpp:18-42,81-89;
+ * driver/engine.hpp:143-150).  out_bucket[i] in [0, nbuckets); the slice of key
+ * i goes to server_thread_ids[out_bucket[i]].  Host memory, any n. */
+int pskv_jump_hash(const uint32_t* keys, uint64_t n, int32_t nbuckets, int32_t* out_bucket);
 
 const char* pskv_last_error(void);
 int pskv_abi_version(void);

@@ -12,6 +12,9 @@ Contents
       in tests/test_oracle.py)
   range_slice_ref                    pure-Python restatement of
       base/range_partition_manager.hpp:19-46 (small inputs)
+  jump_hash_ref / hash_slice_ref     pure-Python restatement of the jump consistent
+      hash (Lamping & Veach 2014) and of ConsistentHashingPartitionManager::Slice
+      (base/consistent_hashing_partition_manager.hpp:18-42,81-89)
 
 Parity pin: the reference cannot be built here (its storages include
 glog/logging.h, absent from the image, and a stand-in header is not allowed), so
@@ -148,6 +151,37 @@ def range_slice_ref(ranges, keys):
             i += 1
         else:
             r += 1
+    return out
+
+
+def jump_hash_ref(key: int, num_buckets: int) -> int:
+    """Jump consistent hash as published (Lamping & Veach, 2014) and as the
+    reference states it (base/consistent_hashing_partition_manager.hpp:81-89):
+    64-bit LCG state, next candidate (b + 1) * 2^31 / ((state >> 33) + 1) in
+    double precision, truncated."""
+    key &= (1 << 64) - 1
+    b, j = -1, 0
+    while j < num_buckets:
+        b = j
+        key = (key * 2862933555777941757 + 1) & ((1 << 64) - 1)
+        j = int((b + 1) * (float(1 << 31) / float((key >> 33) + 1)))
+    return b
+
+
+def hash_slice_ref(server_ids, keys, vals=None):
+    """ConsistentHashingPartitionManager::Slice (base/consistent_hashing_partition_manager.hpp:18-76):
+    one slice per receiving server, in order of its first key; keys (and
+    values) in input order.  Returns [(server_id, [keys...]) or (server_id,
+    [keys...], [vals...]), ...]."""
+    out, where = [], {}
+    for i, k in enumerate(keys):
+        sid = server_ids[jump_hash_ref(int(k), len(server_ids))]
+        if sid not in where:
+            where[sid] = len(out)
+            out.append((sid, [], []) if vals is not None else (sid, []))
+        out[where[sid]][1].append(int(k))
+        if vals is not None:
+            out[where[sid]][2].append(float(vals[i]))
     return out
 
 

@@ -6,9 +6,10 @@ Importing this package loads libpskv.so and raises if it is missing: there is
 no CPU fallback on the product path.
 """
 from ._lib import PskvError, lib  # noqa: F401  (fails loudly if the HIP library is absent)
-from .shard import Shard, device_count, range_slice  # noqa: F401
-from .storage import (AbstractStorage, CheckError, Flag, HipStorage, Message, Meta,  # noqa: F401
-                      RangePartitionManager, typed)
+from .shard import Shard, device_count, jump_hash, range_slice  # noqa: F401
+from .storage import (AbstractStorage, CheckError, ConsistentHashingPartitionManager, Flag,  # noqa: F401
+                      HipStorage, Message, Meta, RangePartitionManager, typed)
 
 __all__ = ["Shard", "HipStorage", "AbstractStorage", "Message", "Meta", "Flag",
-           "RangePartitionManager", "range_slice", "device_count", "CheckError", "PskvError"]
+           "RangePartitionManager", "ConsistentHashingPartitionManager", "range_slice", "jump_hash",
+           "device_count", "CheckError", "PskvError"]

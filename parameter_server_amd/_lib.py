@@ -53,7 +53,7 @@ EXPORTED = [
     "pskv_shard_create", "pskv_shard_create_ex", "pskv_shard_destroy", "pskv_add", "pskv_get",
     "pskv_add_grouped", "pskv_get_grouped", "pskv_sync", "pskv_clear", "pskv_set_stream",
     "pskv_get_stream", "pskv_dense_ptr", "pskv_shard_info", "pskv_set_timing", "pskv_set_timing_mask",
-    "pskv_kernel_time", "pskv_reset_timing", "pskv_range_slice", "pskv_last_error",
+    "pskv_kernel_time", "pskv_reset_timing", "pskv_range_slice", "pskv_jump_hash", "pskv_last_error",
     "pskv_abi_version", "pskv_device_count",
 ]
 
@@ -106,6 +106,7 @@ def _load():
                               ctypes.POINTER(u64)], i32),
         "pskv_reset_timing": ([vp], i32),
         "pskv_range_slice": ([vp, vp, i32, vp, u64, vp, vp, vp], i32),
+        "pskv_jump_hash": ([vp, u64, i32, vp], i32),
         "pskv_last_error": ([], ctypes.c_char_p),
         "pskv_abi_version": ([], i32),
         "pskv_device_count": ([], i32),

@@ -1392,4 +1392,36 @@ int pskv_range_slice(const uint64_t* range_begin, const uint64_t* range_end, int
   return ns;
 }
 
+int pskv_jump_hash(const uint32_t* keys, uint64_t n, int32_t nbuckets, int32_t* out_bucket) {
+  // Jump consistent hash (Lamping & Veach, "A Fast, Minimal Memory, Consistent
+  // Hash Algorithm", 2014), the bucket function of the reference's default
+  // partitioner ConsistentHashingPartitionManager::JumpConsistentHash
+  // (base/consistent_hashing_partition_manager.hpp:81-89): a 64-bit LCG step
+  // per jump, the next candidate bucket (b + 1) * 2^31 / ((state >> 33) + 1)
+  // in double precision; the key enters zero-extended to 64 bits.
+  if (n == 0) return PSKV_OK;
+  if (nbuckets <= 0 || !keys || !out_bucket) return fail(PSKV_EINVAL, "pskv_jump_hash: bad argument");
+  auto hash_range = [&](uint64_t b, uint64_t e) {
+    for (uint64_t i = b; i < e; ++i) {
+      uint64_t key = keys[i];
+      int64_t bk = -1, j = 0;
+      while (j < nbuckets) {
+        bk = j;
+        key = key * 2862933555777941757ULL + 1;
+        j = (int64_t)((double)(bk + 1) * (double(1LL << 31) / double((key >> 33) + 1)));
+      }
+      out_bucket[i] = (int32_t)bk;
+    }
+  };
+  constexpr uint64_t kPiece = 1 << 18;
+  if (n <= kPiece) {
+    hash_range(0, n);
+  } else {
+    HostPool::get().run((size_t)((n + kPiece - 1) / kPiece), [&](size_t t) {
+      hash_range(t * kPiece, std::min<uint64_t>(n, (t + 1) * kPiece));
+    });
+  }
+  return PSKV_OK;
+}
+
 }  // extern "C"

@@ -256,3 +256,14 @@ def range_slice(ranges, keys):
     ns = check(lib.pskv_range_slice(rb.ctypes.data, re.ctypes.data, nr, k.ctypes.data, k.size,
                                     sr.ctypes.data, ss.ctypes.data, sl.ctypes.data))
     return [(int(sr[i]), int(ss[i]), int(sl[i])) for i in range(ns)]
+
+
+def jump_hash(keys, num_buckets: int) -> np.ndarray:
+    """Bucket of every key under the reference's default partitioner
+    (ConsistentHashingPartitionManager, base/consistent_hashing_partition_manager.hpp:81-89)
+    through the product library (pskv_jump_hash).  int32 array, values in
+    [0, num_buckets)."""
+    k = np.ascontiguousarray(keys, dtype=np.uint32)
+    out = np.empty(k.size, dtype=np.int32)
+    check(lib.pskv_jump_hash(k.ctypes.data, k.size, int(num_buckets), out.ctypes.data))
+    return out

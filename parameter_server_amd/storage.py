@@ -8,6 +8,8 @@ Mirrors, with the same names, argument meaning and error behaviour:
   HipStorage                    drop-in for MapStorage<Val> / VectorStorage<Val>
                                  (server/map_storage.hpp, server/vector_storage.hpp)
   RangePartitionManager         base/range_partition_manager.hpp:14-77 (through pskv_range_slice)
+  ConsistentHashingPartitionManager
+                                base/consistent_hashing_partition_manager.hpp:9-90 (through pskv_jump_hash)
 
 A reference glog CHECK failure aborts the process; here it raises CheckError.
 The C++ adaptor with the same shape is include/ps/hip_storage.hpp.
@@ -20,7 +22,7 @@ from typing import List
 
 import numpy as np
 
-from .shard import Shard, range_slice
+from .shard import Shard, jump_hash, range_slice
 
 
 class CheckError(AssertionError):
@@ -154,3 +156,38 @@ class RangePartitionManager:
                     for r, s, n in range_slice(self.ranges_, keys)]
         keys = np.ascontiguousarray(keys_or_kvs, dtype=np.uint32)
         return [(self.server_thread_ids_[r], keys[s:s + n]) for r, s, n in range_slice(self.ranges_, keys)]
+
+
+class ConsistentHashingPartitionManager:
+    """base/consistent_hashing_partition_manager.hpp:9-90 — the reference
+    Engine's default partitioner (driver/engine.hpp:143-150): key -> server
+    server_thread_ids[JumpConsistentHash(key, #servers)].  Slices come in order
+    of each server's first key, keys (and values, as double) in input order,
+    as the reference's own test pins
+    (base/consistent_hashing_partition_manager_test.cpp:48-139)."""
+
+    def __init__(self, server_thread_ids):
+        self.server_thread_ids_ = list(server_thread_ids)
+
+    def GetNumServers(self) -> int:
+        return len(self.server_thread_ids_)
+
+    def GetServerThreadIds(self):
+        return list(self.server_thread_ids_)
+
+    def _groups(self, keys):
+        b = jump_hash(keys, len(self.server_thread_ids_))
+        if b.size == 0:
+            return []
+        first = np.unique(b, return_index=True)[1]          # first appearance of each bucket
+        order = b[np.sort(first)]
+        return [(int(x), np.nonzero(b == x)[0]) for x in order]
+
+    def Slice(self, keys_or_kvs):
+        if isinstance(keys_or_kvs, tuple):
+            keys, vals = keys_or_kvs
+            keys = np.ascontiguousarray(keys, dtype=np.uint32)
+            vals = np.ascontiguousarray(vals, dtype=np.float64)  # KVPairs carry double
+            return [(self.server_thread_ids_[x], (keys[i], vals[i])) for x, i in self._groups(keys)]
+        keys = np.ascontiguousarray(keys_or_kvs, dtype=np.uint32)
+        return [(self.server_thread_ids_[x], keys[i]) for x, i in self._groups(keys)]

@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "ps/hip_storage.hpp"
+#include "ps/consistent_hashing_partition_manager.hpp"
 #include "ps/range_partition_manager.hpp"
 #include "ps/storage_factory.hpp"
 
@@ -138,6 +139,33 @@ static void SliceCases() {
   }
 }
 
+// ConsistentHashShardMap (the Engine's default partitioner): the slices the
+// reference's own test asserts, base/consistent_hashing_partition_manager_test.cpp:48-139
+static void HashSliceCases() {
+  std::printf("[ RUN ] HashSliceKeys / HashSliceKVs\n");
+  ConsistentHashShardMap pm({0, 1, 2});
+  {
+    std::vector<std::pair<int, AbstractPartitionManager::Keys>> sl;
+    pm.Slice(third_party::SArray<uint32_t>({2, 8, 9}), &sl);
+    EXPECT(sl.size() == 2);
+    EXPECT(sl[0].first == 0 && sl[0].second.size() == 2 && sl[0].second[0] == 2 && sl[0].second[1] == 8);
+    EXPECT(sl[1].first == 2 && sl[1].second.size() == 1 && sl[1].second[0] == 9);
+    pm.Slice(third_party::SArray<uint32_t>({2, 8, 9, 10, 11, 12, 13}), &sl);
+    EXPECT(sl.size() == 3);
+    EXPECT(sl[0].first == 0 && sl[0].second.size() == 3 && sl[0].second[2] == 13);
+    EXPECT(sl[1].first == 2 && sl[1].second.size() == 3 && sl[1].second[0] == 9 && sl[1].second[1] == 10);
+    EXPECT(sl[2].first == 1 && sl[2].second.size() == 1 && sl[2].second[0] == 12);
+  }
+  {
+    std::vector<std::pair<int, AbstractPartitionManager::KVPairs>> sl;
+    pm.Slice(std::make_pair(third_party::SArray<uint32_t>({2, 5, 9}), third_party::SArray<double>({.2, .5, .9})),
+             &sl);
+    EXPECT(sl.size() == 3);
+    for (int i = 0; i < 3; ++i) EXPECT(sl[i].first == i && sl[i].second.first.size() == 1);
+    EXPECT(sl[0].second.second[0] == .2 && sl[1].second.first[0] == 5 && sl[1].second.second[0] == .5);
+  }
+}
+
 // CreateTable over three server threads: each server's HipStorage owns its
 // range; keys the slicer routes to the last server beyond its range land in
 // its overflow table.  Adds go through the models (ASP: immediate).
@@ -192,6 +220,7 @@ static void CreateTableHip() {
 int main(int argc, char** argv) {
   const bool host_only = argc > 1 && std::strcmp(argv[1], "--host-only") == 0;
   SliceCases();
+  HashSliceCases();
   if (!host_only) {
     AddGet<int>({1, 2, 3}, "AddGetInt");
     AddGet<float>({0.1f, 0.2f, 0.3f}, "AddGetFloat");

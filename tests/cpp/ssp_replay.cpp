@@ -20,6 +20,11 @@
 //
 // usage: ssp_replay [--model ssp|bsp|asp] [--workers W] [--shards S] [--iters I]
 //                   [--batch B] [--staleness T] [--skew K] [--cpu-only] [--known-answers]
+//                   [--partition range|hash]
+// --partition hash slices with the reference Engine's DEFAULT partitioner, the
+// jump consistent hash (base/consistent_hashing_partition_manager.hpp; the LR
+// app's own configuration, driver/engine.hpp:143-150): every shard then owns
+// the whole feature range [0, n_features).
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
@@ -37,6 +42,7 @@
 
 #include "ps/consistency.hpp"
 #include "ps/hip_storage.hpp"
+#include "ps/consistent_hashing_partition_manager.hpp"
 #include "ps/range_partition_manager.hpp"
 #include "ps/server_thread.hpp"
 #include "ps/storage_factory.hpp"
@@ -111,6 +117,7 @@ struct Config {
   bool cpu_only = false;
   bool bsp_ungrouped = false;
   bool threads = false;  // one ServerThread per shard (concurrent HipStorage use)
+  std::string partition = "range";  // range | hash
 };
 
 struct ReplyRecord {
@@ -130,12 +137,16 @@ class Replay {
  public:
   Replay(const Config& c, bool hip) : c_(c), hip_(hip) {
     const uint64_t step = c.n_features / c.shards;
+    const bool hashed = c.partition == "hash";
     for (int s = 0; s < c.shards; ++s) {
       const uint64_t lo = s * step, hi = s + 1 == c.shards ? c.n_features : (s + 1) * step;
-      ranges_.push_back({lo, hi});
+      ranges_.push_back(hashed ? std::make_pair((uint64_t)0, (uint64_t)c.n_features) : std::make_pair(lo, hi));
       ids_.push_back((uint32_t)s);
     }
-    map_.reset(new RangeShardMap(ids_, ranges_));
+    if (hashed)
+      map_.reset(new ConsistentHashShardMap(ids_));
+    else
+      map_.reset(new RangeShardMap(ids_, ranges_));
     int ndev = pskv_device_count();
     if (c.threads) {
       // Engine::CreateTable (driver/engine.hpp:93-131) through the restated
@@ -143,7 +154,7 @@ class Replay {
       for (int s = 0; s < c.shards; ++s) threads_.emplace_back(new ServerThread((uint32_t)s));
       const ModelType mt = c.model == "ssp" ? ModelType::SSP : c.model == "bsp" ? ModelType::BSP : ModelType::ASP;
       storages_ = CreateTable<double>(
-          threads_, *map_, 0, mt, hip ? StorageType::Hip : StorageType::Map, c.staleness, &replies_,
+          threads_, ranges_, 0, mt, hip ? StorageType::Hip : StorageType::Map, c.staleness, &replies_,
           PSKV_ASSIGN, [](StorageType) { return std::unique_ptr<AbstractStorage>(new OracleStorage<double>()); });
       for (auto& t : threads_) {
         if (auto* bsp = dynamic_cast<BSPModel*>(t->GetModel(0))) bsp->SetGroupedFlush(!c.bsp_ungrouped);
@@ -348,7 +359,7 @@ class Replay {
 
   void send_get(Worker& w, const std::vector<Key>& keys) {  // kv_client_table.hpp:107-139
     ++out_.gets;
-    std::vector<std::pair<int, RangeShardMap::Keys>> sl;
+    std::vector<std::pair<int, AbstractPartitionManager::Keys>> sl;
     map_->Slice(third_party::SArray<Key>(keys), &sl);
     w.reply.clear();
     w.keys_ = keys;
@@ -375,19 +386,17 @@ class Replay {
 
   void send_add(Worker& w, const std::vector<Key>& keys, const std::vector<double>& vals) {
     ++out_.adds;  // kv_client_table.hpp:78-105 (double -> Val is exact for Val = double)
-    std::vector<std::pair<int, RangeShardMap::Keys>> sl;
-    third_party::SArray<Key> ka(keys);
-    map_->Slice(ka, &sl);
+    // the KV form of Slice (values as double, abstract_partition_manager.hpp:21-22)
+    std::vector<std::pair<int, AbstractPartitionManager::KVPairs>> sl;
+    map_->Slice(std::make_pair(third_party::SArray<Key>(keys), third_party::SArray<double>(vals)), &sl);
     for (auto& s : sl) {
-      const size_t off = s.second.data() - ka.data();
       Message m;
       m.meta.sender = w.tid;
       m.meta.recver = s.first;
       m.meta.model_id = 0;
       m.meta.flag = Flag::kAdd;
-      m.AddData(s.second);
-      m.AddData(third_party::SArray<double>(
-          std::vector<double>(vals.begin() + off, vals.begin() + off + s.second.size())));
+      m.AddData(s.second.first);
+      m.AddData(s.second.second);
       deliver(m);
     }
   }
@@ -458,7 +467,7 @@ class Replay {
   bool hip_;
   std::vector<std::pair<uint64_t, uint64_t>> ranges_;
   std::vector<uint32_t> ids_;
-  std::unique_ptr<RangeShardMap> map_;
+  std::unique_ptr<AbstractPartitionManager> map_;
   std::vector<AbstractStorage*> storages_;
   std::vector<std::unique_ptr<AbstractModel>> models_;
   std::vector<std::unique_ptr<ServerThread>> threads_;
@@ -611,6 +620,7 @@ int main(int argc, char** argv) {
     else if (a == "--bsp-ungrouped") c.bsp_ungrouped = true;
     else if (a == "--threads") c.threads = true;
     else if (a == "--known-answers") ka = true;
+    else if (a == "--partition") c.partition = nxt();
   }
   int fails = 0;
   if (ka) {
@@ -623,9 +633,9 @@ int main(int argc, char** argv) {
   Run other = c.cpu_only ? Replay(c, false).run() : Replay(c, true).run();
   std::string why;
   const bool ok = same(ref, other, &why);
-  std::printf("replay model=%s workers=%d shards=%d iters=%d batch=%d staleness=%d: msgs=%llu adds=%llu "
-              "gets=%llu clocks=%llu ssp_releases=%llu replies=%zu\n",
-              c.model.c_str(), c.workers, c.shards, c.iters, c.batch, c.staleness,
+  std::printf("replay model=%s partition=%s workers=%d shards=%d iters=%d batch=%d staleness=%d: msgs=%llu "
+              "adds=%llu gets=%llu clocks=%llu ssp_releases=%llu replies=%zu\n",
+              c.model.c_str(), c.partition.c_str(), c.workers, c.shards, c.iters, c.batch, c.staleness,
               (unsigned long long)ref.msgs, (unsigned long long)ref.adds, (unsigned long long)ref.gets,
               (unsigned long long)ref.clocks, (unsigned long long)ref.echoes, ref.log.size());
   std::printf("cpu %.3f s, %s %.3f s\n", ref.seconds, c.cpu_only ? "cpu" : "hip", other.seconds);

@@ -88,6 +88,19 @@ KNOWN = {
          "ranges": [[2, 4], [4, 8]], "keys": [0, 5], "expect": [[1, [0, 5]]]},
         {"cite": "empty input", "ranges": [[0, 4], [4, 8]], "keys": [], "expect": []},
     ],
+    # ConsistentHashingPartitionManager (the Engine's default partitioner): the
+    # slices its own test asserts, with the per-key servers its recorded log
+    # lines give (server ids [0, 1, 2]); slices in first-appearance order
+    "hash_slice_cases": [
+        {"cite": "base/consistent_hashing_partition_manager_test.cpp:48-77", "servers": [0, 1, 2],
+         "keys": [2, 8, 9], "expect": [[0, [2, 8]], [2, [9]]]},
+        {"cite": "base/consistent_hashing_partition_manager_test.cpp:79-106", "servers": [0, 1, 2],
+         "keys": [2, 8, 9, 10, 11, 12, 13], "expect": [[0, [2, 8, 13]], [2, [9, 10, 11]], [1, [12]]]},
+        {"cite": "base/consistent_hashing_partition_manager_test.cpp:109-139 (SliceKVs)", "servers": [0, 1, 2],
+         "keys": [2, 5, 9], "vals": [0.2, 0.5, 0.9],
+         "expect": [[0, [2], [0.2]], [1, [5], [0.5]], [2, [9], [0.9]]]},
+        {"cite": "empty input", "servers": [0, 1, 2], "keys": [], "expect": []},
+    ],
 }
 
 DT = {"int32": np.int32, "float32": np.float32, "float64": np.float64}

@@ -101,6 +101,58 @@ def test_range_slice_random_vs_oracle(oracle_mod):
         assert got == want
 
 
+def _hash_cases():
+    import json
+
+    with open(os.path.join(ROOT, "tests", "golden", "reference_known_answers.json")) as f:
+        return json.load(f)["hash_slice_cases"]
+
+
+def test_hash_partition_matches_reference_cases():
+    """ConsistentHashingPartitionManager (the reference Engine's default
+    partitioner) through the product library: the slices the reference's own
+    test asserts (base/consistent_hashing_partition_manager_test.cpp:48-139)."""
+    from parameter_server_amd import ConsistentHashingPartitionManager
+
+    for c in _hash_cases():
+        pm = ConsistentHashingPartitionManager(c["servers"])
+        if "vals" in c:
+            got = [[sid, [int(k) for k in kv[0]], [float(v) for v in kv[1]]]
+                   for sid, kv in pm.Slice((c["keys"], c["vals"]))]
+        else:
+            got = [[sid, [int(k) for k in ks]] for sid, ks in pm.Slice(c["keys"])]
+        assert got == c["expect"], c["cite"]
+
+
+def test_oracle_hash_slice_matches_reference_cases(oracle_mod):
+    for c in _hash_cases():
+        got = [list(x) for x in oracle_mod.hash_slice_ref(c["servers"], c["keys"], c.get("vals"))]
+        assert got == c["expect"], c["cite"]
+
+
+def test_jump_hash_random_vs_oracle(oracle_mod):
+    """pskv_jump_hash against the pure-Python restatement: random keys over the
+    whole uint32 range (the sentinel 0xFFFFFFFF included), 1..1000 buckets, and
+    a batch large enough for the host pool's parallel pieces."""
+    from parameter_server_amd import jump_hash
+
+    rng = np.random.default_rng(3)
+    for nb in (1, 2, 3, 7, 8, 64, 1000):
+        keys = np.concatenate([rng.integers(0, 2**32, size=300), [0, 1, 0xFFFFFFFF]]).astype(np.uint32)
+        got = jump_hash(keys, nb)
+        want = [oracle_mod.jump_hash_ref(int(k), nb) for k in keys]
+        assert got.tolist() == want, nb
+    big = rng.integers(0, 2**32, size=(1 << 20) + 12345).astype(np.uint32)
+    got = jump_hash(big, 8)
+    idx = rng.integers(0, big.size, size=2000)
+    assert [int(got[i]) for i in idx] == [oracle_mod.jump_hash_ref(int(big[i]), 8) for i in idx]
+    # consistency: growing 8 -> 9 buckets moves only keys into the new bucket
+    got9 = jump_hash(big, 9)
+    moved = got9 != got
+    assert np.all(got9[moved] == 8) and 0.08 < moved.mean() < 0.14
+    assert jump_hash(np.zeros(0, np.uint32), 4).size == 0
+
+
 def test_cpp_boundary_host_cases():
     """tests/cpp/hip_storage_test.cpp range-map cases (host only)."""
     exe = os.path.join(ROOT, "parameter_server_amd", "bin", "hip_storage_test")

@@ -57,3 +57,30 @@ def test_replay_threaded_hip_vs_cpu(model):
     rc, out = run("--threads", "--model", model, "--iters", "8", "--shards", "8", "--workers", "4")
     assert rc == 0, out
     assert "REPLAY OK (bit-exact)" in out
+
+
+@pytest.mark.parametrize("model", ["ssp", "bsp"])
+def test_replay_hash_partition_cpu_deterministic(model):
+    """The reference Engine's default partitioner (jump consistent hash,
+    base/consistent_hashing_partition_manager.hpp) on the worker side; every
+    shard owns the whole feature range."""
+    rc, out = run("--cpu-only", "--partition", "hash", "--model", model, "--iters", "4",
+                  "--features", "200000")
+    assert rc == 0, out
+    assert "partition=hash" in out and "REPLAY OK" in out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model,threads", [("bsp", False), ("bsp", True), ("ssp", False)])
+def test_replay_hash_partition_hip_vs_cpu(model, threads):
+    """The LR app's own configuration (BSP, consistent hashing, Val = double;
+    app/logistic_regression.cpp:154, driver/engine.hpp:143-150) over 8 HBM
+    shards: every Get reply and every shard's contents bit-identical to the
+    oracle storage run."""
+    args = ["--partition", "hash", "--model", model, "--iters", "8", "--shards", "8", "--workers", "4",
+            "--features", "200000"]
+    if threads:
+        args.append("--threads")
+    rc, out = run(*args)
+    assert rc == 0, out
+    assert "REPLAY OK (bit-exact)" in out
