@@ -26,6 +26,7 @@ constexpr int kRbMaxBuckets = 2064;  // key buckets incl. the out-of-range bucke
 constexpr uint32_t kRbMaxSc = 1024;  // K5 super-chunks per launch (one run per resolve thread)
 constexpr int kInlineMax = 256;      // keys of an inline (kernarg-carried) Add
 constexpr int kInlineGetMax = 512;   // keys of an inline Get
+constexpr int kInlineMaxChunks = 16;   // inline launches per call at most (reply buffer size)
 constexpr unsigned long long kEmpty64 = ~0ull;
 constexpr uint32_t kEmpty32 = 0xFFFFFFFFu;
 

@@ -236,6 +236,13 @@ struct pskv_shard {
   // PSKV_INLINE: host calls of <= kInlineMax (Add) / kInlineGetMax (Get) keys in
   // all travel inside the kernel arguments (K8); 0 sends them through staging
   bool tune_inline = true;
+  // PSKV_INLINE_ADD_CHUNKS / PSKV_INLINE_GET_CHUNKS: K8 launches per call at
+  // most (1..kInlineMaxChunks).  Measured (tools/micro/small_latency.cpp): an
+  // Add launch costs ~3-7 us of enqueue, the staged path ~48-65 us, so up to 8
+  // (2048 keys) win; a Get launch beyond the first costs ~10 us (the reply
+  // goes over PCIe as it is written) against ~32 us staged, so one.
+  int tune_inline_add_chunks = 8;
+  int tune_inline_get_chunks = 1;
   void* ireply = nullptr;  // page-locked reply buffer of inline Gets (kInlineGetMax values)
   bool tune_ispin = true;  // PSKV_ISPIN: poll the reply's sequence word instead of a stream wait
   unsigned int ireply_seq = 0;
@@ -825,30 +832,17 @@ int stage_host_batches(pskv_shard* s, const std::vector<pskv_batch>& in,
   return PSKV_OK;
 }
 
-// K8: a host Add of at most kInlineMax keys in all (the reference's per-sample
-// messages).  The grouped form equals the concatenation of its batches in
-// order (last-wins / sums follow index order across batches), so the batches
-// are packed into one kernel-argument message; the caller's buffers are free
-// once the launch is enqueued (the runtime copies the arguments).
+// K8: a host Add of at most kInlineMax keys per launch (the reference's
+// per-sample messages), up to tune_inline_chunks launches per call.  The
+// grouped form equals the concatenation of its batches in order (last-wins /
+// sums follow index order across batches), and so does a sequence of launches
+// over consecutive pieces of it, so the batches are packed into kernel-argument
+// messages of kInlineMax keys; the caller's buffers are free once the launches
+// are enqueued (the runtime copies the arguments).
 int inline_add(pskv_shard* s, const std::vector<pskv_batch>& v, uint64_t total) {
-  InlineAdd a;
-  a.n = (uint32_t)total;
-  uint32_t i = 0;
   uint64_t outside = 0;
-  for (const auto& b : v) {
-    for (uint64_t e = 0; e < b.n; ++e, ++i) {
-      const uint32_t k = b.keys[e];
-      a.keys[i] = k;
-      outside += (uint64_t)(uint32_t)(k - s->key_begin) >= s->range;
-      if (s->vb == 8) {
-        std::memcpy(&a.vals[i], static_cast<const char*>(b.vals) + e * 8, 8);
-      } else {
-        uint32_t w;
-        std::memcpy(&w, static_cast<const char*>(b.vals) + e * 4, 4);
-        a.vals[i] = w;
-      }
-    }
-  }
+  for (const auto& b : v)
+    for (uint64_t e = 0; e < b.n; ++e) outside += (uint64_t)(uint32_t)(b.keys[e] - s->key_begin) >= s->range;
   if (outside) {
     // exact bound on new overflow keys, as for staged host inputs
     if (2 * (s->ocount_known + outside) > s->ocap) {
@@ -859,42 +853,81 @@ int inline_add(pskv_shard* s, const std::vector<pskv_batch>& v, uint64_t total) 
     }
     s->ocount_known += outside;
   }
-  LaunchTimer t(s, PSKV_K_INLINE_ADD, total);
-  PSKV_HIP(launch_inline_add(s->dtype, s->mode, a, s->dview(), s->ovf, s->stream));
-  t.done();
-  return PSKV_OK;
+  InlineAdd a;
+  a.n = 0;
+  auto flush = [&]() -> int {
+    if (a.n == 0) return PSKV_OK;
+    LaunchTimer t(s, PSKV_K_INLINE_ADD, a.n);
+    PSKV_HIP(launch_inline_add(s->dtype, s->mode, a, s->dview(), s->ovf, s->stream));
+    t.done();
+    a.n = 0;
+    return PSKV_OK;
+  };
+  for (const auto& b : v) {
+    for (uint64_t e = 0; e < b.n; ++e) {
+      const uint32_t i = a.n++;
+      a.keys[i] = b.keys[e];
+      if (s->vb == 8) {
+        std::memcpy(&a.vals[i], static_cast<const char*>(b.vals) + e * 8, 8);
+      } else {
+        uint32_t w;
+        std::memcpy(&w, static_cast<const char*>(b.vals) + e * 4, 4);
+        a.vals[i] = w;
+      }
+      if (a.n == (uint32_t)kInlineMax)
+        if (int rc = flush()) return rc;
+    }
+  }
+  (void)total;
+  return flush();
 }
 
-// K8 Get: keys in the kernel arguments, the reply written by the kernel into a
-// page-locked buffer, copied out to the caller after the stream completes.
+// K8 Get: keys in the kernel arguments (kInlineGetMax per launch), the reply
+// written by the kernels into a page-locked buffer, copied out to the caller
+// once the LAST launch has published (stream order: the earlier ones are done).
 int inline_get(pskv_shard* s, const std::vector<pskv_batch>& v, uint64_t total) {
+  const size_t cap = (size_t)kInlineGetMax * kInlineMaxChunks * 8;
   if (!s->ireply) {
-    // kInlineGetMax values, then the reply's sequence word on its own line.
-    // Coherent (fine-grained) memory: the kernel's stores go straight to the
-    // host.  Measured alternatives (tools/micro/small_latency.cpp, DESIGN.md
-    // §5): non-coherent pinned memory the same, a device reply + D2H copy
-    // 3 us slower.
-    if (hipHostMalloc(&s->ireply, (size_t)kInlineGetMax * 8 + 128, hipHostMallocCoherent) != hipSuccess) {
+    // kInlineGetMax * kInlineMaxChunks values, then the reply's sequence word
+    // on its own line.  Coherent (fine-grained) memory: the kernel's stores go
+    // straight to the host.  Measured alternatives (tools/micro/small_latency.cpp,
+    // DESIGN.md §5): non-coherent pinned memory the same, a device reply + D2H
+    // copy 3 us slower.
+    if (hipHostMalloc(&s->ireply, cap + 128, hipHostMallocCoherent) != hipSuccess) {
       s->ireply = nullptr;
       return fail(PSKV_ENOMEM, "inline reply buffer allocation failed");
     }
   }
-  InlineGet a;
-  a.n = (uint32_t)total;
-  uint32_t i = 0;
-  for (const auto& b : v) {
-    std::memcpy(&a.keys[i], b.keys, b.n * 4);
-    i += (uint32_t)b.n;
-  }
-  LaunchTimer t(s, PSKV_K_INLINE_GET, total);
-  // spin-wait reply (coherent host buffer, no timing events to drain): the
-  // kernel publishes a sequence number after the values and the host polls it
-  const bool spin = s->tune_ispin && !t.a;
-  unsigned int* done = reinterpret_cast<unsigned int*>(static_cast<char*>(s->ireply) + (size_t)kInlineGetMax * 8);
+  unsigned int* done = reinterpret_cast<unsigned int*>(static_cast<char*>(s->ireply) + cap);
   const unsigned int seq = ++s->ireply_seq;
-  PSKV_HIP(launch_inline_get(s->vb, a, s->dview(), s->ovf, s->ireply, spin ? done : nullptr, seq,
-                             s->stream));
-  t.done();
+  InlineGet a;
+  a.n = 0;
+  uint64_t issued = 0;  // values requested by earlier launches
+  bool spin = false;
+  auto flush = [&](bool last) -> int {
+    if (a.n == 0) return PSKV_OK;
+    LaunchTimer t(s, PSKV_K_INLINE_GET, a.n);
+    // spin-wait reply (coherent host buffer, no timing events to drain): the
+    // last kernel publishes a sequence number after the values; the host polls it
+    spin = last && s->tune_ispin && !t.a;
+    PSKV_HIP(launch_inline_get(s->vb, a, s->dview(), s->ovf,
+                               static_cast<char*>(s->ireply) + issued * (size_t)s->vb,
+                               spin ? done : nullptr, seq, s->stream));
+    t.done();
+    issued += a.n;
+    a.n = 0;
+    return PSKV_OK;
+  };
+  uint64_t seen = 0;
+  for (const auto& b : v) {
+    for (uint64_t e = 0; e < b.n; ++e) {
+      a.keys[a.n++] = b.keys[e];
+      ++seen;
+      if (a.n == (uint32_t)kInlineGetMax)
+        if (int rc = flush(seen == total)) return rc;
+    }
+  }
+  if (int rc = flush(true)) return rc;
   if (spin) {
     // poll the sequence word; every 1024 polls ask the stream whether it
     // finished (or failed) without publishing, so a fault cannot hang the host
@@ -935,7 +968,7 @@ int add_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
   if (!device && s->tune_inline) {
     uint64_t total = 0;
     for (const auto& b : v) total += b.n;
-    if (total <= (uint64_t)kInlineMax) return inline_add(s, v, total);
+    if (total <= (uint64_t)kInlineMax * s->tune_inline_add_chunks) return inline_add(s, v, total);
   }
   bool host_verified = false, host_dense = false;
   if (!device) {
@@ -1000,7 +1033,7 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
   if (!device && s->tune_inline) {
     uint64_t total = 0;
     for (const auto& b : v) total += b.n;
-    if (total <= (uint64_t)kInlineGetMax) return inline_get(s, v, total);
+    if (total <= (uint64_t)kInlineGetMax * s->tune_inline_get_chunks) return inline_get(s, v, total);
   }
   std::vector<pskv_batch> dv = v;
   size_t out_off = 0;
@@ -1160,6 +1193,10 @@ int pskv_shard_create_ex(int device, uint32_t key_begin, uint64_t key_end, int d
   if (const char* e = std::getenv("PSKV_NTP")) s->tune_ntp = std::atoi(e) != 0;
   if (const char* e = std::getenv("PSKV_PAGEABLE_DMA")) s->tune_pageable_dma = std::atoi(e) != 0;
   if (const char* e = std::getenv("PSKV_INLINE")) s->tune_inline = std::atoi(e) != 0;
+  if (const char* e = std::getenv("PSKV_INLINE_ADD_CHUNKS"))
+    s->tune_inline_add_chunks = std::max(1, std::min(kInlineMaxChunks, std::atoi(e)));
+  if (const char* e = std::getenv("PSKV_INLINE_GET_CHUNKS"))
+    s->tune_inline_get_chunks = std::max(1, std::min(kInlineMaxChunks, std::atoi(e)));
   if (const char* e = std::getenv("PSKV_ISPIN")) s->tune_ispin = std::atoi(e) != 0;
   if (const char* e = std::getenv("PSKV_TILE_GRID")) {
     const int v = std::atoi(e);

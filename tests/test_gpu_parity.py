@@ -973,8 +973,9 @@ def test_inline_small_messages_assign(cuda, oracle_mod, dt, monkeypatch):
     assert_bits_equal(big_staged, ref.get(q), "full read after staged adds")
 
 
+@pytest.mark.parametrize("max_n", [256, 2048])
 @pytest.mark.parametrize("dt", [np.int32, np.float32, np.float64])
-def test_inline_accumulate_sequential_bits(cuda, dt):
+def test_inline_accumulate_sequential_bits(cuda, dt, max_n):
     """K8 accumulate: the first occurrence of a key adds every occurrence in
     index order, so the result equals sequential accumulation in the value
     dtype BIT FOR BIT (np.add.at), overflow keys included."""
@@ -982,7 +983,7 @@ def test_inline_accumulate_sequential_bits(cuda, dt):
 
     rng = np.random.default_rng(909)
     kb, ke = 0, 2048
-    msgs = _small_messages(rng, kb, ke, 80)
+    msgs = _small_messages(rng, kb, ke, 80, max_n=max_n)  # 2048: several launches per message
     want = np.zeros(ke - kb, dt)
     want_ovf = {}
     with ps.Shard(kb, ke, dt, mode="accumulate", overflow_slots=64) as sh:
@@ -1002,10 +1003,12 @@ def test_inline_accumulate_sequential_bits(cuda, dt):
     assert_bits_equal(got_ovf, np.array([want_ovf[int(x)] for x in ok], dt), "inline accumulate (overflow)")
 
 
-@pytest.mark.parametrize("n", [255, 256, 257, 511, 512, 513])
+@pytest.mark.parametrize("n", [255, 256, 257, 511, 512, 513, 2048, 2049])
 def test_inline_size_boundaries(cuda, oracle_mod, n):
-    """Messages at and beyond the inline limits (256 keys per Add, 512 per
-    Get; grouped calls count their batches together) agree with the oracle."""
+    """Messages at and beyond the inline limits (an Add goes out in launches
+    of 256 keys, at most 8 of them, so 2048 keys; a Get of at most 512 keys in
+    one launch; grouped calls count their batches together) agree with the
+    oracle, duplicates straddling launch boundaries included."""
     import parameter_server_amd as ps
     from parameter_server_amd import _lib
 
@@ -1029,7 +1032,7 @@ def test_inline_size_boundaries(cuda, oracle_mod, n):
         got = sh.get(k)
         adds = sh.kernel_time(_lib.PSKV_K_INLINE_ADD)["launches"]
         gets = sh.kernel_time(_lib.PSKV_K_INLINE_GET)["launches"]
-    assert adds == (2 if n <= 256 else 0)
+    assert adds == (2 * -(-n // 256) if n <= 2048 else 0)
     assert gets == (2 if n <= 512 else 0)
     assert_bits_equal(got, ref.get(k), "single")
     for p, o in zip(parts, outs):

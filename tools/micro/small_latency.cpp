@@ -28,17 +28,22 @@ static void die(int rc, const char* what) {
 }
 
 int main() {
-  const int sizes[] = {1, 16, 64, 256};
+  const int sizes[] = {1, 16, 64, 256, 512, 1024, 2048, 4096};
   const int reps = 2000;
   std::mt19937 rng(7);
   std::printf("%-10s %6s %10s %10s %12s %12s\n", "path", "keys", "add_us", "get_us", "add+get_us",
               "get_only_us");
   // variants: inline with the polled reply, inline with a stream wait
   // (PSKV_ISPIN=0), staged (PSKV_INLINE=0)
-  const char* names[] = {"inline", "inline-sync", "staged"};
-  for (int var = 0; var < 3; ++var) {
-    setenv("PSKV_INLINE", var < 2 ? "1" : "0", 1);
-    setenv("PSKV_ISPIN", var == 0 ? "1" : "0", 1);
+  // and inline with up to 16 launches per call for both (PSKV_INLINE_*_CHUNKS=16)
+  const char* names[] = {"inline", "inline-sync", "staged", "inline-x16"};
+  for (int var = 0; var < 4; ++var) {
+    setenv("PSKV_INLINE", var != 2 ? "1" : "0", 1);
+    setenv("PSKV_ISPIN", var != 1 ? "1" : "0", 1);
+    if (var == 3) {
+      setenv("PSKV_INLINE_ADD_CHUNKS", "16", 1);
+      setenv("PSKV_INLINE_GET_CHUNKS", "16", 1);
+    }
     pskv_shard* s = nullptr;
     die(pskv_shard_create(0, 0, 1000000, PSKV_F64, PSKV_ASSIGN, &s), "create");
     for (int n : sizes) {
