@@ -839,7 +839,7 @@ int stage_host_batches(pskv_shard* s, const std::vector<pskv_batch>& in,
 // over consecutive pieces of it, so the batches are packed into kernel-argument
 // messages of kInlineMax keys; the caller's buffers are free once the launches
 // are enqueued (the runtime copies the arguments).
-int inline_add(pskv_shard* s, const std::vector<pskv_batch>& v, uint64_t total) {
+int inline_add(pskv_shard* s, const std::vector<pskv_batch>& v) {
   uint64_t outside = 0;
   for (const auto& b : v)
     for (uint64_t e = 0; e < b.n; ++e) outside += (uint64_t)(uint32_t)(b.keys[e] - s->key_begin) >= s->range;
@@ -878,7 +878,6 @@ int inline_add(pskv_shard* s, const std::vector<pskv_batch>& v, uint64_t total) 
         if (int rc = flush()) return rc;
     }
   }
-  (void)total;
   return flush();
 }
 
@@ -968,7 +967,7 @@ int add_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
   if (!device && s->tune_inline) {
     uint64_t total = 0;
     for (const auto& b : v) total += b.n;
-    if (total <= (uint64_t)kInlineMax * s->tune_inline_add_chunks) return inline_add(s, v, total);
+    if (total <= (uint64_t)kInlineMax * s->tune_inline_add_chunks) return inline_add(s, v);
   }
   bool host_verified = false, host_dense = false;
   if (!device) {
