@@ -97,15 +97,25 @@ hipError_t launch_general_commit(int vb, const GroupArgs& ga, uint32_t nwg, cons
                                  const uint32_t* cond, uint32_t epoch, hipStream_t st);
 hipError_t launch_ovf_rehash(int vb, const Ovf& from, uint64_t from_cap, const Ovf& to,
                              hipStream_t st);
+// K5 key buckets: windows of 2^wbits keys of the owned range, window w in
+// bucket w % nbd (nbd >= 1); rcp = 1.0 / nbd; span = keys per bucket at most
+// (ceil(windows / nbd) << wbits), the extent of a bucket's local index.
+struct RbMap {
+  uint32_t wbits;
+  uint32_t nbd;
+  double rcp;
+  uint32_t span;
+};
+
 // K5 radix-bucket general Add (2 launches: K5a bin, K5b resolve).  `ga`
-// chunked by rb_superchunk(vb) keys (nsc <= kRbMaxSc super-chunks); buckets
-// are key offset >> bshift (nbd dense buckets) plus one out-of-range bucket.
+// chunked by rb_superchunk(vb) keys (nsc <= kRbMaxSc super-chunks); nbd dense
+// buckets (RbMap) plus one out-of-range bucket.
 // Scratch: loff: nsc * (nbd+2) u16 (each super-chunk's bucket starts); tmp:
 // nsc * rb_superchunk(vb) entries (rb_entry_bytes(vb) each).
 // apply_log2: log2 of the resolve workgroup's LDS table slots (13: 64 KiB, two
 // workgroups per CU, ~7 Ki entries per bucket in one pass; 14: 128 KiB, ~14 Ki).
 hipError_t launch_rb_add(int dtype, int mode, const GroupArgs& ga, uint32_t nsc,
-                         const DenseView& d, const Ovf& o, uint32_t bshift, uint32_t nbd,
+                         const DenseView& d, const Ovf& o, const RbMap& bm,
                          int apply_log2, uint16_t* loff, void* tmp, hipStream_t st);
 uint32_t rb_superchunk(int vb);
 // K8: one small host message carried in the kernarg segment (one workgroup).

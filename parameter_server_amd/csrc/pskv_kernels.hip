@@ -850,7 +850,13 @@ __global__ __launch_bounds__(kBlock) void k_ovf_rehash(Ovf from, uint64_t from_c
 // atomics": 64 lanes in 64 rows ≈ 17x slower).  K5 instead moves the data to
 // where it can be resolved locally, in two launches.  Work unit of the first:
 // a SUPER-CHUNK of 8 Ki keys of one batch (4 Ki for 8-byte values); key
-// bucket = key offset >> bshift, plus one bucket for out-of-range keys.
+// buckets (RbMap): the owned range is cut into windows of 2^wbits keys, dealt
+// round-robin to nbd buckets (window w -> bucket w % nbd), plus one bucket for
+// out-of-range keys.  Interleaved windows keep a batch that covers only part of
+// the range — sorted or dense keys pushed without the hint — spread over every
+// bucket; with one contiguous window per bucket such a batch lands in a few
+// buckets and the resolve of each runs on one CU (2^32 sequential keys: over
+// 3 minutes, against 1.4 s interleaved).
 //   K5a k_rb_bin      per super-chunk: LDS hash dedup (one entry per distinct
 //                     key: its last value / its sum), LDS counting sort of the
 //                     entries by bucket, one coalesced write of the sorted
@@ -882,10 +888,34 @@ struct RbEnt<8> {
   unsigned long long val;
 };
 
-__device__ __forceinline__ uint32_t rb_bucket(const DenseView& d, uint32_t k, uint32_t bshift,
-                                              uint32_t nbd) {
+// Window w = off >> wbits -> bucket w % nbd, and the bucket-local window index
+// w / nbd (exact: double reciprocal, then a +-1 fix-up).
+__device__ __forceinline__ uint32_t rb_split(const RbMap& m, uint32_t off, uint32_t* j) {
+  const uint32_t w = off >> m.wbits;
+  uint32_t q = (uint32_t)((double)w * m.rcp);
+  int64_t r = (int64_t)w - (int64_t)q * m.nbd;
+  if (r < 0) {
+    --q;
+    r += m.nbd;
+  } else if (r >= (int64_t)m.nbd) {
+    ++q;
+    r -= m.nbd;
+  }
+  *j = q;
+  return (uint32_t)r;
+}
+
+__device__ __forceinline__ uint32_t rb_bucket(const DenseView& d, uint32_t k, const RbMap& m) {
   const uint32_t off = k - d.key_begin;
-  return (uint64_t)off < d.range ? (off >> bshift) : nbd;  // nbd = the out-of-range bucket
+  uint32_t j;
+  return (uint64_t)off < d.range ? rb_split(m, off, &j) : m.nbd;  // nbd = the out-of-range bucket
+}
+
+// Bucket-local index of an in-range key offset (dense in [0, m.span)).
+__device__ __forceinline__ uint32_t rb_local(const RbMap& m, uint32_t off) {
+  uint32_t j;
+  (void)rb_split(m, off, &j);
+  return (j << m.wbits) | (off & ((1u << m.wbits) - 1u));
 }
 
 // Block-wide exclusive scan of a[0..n) in LDS, in place (n <= kRbMaxBuckets + 1).
@@ -995,8 +1025,8 @@ constexpr uint32_t rb_sc() {
 }
 
 template <typename AT, typename BT, int MODE>
-__global__ __launch_bounds__(kBinBlock) void k_rb_bin(GroupArgs ga, DenseView d, uint32_t bshift,
-                                                      uint32_t nbd, uint32_t nbk,
+__global__ __launch_bounds__(kBinBlock) void k_rb_bin(GroupArgs ga, DenseView d, RbMap bm,
+                                                      uint32_t nbk,
                                                       uint16_t* __restrict__ loff, uint32_t nsc,
                                                       RbEnt<sizeof(BT)>* __restrict__ tmp) {
   constexpr uint32_t SC = rb_sc<BT>();
@@ -1112,7 +1142,7 @@ __global__ __launch_bounds__(kBinBlock) void k_rb_bin(GroupArgs ga, DenseView d,
       rk[q] = 0;
       if (keep) {
         emask |= 1u << q;
-        rk[q] = atomicAdd(&cnt[rb_bucket(d, kc[q], bshift, nbd)], 1u);
+        rk[q] = atomicAdd(&cnt[rb_bucket(d, kc[q], bm)], 1u);
       }
     }
     __syncthreads();  // table read and every entry counted
@@ -1126,7 +1156,7 @@ __global__ __launch_bounds__(kBinBlock) void k_rb_bin(GroupArgs ga, DenseView d,
       e.key = kc[q];
       if (sizeof(BT) == 8) reinterpret_cast<uint32_t*>(&e)[1] = 0;
       e.val = kv[q];
-      stg[cnt[rb_bucket(d, kc[q], bshift, nbd)] + rk[q]] = e;
+      stg[cnt[rb_bucket(d, kc[q], bm)] + rk[q]] = e;
     }
     __syncthreads();
     // the staged, bucket-sorted entries out as one coalesced stream.  The
@@ -1176,8 +1206,8 @@ __global__ __launch_bounds__(kBinBlock) void k_rb_bin(GroupArgs ga, DenseView d,
 constexpr int kApplyBlock = 1024;
 static_assert(kRbMaxSc <= (uint32_t)kApplyBlock, "one run per resolve thread");
 template <typename AT, typename BT, int MODE, int LOGS>
-__global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, uint32_t bshift,
-                                                            uint32_t nbd, uint32_t nbk,
+__global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, RbMap bm,
+                                                            uint32_t nbk,
                                                             const uint16_t* __restrict__ loff,
                                                             uint32_t nsc,
                                                             const RbEnt<sizeof(BT)>* __restrict__ tmp) {
@@ -1206,6 +1236,7 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
   __shared__ __attribute__((aligned(16))) uint32_t wtmp[kApplyBlock / 64];
   __shared__ uint32_t sent;
   const int tid = threadIdx.x;
+  const uint32_t nbd = bm.nbd;
   auto find = [&](uint32_t key) -> uint32_t {
     if (key == kEmpty32) return SLOTS;
     uint32_t h = fmix32(key) & (SLOTS - 1);
@@ -1321,7 +1352,7 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
   };
   uint32_t dlog = 0;
   while ((1u << dlog) < DSPAN) ++dlog;
-  const uint32_t halves = bshift > dlog ? 1u << (bshift - dlog) : 1u;  // direct passes per bucket
+  const uint32_t halves = (uint32_t)(((uint64_t)bm.span + DSPAN - 1) >> dlog);  // direct passes per bucket
   bool clean = false;  // best[] holds only values below tag << kPosBits
   uint32_t tag = 0;
   auto zero_best = [&]() {
@@ -1353,10 +1384,9 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
     const bool direct = MODE == 0 && b != nbd && !long_run && halves <= 4 &&
                         ne < (1u << kPosBits) - 1u;
     if (direct) {
-      const uint32_t bbase = b << bshift;
       uint32_t rel[RPT];
 #pragma unroll
-      for (int q = 0; q < RPT; ++q) rel[q] = (uint32_t)q < len ? x[q].key - d.key_begin - bbase : 0u;
+      for (int q = 0; q < RPT; ++q) rel[q] = (uint32_t)q < len ? rb_local(bm, x[q].key - d.key_begin) : 0u;
       // every pass only marks this lane's winners (bit q of win); the stores
       // of all passes go out together afterwards, so the random parameter
       // stores of the whole bucket are in flight at once
@@ -1374,7 +1404,7 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
           if ((uint32_t)q < len && (rel[q] >> dlog) == h)
             atomicMax(&best[rel[q] & (DSPAN - 1)], tg | (p0 + (uint32_t)q + 1u));
         for (uint32_t q = RPT; q < len; ++q) {  // a run's short tail, from memory
-          const uint32_t r = tmp[st + q].key - d.key_begin - bbase;
+          const uint32_t r = rb_local(bm, tmp[st + q].key - d.key_begin);
           if ((r >> dlog) == h) atomicMax(&best[r & (DSPAN - 1)], tg | (p0 + q + 1u));
         }
         __syncthreads();
@@ -1384,7 +1414,7 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
               best[rel[q] & (DSPAN - 1)] == (tg | (p0 + (uint32_t)q + 1u)))
             win |= 1ull << q;
         for (uint32_t q = RPT; q < len; ++q) {
-          const uint32_t r = tmp[st + q].key - d.key_begin - bbase;
+          const uint32_t r = rb_local(bm, tmp[st + q].key - d.key_begin);
           if ((r >> dlog) == h && best[r & (DSPAN - 1)] == (tg | (p0 + q + 1u))) win |= 1ull << q;
         }
         if (h + 1 < halves) __syncthreads();  // the table is read before the next pass
@@ -1891,26 +1921,25 @@ hipError_t launch_ovf_rehash(int vb, const Ovf& from, uint64_t from_cap, const O
 
 template <typename AT, typename BT, int MODE>
 static hipError_t rb_launch(const GroupArgs& ga, uint32_t nsc, const DenseView& d, const Ovf& o,
-                            uint32_t bshift, uint32_t nbd, int apply_log2, uint16_t* loff,
-                            void* tmp, hipStream_t st) {
-  const uint32_t nbk = nbd + 1;
+                            const RbMap& bm, int apply_log2, uint16_t* loff, void* tmp, hipStream_t st) {
+  const uint32_t nbk = bm.nbd + 1;
   auto* t = reinterpret_cast<RbEnt<sizeof(BT)>*>(tmp);
   // persistent grid, one 1024-thread workgroup per CU (~140 KiB LDS)
   const uint32_t gb = nsc < 256u ? nsc : 256u;
-  k_rb_bin<AT, BT, MODE><<<gb, kBinBlock, 0, st>>>(ga, d, bshift, nbd, nbk, loff, nsc, t);
+  k_rb_bin<AT, BT, MODE><<<gb, kBinBlock, 0, st>>>(ga, d, bm, nbk, loff, nsc, t);
   if (apply_log2 == 13)  // 2^13 slots: two workgroups per CU
-    k_rb_resolve<AT, BT, MODE, 13><<<512, kApplyBlock, 0, st>>>(d, o, bshift, nbd, nbk, loff, nsc, t);
+    k_rb_resolve<AT, BT, MODE, 13><<<512, kApplyBlock, 0, st>>>(d, o, bm, nbk, loff, nsc, t);
   else
-    k_rb_resolve<AT, BT, MODE, 14><<<256, kApplyBlock, 0, st>>>(d, o, bshift, nbd, nbk, loff, nsc, t);
+    k_rb_resolve<AT, BT, MODE, 14><<<256, kApplyBlock, 0, st>>>(d, o, bm, nbk, loff, nsc, t);
   return hipGetLastError();
 }
 
 hipError_t launch_rb_add(int dtype, int mode, const GroupArgs& ga, uint32_t nsc,
-                         const DenseView& d, const Ovf& o, uint32_t bshift, uint32_t nbd,
+                         const DenseView& d, const Ovf& o, const RbMap& bm,
                          int apply_log2, uint16_t* loff, void* tmp, hipStream_t st) {
   if (nsc == 0) return hipSuccess;
-  if (nbd + 1 > (uint32_t)kRbMaxBuckets || nsc > kRbMaxSc) return hipErrorInvalidValue;
-#define PSKV_RB(AT, BT, M) rb_launch<AT, BT, M>(ga, nsc, d, o, bshift, nbd, apply_log2, loff, tmp, st)
+  if (bm.nbd + 1 > (uint32_t)kRbMaxBuckets || nsc > kRbMaxSc || bm.nbd == 0) return hipErrorInvalidValue;
+#define PSKV_RB(AT, BT, M) rb_launch<AT, BT, M>(ga, nsc, d, o, bm, apply_log2, loff, tmp, st)
   if (mode == 0) {
     if (dtype == 0) return PSKV_RB(int, uint32_t, 0);
     if (dtype == 1) return PSKV_RB(float, uint32_t, 0);

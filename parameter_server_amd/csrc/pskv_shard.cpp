@@ -233,6 +233,7 @@ struct pskv_shard {
   // 8 x 1M keys: 1.43 ms against 1.75 ms staged, Get 1.37 against 1.44 ms.
   bool tune_pageable_dma = true;
   uint32_t tune_rb_tb = 0; // PSKV_RB_TB: K5 bucket bits (0 = by element count)
+  uint32_t tune_rb_wbits = 0; // PSKV_RB_WBITS: K5 window bits (0 = 11; >= bucket shift: contiguous buckets)
   // PSKV_INLINE: host calls of <= kInlineMax (Add) / kInlineGetMax (Get) keys in
   // all travel inside the kernel arguments (K8); 0 sends them through staging
   bool tune_inline = true;
@@ -427,8 +428,20 @@ uint32_t next_epoch(pskv_shard* s) {
   return ++s->epoch;
 }
 
+// Append batch b to v as consecutive pieces of at most kMaxPiece elements
+// (empty batches are dropped).  A batch applied piece by piece in order is the
+// same Add (last-wins / sums follow index order) and the same Get, and every
+// launch group then stays below 2^32 elements (the stamp index and the
+// per-launch element counts are 32 bits).
+constexpr uint64_t kMaxPiece = 1ull << 31;
+void push_pieces(std::vector<pskv_batch>& v, const pskv_batch& b, size_t vb) {
+  for (uint64_t off = 0; off < b.n; off += kMaxPiece)
+    v.push_back(pskv_batch{b.keys + off, static_cast<char*>(b.vals) + off * vb, std::min(kMaxPiece, b.n - off)});
+}
+
 // Split a batch list into launch groups: <= kMaxBatches batches and < 2^32
-// elements each (the stamp index is 32 bits).  Empty batches are dropped.
+// elements each.  Every batch holds at most kMaxPiece elements (push_pieces),
+// so every group takes at least one batch.
 std::vector<std::pair<size_t, size_t>> split_groups(const std::vector<pskv_batch>& v) {
   std::vector<std::pair<size_t, size_t>> out;
   size_t b = 0;
@@ -489,6 +502,14 @@ int radix_launch(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size
   const uint32_t bshift = bits > tb ? bits - tb : 0;
   const uint32_t nbd = (uint32_t)(((s->range - 1) >> bshift) + 1);
   const uint32_t nbk = nbd + 1;
+  // The buckets own windows of 2^wbits keys dealt round-robin (window w ->
+  // bucket w % nbd); wbits = bshift is one contiguous window per bucket.
+  RbMap bm;
+  bm.wbits = std::min<uint32_t>(bshift, s->tune_rb_wbits ? s->tune_rb_wbits : 11u);
+  bm.nbd = nbd;
+  bm.rcp = 1.0 / (double)nbd;
+  const uint64_t nwin = ((s->range - 1) >> bm.wbits) + 1;
+  bm.span = (uint32_t)std::min<uint64_t>(((nwin + nbd - 1) / nbd) << bm.wbits, 0xFFFFFFFFull);
   int apply_log2 = elems / nbd <= 2048 ? 13 : 14;
   if (s->tune_rb_apply_log2) apply_log2 = s->tune_rb_apply_log2;
   if (nbk > (uint32_t)kRbMaxBuckets) return fail(PSKV_EINVAL, "radix path: too many buckets");
@@ -499,7 +520,7 @@ int radix_launch(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size
   if (!rc) rc = ensure_scratch(s, &s->rb_ent, &s->rb_ent_bytes, (size_t)nsc * rb_superchunk(s->vb) * eb);
   if (rc) return rc;
   LaunchTimer t(s, PSKV_K_RADIX, elems);
-  PSKV_HIP(launch_rb_add(s->dtype, s->mode, ga, nsc, s->dview(), s->ovf, bshift, nbd, apply_log2,
+  PSKV_HIP(launch_rb_add(s->dtype, s->mode, ga, nsc, s->dview(), s->ovf, bm, apply_log2,
                          s->rb_loff, s->rb_ent, s->stream));
   t.done();
   s->n_general += 2;
@@ -957,7 +978,7 @@ int add_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
   for (auto& b : in) {
     if (b.n == 0) continue;
     if (!b.keys || !b.vals) return fail(PSKV_EINVAL, "pskv_add: null keys/vals with n > 0");
-    v.push_back(b);
+    push_pieces(v, b, (size_t)s->vb);
   }
   s->n_add++;
   if (v.empty()) return PSKV_OK;
@@ -1022,7 +1043,7 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
   for (auto& b : in) {
     if (b.n == 0) continue;
     if (!b.keys || !b.vals) return fail(PSKV_EINVAL, "pskv_get: null keys/out with n > 0");
-    v.push_back(b);
+    push_pieces(v, b, (size_t)s->vb);
   }
   s->n_get++;
   if (v.empty()) return PSKV_OK;
@@ -1201,6 +1222,7 @@ int pskv_shard_create_ex(int device, uint32_t key_begin, uint64_t key_end, int d
     const int v = std::atoi(e);
     if (v >= 1 && v <= 65536) s->tune_tile_grid = (uint32_t)v;
   }
+  if (const char* e = std::getenv("PSKV_RB_WBITS")) s->tune_rb_wbits = (uint32_t)std::max(0, std::min(31, std::atoi(e)));
   if (const char* e = std::getenv("PSKV_RB_TB")) {
     const int v = std::atoi(e);
     if (v >= 1 && v <= 11) s->tune_rb_tb = (uint32_t)v;

@@ -1059,3 +1059,42 @@ def test_inline_get_reply_paths(cuda, oracle_mod, spin, monkeypatch):
                 sh.set_timing(True)
             q = rng.integers(0, 1 << 17, size=int(rng.integers(1, 513))).astype(np.uint32)
             assert_bits_equal(sh.get(q), ref.get(q), f"get {i}")
+
+
+def test_batch_beyond_2_to_32_elements(cuda):
+    """Maximum sizes: ONE device batch of 2^32 + 2^20 elements (keys i mod 2^32
+    over a shard of the whole uint32 key space, int32 values), so the batch is
+    cut into pieces below the 32-bit per-launch counts and the first 2^20 keys
+    are written twice — the later occurrence must win.  Add without a hint (K5
+    over ~525 K super-chunks), then a Get of the same 2^32 + 2^20 keys.  (The
+    tensors are filled and checked in pieces of 2^28: torch's own kernels are
+    not used on more than 2^31 elements at once.)"""
+    import torch
+
+    import parameter_server_amd as ps
+
+    n, P = (1 << 32) + (1 << 20), 1 << 28
+    keys = torch.empty(n, dtype=torch.int32, device=cuda)
+    vals = torch.empty(n, dtype=torch.int32, device=cuda)
+    for off in range(0, n, P):
+        m = min(P, n - off)
+        k = torch.arange(off, off + m, dtype=torch.int64, device=cuda) % (1 << 32)
+        keys[off:off + m] = torch.where(k >= 1 << 31, k - (1 << 32), k).to(torch.int32)  # uint32 bits
+        vals[off:off + m] = 1 if off < 1 << 32 else 2
+    assert int(keys[(1 << 32) + 5]) == 5 and int(keys[(1 << 31) + 1]) == -(1 << 31) + 1
+    with ps.Shard(0, 1 << 32, np.int32) as sh:
+        sh.add(keys, vals)
+        del vals
+        out = sh.get(keys)
+        torch.cuda.synchronize()
+        sh.sync()
+    del keys
+    # keys below 2^20 were pushed twice (value 1, then 2): they read 2 in both places
+    for off in range(0, n, P):
+        m = min(P, n - off)
+        want = torch.ones(m, dtype=torch.int32, device=cuda)
+        lo = max(0, min(m, (1 << 20) - off))
+        want[:lo] = 2                         # the first 2^20 positions
+        if off >= 1 << 32:
+            want[:] = 2                       # the repeated tail
+        assert torch.equal(out[off:off + m], want), off
