@@ -98,13 +98,15 @@ hipError_t launch_general_commit(int vb, const GroupArgs& ga, uint32_t nwg, cons
 hipError_t launch_ovf_rehash(int vb, const Ovf& from, uint64_t from_cap, const Ovf& to,
                              hipStream_t st);
 // K5 key buckets: windows of 2^wbits keys of the owned range, window w in
-// bucket w % nbd (nbd >= 1); rcp = 1.0 / nbd; span = keys per bucket at most
+// bucket w % nbd (1 <= nbd < 2^12, windows < 2^21: wbits >= 11 or a range
+// below 2^32); magic = ceil(2^32 / nbd); span = keys per bucket at most
 // (ceil(windows / nbd) << wbits), the extent of a bucket's local index.
 struct RbMap {
   uint32_t wbits;
   uint32_t nbd;
-  double rcp;
+  uint32_t magic;
   uint32_t span;
+  int32_t nlog;  // log2(nbd) when nbd is a power of two (then magic is unused), else -1
 };
 
 // K5 radix-bucket general Add (2 launches: K5a bin, K5b resolve).  `ga`

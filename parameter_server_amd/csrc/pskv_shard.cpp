@@ -234,6 +234,7 @@ struct pskv_shard {
   bool tune_pageable_dma = true;
   uint32_t tune_rb_tb = 0; // PSKV_RB_TB: K5 bucket bits (0 = by element count)
   uint32_t tune_rb_wbits = 0; // PSKV_RB_WBITS: K5 window bits (0 = 11; >= bucket shift: contiguous buckets)
+  uint32_t tune_rb_nbd = 0;   // PSKV_RB_NBD: K5 dense bucket count (0 = by the rule; tuning)
   // PSKV_INLINE: host calls of <= kInlineMax (Add) / kInlineGetMax (Get) keys in
   // all travel inside the kernel arguments (K8); 0 sends them through staging
   bool tune_inline = true;
@@ -500,15 +501,19 @@ int radix_launch(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size
   while (tb < tmax && (elems >> (per + tb)) != 0) ++tb;
   if (s->tune_rb_tb) tb = s->tune_rb_tb;
   const uint32_t bshift = bits > tb ? bits - tb : 0;
-  const uint32_t nbd = (uint32_t)(((s->range - 1) >> bshift) + 1);
+  uint32_t nbd = (uint32_t)(((s->range - 1) >> bshift) + 1);
+  if (s->tune_rb_nbd) nbd = s->tune_rb_nbd;
   const uint32_t nbk = nbd + 1;
   // The buckets own windows of 2^wbits keys dealt round-robin (window w ->
   // bucket w % nbd); wbits = bshift is one contiguous window per bucket.
   RbMap bm;
   bm.wbits = std::min<uint32_t>(bshift, s->tune_rb_wbits ? s->tune_rb_wbits : 11u);
   bm.nbd = nbd;
-  bm.rcp = 1.0 / (double)nbd;
-  const uint64_t nwin = ((s->range - 1) >> bm.wbits) + 1;
+  bm.nlog = -1;
+  for (int l = 0; l < 12; ++l)
+    if (nbd == (1u << l)) bm.nlog = l;
+  bm.magic = nbd > 1 ? (uint32_t)(((1ull << 32) + nbd - 1) / nbd) : 0u;  // nbd = 1 takes the shift path
+  const uint64_t nwin = ((s->range - 1) >> bm.wbits) + 1;  // < 2^21: wbits = 11, or wbits = bshift and nwin = nbd
   bm.span = (uint32_t)std::min<uint64_t>(((nwin + nbd - 1) / nbd) << bm.wbits, 0xFFFFFFFFull);
   int apply_log2 = elems / nbd <= 2048 ? 13 : 14;
   if (s->tune_rb_apply_log2) apply_log2 = s->tune_rb_apply_log2;
@@ -1223,6 +1228,8 @@ int pskv_shard_create_ex(int device, uint32_t key_begin, uint64_t key_end, int d
     if (v >= 1 && v <= 65536) s->tune_tile_grid = (uint32_t)v;
   }
   if (const char* e = std::getenv("PSKV_RB_WBITS")) s->tune_rb_wbits = (uint32_t)std::max(0, std::min(31, std::atoi(e)));
+  if (const char* e = std::getenv("PSKV_RB_NBD"))
+    if (std::atoi(e) > 0) s->tune_rb_nbd = (uint32_t)std::min(kRbMaxBuckets - 1, std::atoi(e));
   if (const char* e = std::getenv("PSKV_RB_TB")) {
     const int v = std::atoi(e);
     if (v >= 1 && v <= 11) s->tune_rb_tb = (uint32_t)v;
