@@ -67,6 +67,9 @@ __device__ __forceinline__ bool chunk_of(const Win& w, uint32_t c, int& j, uint3
 // MODE 3: K2g add honouring `covered` (keys only for covered windows)
 // MODE 4: K2g add, keys and values interleaved per u (load k,v ; k,v ; ...)
 // MODE 5: K2g add pattern but the values go to `out` (contiguous) instead of the param windows
+// MODE 6: MODE 3 behind a K2g-style prologue: waves 0-1 load the first and last
+//         key of every window (128 dependent scattered loads) and the workgroup
+//         waits for them (barrier) before its chunk loads
 template <int MODE, int U, bool STNT, bool KNT = true, bool VNT = true>
 __global__ __launch_bounds__(kB) void k_mix(const uint32_t* __restrict__ keys,
                                             const uint32_t* __restrict__ vals,
@@ -79,6 +82,15 @@ __global__ __launch_bounds__(kB) void k_mix(const uint32_t* __restrict__ keys,
   const size_t g0 = (size_t)j * kN + base;  // element index in the concatenation
   const uint32_t first = w.first[j];
   bool b = false;
+  if (MODE == 6) {
+    __shared__ uint32_t s_fl[2 * kJ];
+    if (t < 2 * kJ) {
+      const int q = (int)t % kJ;
+      s_fl[t] = keys[(size_t)q * kN + (t < kJ ? 0 : kN - 1)];
+    }
+    __syncthreads();
+    b |= s_fl[j] != first;
+  }
   if (MODE == 0) {
     u32x4 k[U], v[U];
 #pragma unroll
@@ -107,7 +119,7 @@ __global__ __launch_bounds__(kB) void k_mix(const uint32_t* __restrict__ keys,
       st<STNT>(param + k0, v[u]);
     }
   } else {
-    const bool cov = MODE == 3 && w.covered[j];
+    const bool cov = (MODE == 3 || MODE == 6) && w.covered[j];
     u32x4 k[U], v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) k[u] = ld<KNT>(keys + g0 + (u * kB + t) * 4);
@@ -187,6 +199,7 @@ int main() {
   for (int rep = 0; rep < 2; ++rep) {
     run("K1 gather keys+param->out", k_mix<0, 8, false>, 8, 12, 12);
     run("K2g add keys+vals->param (plain st)", k_mix<1, 8, false>, 8, 12, 12);
+    run("K2g covered-skip behind a first/last prologue", k_mix<6, 8, false>, 8, 12, 4);
     run("K2g add keys+vals->param (nt st)", k_mix<1, 8, true>, 8, 12, 12);
     run("K2g add covered-skip (plain st)", k_mix<3, 8, false>, 8, 12, 4);
     run("K2g add interleaved loads (plain st)", k_mix<4, 8, false>, 8, 12, 12);
