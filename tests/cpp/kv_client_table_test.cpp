@@ -34,6 +34,7 @@
 #include <thread>
 #include <vector>
 
+#include "ps/consistent_hashing_partition_manager.hpp"
 #include "ps/kv_client_table.hpp"
 #include "ps/range_partition_manager.hpp"
 #include "ps/server_thread.hpp"
@@ -306,20 +307,27 @@ float ValueOf(int w, int it, Key k) { return (float)((it * 131 + (int)(k % 977))
 
 bool InSet(Key k, int it) { return ((k * 2654435761u) >> 7 ^ (uint32_t)it * 40503u) % 3 != 0; }
 
-void System(ModelType model_type, const char* model_name, StorageType storage_type) {
-  std::printf("[ RUN ] System %s (%s storage)\n", model_name,
-              storage_type == StorageType::Hip ? "hip" : "cpu");
+void System(ModelType model_type, const char* model_name, StorageType storage_type, bool hashed = false) {
+  std::printf("[ RUN ] System %s (%s storage, %s partitioning)\n", model_name,
+              storage_type == StorageType::Hip ? "hip" : "cpu", hashed ? "consistent-hash" : "range");
   const int W = 4, S = 3, I = 12;
   const Key K = 3000;  // range keys [0, K); each worker also owns one key >= K
   const uint32_t model_id = 0;
   std::vector<uint32_t> sids = {0, 1, 2};
-  RangeShardMap map(sids, {{0, 1000}, {1000, 2000}, {2000, 3000}});
+  RangeShardMap range_map(sids, {{0, 1000}, {1000, 2000}, {2000, 3000}});
+  // the reference Engine's default partitioner: every server owns [0, K) and
+  // the keys >= K land in the overflow table of whichever server they hash to
+  ConsistentHashShardMap hash_map(sids);
+  const AbstractPartitionManager& map = hashed ? static_cast<const AbstractPartitionManager&>(hash_map)
+                                               : static_cast<const AbstractPartitionManager&>(range_map);
   std::vector<std::unique_ptr<ServerThread>> servers;
   for (auto id : sids) servers.emplace_back(new ServerThread(id));
   ReplyQueue replies;
-  auto storages = CreateTable<float>(
-      servers, map, model_id, model_type, storage_type, /*staleness=*/1, &replies, PSKV_ASSIGN,
-      [](StorageType) { return std::unique_ptr<AbstractStorage>(new LocalMapStorage<float>()); });
+  auto cpu = [](StorageType) { return std::unique_ptr<AbstractStorage>(new LocalMapStorage<float>()); };
+  auto storages = hashed ? CreateTable<float>(servers, hash_map, K, model_id, model_type, storage_type,
+                                              /*staleness=*/1, &replies, PSKV_ASSIGN, cpu)
+                         : CreateTable<float>(servers, range_map, model_id, model_type, storage_type,
+                                              /*staleness=*/1, &replies, PSKV_ASSIGN, cpu);
   // ResetWorker: every model tracks the W worker threads (server/abstract_model.hpp)
   std::vector<uint32_t> tids;
   for (int w = 0; w < W; ++w) tids.push_back(100 + w);
@@ -446,6 +454,9 @@ int main(int argc, char** argv) {
   System(ModelType::ASP, "ASP", st);
   System(ModelType::SSP, "SSP", st);
   System(ModelType::BSP, "BSP", st);
+  System(ModelType::ASP, "ASP", st, /*hashed=*/true);
+  System(ModelType::SSP, "SSP", st, /*hashed=*/true);
+  System(ModelType::BSP, "BSP", st, /*hashed=*/true);
   std::printf("%d passed, %d failed\n", g_pass.load(), g_fail.load());
   return g_fail.load() ? 1 : 0;
 }
