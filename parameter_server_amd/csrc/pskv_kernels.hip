@@ -1758,7 +1758,20 @@ __global__ __launch_bounds__(kInlineMax) void k_inline_add(InlineAdd a, DenseVie
 template <typename VT>
 __global__ __launch_bounds__(64) void k_inline_get(InlineGet a, DenseView d, Ovf o, VT* out,
                                                    unsigned int* done, unsigned int seq) {
-  for (uint32_t i = threadIdx.x; i < a.n; i += 64) out[i] = load_one<VT>(d, o, a.keys[i]);
+  // every lane's gathers first (independent, all in flight), then the reply
+  // stores: interleaved, each store would wait for its own load
+  constexpr int PER = kInlineGetMax / 64;
+  VT v[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const uint32_t i = threadIdx.x + 64u * q;
+    v[q] = i < a.n ? load_one<VT>(d, o, a.keys[i]) : VT(0);
+  }
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const uint32_t i = threadIdx.x + 64u * q;
+    if (i < a.n) out[i] = v[q];
+  }
   if (done) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the reply before the flag
     // MI355X_MICROARCH.md "Compiler hazard": keep the wait after the write-back

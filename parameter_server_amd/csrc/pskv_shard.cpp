@@ -240,11 +240,11 @@ struct pskv_shard {
   bool tune_inline = true;
   // PSKV_INLINE_ADD_CHUNKS / PSKV_INLINE_GET_CHUNKS: K8 launches per call at
   // most (1..kInlineMaxChunks).  Measured (tools/micro/small_latency.cpp): an
-  // Add launch costs ~3-7 us of enqueue, the staged path ~48-65 us, so up to 8
-  // (2048 keys) win; a Get launch beyond the first costs ~10 us (the reply
-  // goes over PCIe as it is written) against ~32 us staged, so one.
+  // Add launch costs ~3-7 us of enqueue against ~45-65 us staged, so up to 8
+  // (2048 keys); a Get launch beyond the first ~4-12 us against ~32 us staged
+  // (1024 keys: 16 us; 2048 keys: 25-35 us over boxes), so up to 2 (1024 keys).
   int tune_inline_add_chunks = 8;
-  int tune_inline_get_chunks = 1;
+  int tune_inline_get_chunks = 2;
   void* ireply = nullptr;  // page-locked reply buffer of inline Gets (kInlineGetMax values)
   bool tune_ispin = true;  // PSKV_ISPIN: poll the reply's sequence word instead of a stream wait
   unsigned int ireply_seq = 0;

@@ -1003,12 +1003,12 @@ def test_inline_accumulate_sequential_bits(cuda, dt, max_n):
     assert_bits_equal(got_ovf, np.array([want_ovf[int(x)] for x in ok], dt), "inline accumulate (overflow)")
 
 
-@pytest.mark.parametrize("n", [255, 256, 257, 511, 512, 513, 2048, 2049])
+@pytest.mark.parametrize("n", [255, 256, 257, 511, 512, 513, 1024, 1025, 2048, 2049])
 def test_inline_size_boundaries(cuda, oracle_mod, n):
     """Messages at and beyond the inline limits (an Add goes out in launches
-    of 256 keys, at most 8 of them, so 2048 keys; a Get of at most 512 keys in
-    one launch; grouped calls count their batches together) agree with the
-    oracle, duplicates straddling launch boundaries included."""
+    of 256 keys, at most 8 of them (2048 keys), a Get in launches of 512 keys,
+    at most 2 of them (1024 keys); grouped calls count their batches together)
+    agree with the oracle, duplicates straddling launch boundaries included."""
     import parameter_server_amd as ps
     from parameter_server_amd import _lib
 
@@ -1033,7 +1033,7 @@ def test_inline_size_boundaries(cuda, oracle_mod, n):
         adds = sh.kernel_time(_lib.PSKV_K_INLINE_ADD)["launches"]
         gets = sh.kernel_time(_lib.PSKV_K_INLINE_GET)["launches"]
     assert adds == (2 * -(-n // 256) if n <= 2048 else 0)
-    assert gets == (2 if n <= 512 else 0)
+    assert gets == (2 * -(-n // 512) if n <= 1024 else 0)
     assert_bits_equal(got, ref.get(k), "single")
     for p, o in zip(parts, outs):
         assert_bits_equal(o, ref.get(k2[p]), "grouped")
