@@ -397,13 +397,15 @@ void System(ModelType model_type, const char* model_name, StorageType storage_ty
     });
   }
   for (auto& t : workers) t.join();
-  for (auto& s : servers) s->Stop();  // FIFO: every queued message is handled first
-  stop = true;
-  receiver.join();
+  // drain the sender first: every worker message (the last Clocks, which
+  // trigger BSP's final flush) is in its server's FIFO before kExit is
   Message ex;
   ex.meta.flag = Flag::kExit;
   sender_queue.Push(ex);
   sender.join();
+  for (auto& s : servers) s->Stop();  // FIFO: every queued message is handled first
+  stop = true;
+  receiver.join();
   EXPECT(mismatches.load() == 0);
   if (model_type == ModelType::SSP) std::printf("  SSP released %d buffered requests\n", released.load());
 
