@@ -72,6 +72,12 @@ uint64_t next_pow2(uint64_t x) {
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 constexpr uint64_t kDefaultOverflowSlots = 1ull << 16;
+// see tune_dma_min_bytes: measured per call (tools/micro/small_latency.cpp,
+// f64): Add via the pinned copy 6-7 us up to 4 Ki keys, 338 us at 1 Mi keys
+// (direct DMA 48 / 366 us), DMA ahead from ~4 Mi keys; Get via the copy 18 us
+// up to 2 Ki keys (DMA 26), DMA ahead from 4 Ki keys
+constexpr size_t kDefaultDmaMinBytes = 32ull << 20;
+constexpr size_t kDefaultDmaMinBytesGet = 32ull << 10;
 
 struct TimedLaunch {
   int kernel;
@@ -176,6 +182,21 @@ class HostPool {
 
 constexpr size_t kPieceBytes = 1 << 20;   // one pool task
 constexpr size_t kWindowBytes = 8 << 20;  // one H2D / D2H DMA while the next window is copied
+constexpr size_t kInlineCopyBytes = 256 << 10;  // smaller windows are copied by the calling thread
+
+// Run fn over pieces [b, e) of `pieces`: on the calling thread when they are
+// small (waking the pool costs more than copying a few hundred KiB), on the
+// pool otherwise.
+template <typename PieceT, typename Fn>
+void run_pieces(std::vector<PieceT>& pieces, size_t b, size_t e, const Fn& fn) {
+  size_t bytes = 0;
+  for (size_t i = b; i < e; ++i) bytes += pieces[i].bytes;
+  if (bytes < kInlineCopyBytes) {
+    for (size_t i = b; i < e; ++i) fn(pieces[i]);
+    return;
+  }
+  HostPool::get().run(e - b, [&](size_t t) { fn(pieces[b + t]); });
+}
 
 }  // namespace
 
@@ -232,6 +253,11 @@ struct pskv_shard {
   // pinned staging first; 0 selects the staging path.  cfg-2-shaped Add of
   // 8 x 1M keys: 1.43 ms against 1.75 ms staged, Get 1.37 against 1.44 ms.
   bool tune_pageable_dma = true;
+  // PSKV_DMA_MIN_BYTES / PSKV_DMA_MIN_BYTES_GET: pageable host Adds / Gets of
+  // at least this many bytes (keys + values) take the direct DMA; smaller ones
+  // the pinned staging copy
+  size_t tune_dma_min_bytes = kDefaultDmaMinBytes;
+  size_t tune_dma_min_bytes_get = kDefaultDmaMinBytesGet;
   uint32_t tune_rb_tb = 0; // PSKV_RB_TB: K5 bucket bits (0 = by element count)
   uint32_t tune_rb_wbits = 0; // PSKV_RB_WBITS: K5 window bits (0 = 11; >= bucket shift: contiguous buckets)
   uint32_t tune_rb_nbd = 0;   // PSKV_RB_NBD: K5 dense bucket count (0 = by the rule; tuning)
@@ -240,10 +266,11 @@ struct pskv_shard {
   bool tune_inline = true;
   // PSKV_INLINE_ADD_CHUNKS / PSKV_INLINE_GET_CHUNKS: K8 launches per call at
   // most (1..kInlineMaxChunks).  Measured (tools/micro/small_latency.cpp): an
-  // Add launch costs ~3-7 us of enqueue against ~45-65 us staged, so up to 8
-  // (2048 keys); a Get launch beyond the first ~4-12 us against ~32 us staged
-  // (1024 keys: 16 us; 2048 keys: 25-35 us over boxes), so up to 2 (1024 keys).
-  int tune_inline_add_chunks = 8;
+  // Add launch costs ~3-7 us of enqueue, and the pinned staging copy returns
+  // in 6-8 us up to 4 Ki keys (its DMA and kernels run on), so one launch;
+  // a Get launch beyond the first ~4-12 us against ~20 us through the copy
+  // (1024 keys: 16 us), so up to 2 (1024 keys).
+  int tune_inline_add_chunks = 1;
   int tune_inline_get_chunks = 2;
   void* ireply = nullptr;  // page-locked reply buffer of inline Gets (kInlineGetMax values)
   bool tune_ispin = true;  // PSKV_ISPIN: poll the reply's sequence word instead of a stream wait
@@ -722,12 +749,11 @@ void add_pieces(std::vector<Piece>& out, const void* src, char* dst, size_t byte
 // device as soon as it is staged, so the copy of window w+1 overlaps the H2D
 // of window w.  Pieces must be in increasing staging order.
 int pipelined_h2d(pskv_shard* s, std::vector<Piece>& pieces, char* h, char* d) {
-  HostPool& pool = HostPool::get();
   size_t i = 0;
   while (i < pieces.size()) {
     size_t j = i, win = 0;
     while (j < pieces.size() && (win < kWindowBytes || j == i)) win += pieces[j++].bytes;
-    pool.run(j - i, [&](size_t t) { copy_piece(pieces[i + t], s->key_begin, s->range); });
+    run_pieces(pieces, i, j, [&](Piece& p) { copy_piece(p, s->key_begin, s->range); });
     char* lo = pieces[i].dst;
     char* hi = pieces[j - 1].dst + pieces[j - 1].bytes;
     PSKV_HIP(hipMemcpyAsync(d + (lo - h), lo, (size_t)(hi - lo), hipMemcpyHostToDevice, s->stream));
@@ -757,7 +783,11 @@ int stage_host_batches(pskv_shard* s, const std::vector<pskv_batch>& in,
   for (auto& b : in) bytes += round16(b.n * 4) + round16(b.n * (size_t)s->vb);
   bool locked = true;
   for (const auto& b : in) locked = locked && is_pinned(b.keys) && is_pinned(b.vals);
-  const bool pinned = locked || s->tune_pageable_dma;
+  // pageable buffers: DMA'd directly only when large (the runtime's pageable
+  // copy has a high fixed cost and blocks until done); smaller ones are copied
+  // into pinned staging and DMA'd asynchronously (the call returns after the
+  // host copy)
+  const bool pinned = locked || (s->tune_pageable_dma && bytes >= s->tune_dma_min_bytes);
   int rc = pinned ? PSKV_OK : ensure_hstage(s, bytes);
   if (rc) return rc;
   rc = ensure_dstage(s, bytes);
@@ -1064,7 +1094,11 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
   size_t out_off = 0;
   bool pinned = !device;
   for (const auto& b : v) pinned = pinned && is_pinned(b.keys) && is_pinned(b.vals);
-  pinned = pinned || (!device && s->tune_pageable_dma);
+  if (!device && !pinned && s->tune_pageable_dma) {  // pageable: direct DMA only when large
+    size_t bytes = 0;
+    for (auto& b : v) bytes += round16(b.n * 4) + round16(b.n * (size_t)s->vb);
+    pinned = bytes >= s->tune_dma_min_bytes_get;
+  }
   if (pinned) {
     // page-locked caller buffers: keys DMA'd in directly, values DMA'd out directly
     size_t bytes = 0;
@@ -1163,11 +1197,10 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
                               hipMemcpyDeviceToHost, s->stream));
       PSKV_HIP(hipEventRecord(s->win_events[w], s->stream));
     }
-    HostPool& pool = HostPool::get();
     for (size_t w = 0; w < wins.size(); ++w) {
       PSKV_HIP(hipEventSynchronize(s->win_events[w]));
-      pool.run(wins[w].second - wins[w].first,
-               [&](size_t t) { copy_piece(pieces[wins[w].first + t], s->key_begin, s->range); });
+      run_pieces(pieces, wins[w].first, wins[w].second,
+                 [&](Piece& p) { copy_piece(p, s->key_begin, s->range); });
     }
   }
   return PSKV_OK;
@@ -1217,6 +1250,8 @@ int pskv_shard_create_ex(int device, uint32_t key_begin, uint64_t key_end, int d
   if (const char* e = std::getenv("PSKV_NT")) s->tune_nt = std::atoi(e) != 0;
   if (const char* e = std::getenv("PSKV_NTP")) s->tune_ntp = std::atoi(e) != 0;
   if (const char* e = std::getenv("PSKV_PAGEABLE_DMA")) s->tune_pageable_dma = std::atoi(e) != 0;
+  if (const char* e = std::getenv("PSKV_DMA_MIN_BYTES")) s->tune_dma_min_bytes = (size_t)std::atoll(e);
+  if (const char* e = std::getenv("PSKV_DMA_MIN_BYTES_GET")) s->tune_dma_min_bytes_get = (size_t)std::atoll(e);
   if (const char* e = std::getenv("PSKV_INLINE")) s->tune_inline = std::atoi(e) != 0;
   if (const char* e = std::getenv("PSKV_INLINE_ADD_CHUNKS"))
     s->tune_inline_add_chunks = std::max(1, std::min(kInlineMaxChunks, std::atoi(e)));

@@ -871,8 +871,11 @@ def test_pinned_host_buffers_direct_dma(cuda, oracle_mod, mode, pageable_path, m
     pageable buffers, for sorted, dense and unsorted batches, Add and Get."""
     import parameter_server_amd as ps
 
-    # pageable buffers go by direct DMA (default) or through pinned staging
+    # pageable buffers go by direct DMA (forced at every size: by default only
+    # calls of >= 32 MiB (Add) / 32 KiB (Get) do) or through pinned staging
     monkeypatch.setenv("PSKV_PAGEABLE_DMA", "1" if pageable_path == "dma" else "0")
+    monkeypatch.setenv("PSKV_DMA_MIN_BYTES", "0")
+    monkeypatch.setenv("PSKV_DMA_MIN_BYTES_GET", "0")
     rng = np.random.default_rng(71)
     kb, size = 10, 400_000
     batches = []
@@ -973,17 +976,18 @@ def test_inline_small_messages_assign(cuda, oracle_mod, dt, monkeypatch):
     assert_bits_equal(big_staged, ref.get(q), "full read after staged adds")
 
 
-@pytest.mark.parametrize("max_n", [256, 2048])
+@pytest.mark.parametrize("max_n,chunks", [(256, "1"), (2048, "8")])
 @pytest.mark.parametrize("dt", [np.int32, np.float32, np.float64])
-def test_inline_accumulate_sequential_bits(cuda, dt, max_n):
+def test_inline_accumulate_sequential_bits(cuda, dt, max_n, chunks, monkeypatch):
     """K8 accumulate: the first occurrence of a key adds every occurrence in
     index order, so the result equals sequential accumulation in the value
     dtype BIT FOR BIT (np.add.at), overflow keys included."""
     import parameter_server_amd as ps
 
+    monkeypatch.setenv("PSKV_INLINE_ADD_CHUNKS", chunks)  # 8: messages of up to 8 launches
     rng = np.random.default_rng(909)
     kb, ke = 0, 2048
-    msgs = _small_messages(rng, kb, ke, 80, max_n=max_n)  # 2048: several launches per message
+    msgs = _small_messages(rng, kb, ke, 80, max_n=max_n)
     want = np.zeros(ke - kb, dt)
     want_ovf = {}
     with ps.Shard(kb, ke, dt, mode="accumulate", overflow_slots=64) as sh:
@@ -1005,10 +1009,10 @@ def test_inline_accumulate_sequential_bits(cuda, dt, max_n):
 
 @pytest.mark.parametrize("n", [255, 256, 257, 511, 512, 513, 1024, 1025, 2048, 2049])
 def test_inline_size_boundaries(cuda, oracle_mod, n):
-    """Messages at and beyond the inline limits (an Add goes out in launches
-    of 256 keys, at most 8 of them (2048 keys), a Get in launches of 512 keys,
-    at most 2 of them (1024 keys); grouped calls count their batches together)
-    agree with the oracle, duplicates straddling launch boundaries included."""
+    """Messages at and beyond the inline limits (an Add of at most 256 keys in
+    one launch, a Get in launches of 512 keys, at most 2 of them, so 1024
+    keys; grouped calls count their batches together; beyond them the pinned
+    staging copy) agree with the oracle."""
     import parameter_server_amd as ps
     from parameter_server_amd import _lib
 
@@ -1032,7 +1036,7 @@ def test_inline_size_boundaries(cuda, oracle_mod, n):
         got = sh.get(k)
         adds = sh.kernel_time(_lib.PSKV_K_INLINE_ADD)["launches"]
         gets = sh.kernel_time(_lib.PSKV_K_INLINE_GET)["launches"]
-    assert adds == (2 * -(-n // 256) if n <= 2048 else 0)
+    assert adds == (2 if n <= 256 else 0)
     assert gets == (2 * -(-n // 512) if n <= 1024 else 0)
     assert_bits_equal(got, ref.get(k), "single")
     for p, o in zip(parts, outs):

@@ -67,9 +67,17 @@ def main():
             h_pin[n:].copy_(d_buf[n:], non_blocking=True)
     t = timeit(duplex)
     print(f"raw duplex pinned {8 * n / t / 1e9:7.1f} GB/s (4 B/key each way, two streams)")
-    variants = [("pageable", hk, hv, ho, "0"), ("pageable-dma", hk, hv, ho, "1"), ("pinned", pk, pv, po, "0")]
-    for name, K, Vv, O, knob in variants:
+    # pageable: staged copy always / direct DMA always / the library's size
+    # thresholds (PSKV_DMA_MIN_BYTES[_GET]); page-locked: direct DMA
+    variants = [("pageable", hk, hv, ho, ("0", None)), ("pageable-dma", hk, hv, ho, ("1", "0")),
+                ("pageable-def", hk, hv, ho, ("1", None)), ("pinned", pk, pv, po, ("0", None))]
+    for name, K, Vv, O, (knob, th) in variants:
         os.environ["PSKV_PAGEABLE_DMA"] = knob
+        for e in ("PSKV_DMA_MIN_BYTES", "PSKV_DMA_MIN_BYTES_GET"):
+            if th is None:
+                os.environ.pop(e, None)
+            else:
+                os.environ[e] = th
         with ps.Shard(0, space, np.float32) as sh:
             ta = timeit(lambda: sh.add_grouped(list(zip(K, Vv))))
             tg = timeit(lambda: sh.get_grouped(list(zip(K, O))))

@@ -28,21 +28,28 @@ static void die(int rc, const char* what) {
 }
 
 int main() {
-  const int sizes[] = {1, 16, 64, 256, 512, 1024, 2048, 4096};
-  const int reps = 2000;
+  const int sizes[] = {1, 16, 64, 256, 512, 1024, 2048, 4096, 16384, 65536, 262144, 1048576, 4194304};
+  const int reps = 600;
   std::mt19937 rng(7);
   std::printf("%-10s %6s %10s %10s %12s %12s\n", "path", "keys", "add_us", "get_us", "add+get_us",
               "get_only_us");
-  // variants: inline with the polled reply, inline with a stream wait
-  // (PSKV_ISPIN=0), staged (PSKV_INLINE=0)
-  // and inline with up to 16 launches per call for both (PSKV_INLINE_*_CHUNKS=16)
-  const char* names[] = {"inline", "inline-sync", "staged", "inline-x16"};
+  // variants: the defaults (inline small messages, pinned staging copy for
+  // medium ones, direct DMA of pageable buffers from PSKV_DMA_MIN_BYTES on);
+  // inline Gets waiting on the stream (PSKV_ISPIN=0); no inline path with
+  // every pageable buffer DMA'd directly; no inline path with every pageable
+  // buffer copied into pinned staging
+  const char* names[] = {"default", "inline-sync", "dma-always", "copy-always"};
+  for (int pass = 0; pass < 2; ++pass)  // pass 0 warms the runtime up (its pageable-copy paths); pass 1 prints
   for (int var = 0; var < 4; ++var) {
-    setenv("PSKV_INLINE", var != 2 ? "1" : "0", 1);
+    setenv("PSKV_INLINE", var < 2 ? "1" : "0", 1);
     setenv("PSKV_ISPIN", var != 1 ? "1" : "0", 1);
-    if (var == 3) {
-      setenv("PSKV_INLINE_ADD_CHUNKS", "16", 1);
-      setenv("PSKV_INLINE_GET_CHUNKS", "16", 1);
+    const char* th = var == 2 ? "0" : var == 3 ? "1000000000000" : nullptr;  // nullptr: library defaults
+    if (th) {
+      setenv("PSKV_DMA_MIN_BYTES", th, 1);
+      setenv("PSKV_DMA_MIN_BYTES_GET", th, 1);
+    } else {
+      unsetenv("PSKV_DMA_MIN_BYTES");
+      unsetenv("PSKV_DMA_MIN_BYTES_GET");
     }
     pskv_shard* s = nullptr;
     die(pskv_shard_create(0, 0, 1000000, PSKV_F64, PSKV_ASSIGN, &s), "create");
@@ -50,7 +57,8 @@ int main() {
       std::vector<uint32_t> k(n);
       std::vector<double> v(n), out(n);
       std::vector<double> ta, tg, tb, to;
-      for (int r = 0; r < reps + 50; ++r) {
+      const int nrep = std::max(20, std::min(reps, (int)((1 << 22) / n)));
+      for (int r = 0; r < nrep + 10; ++r) {
         for (int i = 0; i < n; ++i) {
           k[i] = rng() % 1000000;
           v[i] = (double)r + i;
@@ -63,7 +71,7 @@ int main() {
         const double t2 = now_us();
         die(pskv_get(s, k.data(), n, out.data(), PSKV_HOST), "get");  // nothing queued before it
         const double t3 = now_us();
-        if (r >= 50) {
+        if (r >= 10) {
           ta.push_back(t1 - t0);
           tg.push_back(t2 - t1);
           tb.push_back(t2 - t0);
@@ -80,8 +88,9 @@ int main() {
         std::nth_element(x.begin(), x.begin() + x.size() / 2, x.end());
         return x[x.size() / 2];
       };
-      std::printf("%-10s %6d %10.2f %10.2f %12.2f %12.2f\n", names[var], n, med(ta), med(tg), med(tb),
-                  med(to));
+      if (pass == 1)
+        std::printf("%-10s %6d %10.2f %10.2f %12.2f %12.2f\n", names[var], n, med(ta), med(tg), med(tb),
+                    med(to));
     }
     die(pskv_shard_destroy(s), "destroy");
   }
