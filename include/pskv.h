@@ -143,11 +143,12 @@ int pskv_shard_destroy(pskv_shard* s);
 /* Push: apply n (key, value) pairs.  Asynchronous on the shard's stream for
  * PSKV_DEVICE inputs (the caller keeps them alive until the stream passes the
  * call); host inputs are staged before return and may be reused immediately.
- * A host Add of at most 2048 keys in all (grouped: summed over its batches)
- * travels inside the kernel arguments, 256 keys per launch (no staging copy),
- * and returns once the launches are enqueued; a host Get of at most 1024 keys
- * likewise, 512 keys per launch, its reply written by the kernels into
- * page-locked memory (PSKV_INLINE=0 disables). */
+ * A host Add of at most 256 keys in all (grouped: summed over its batches)
+ * travels inside the kernel arguments and returns once the launch is
+ * enqueued; a host Get of at most 1024 keys likewise, 512 keys per launch,
+ * its reply written by the kernels into page-locked memory (PSKV_INLINE=0
+ * disables).  Larger pageable host Adds below 32 MiB are copied into pinned
+ * staging and return once the copy is queued for DMA. */
 int pskv_add(pskv_shard* s, const uint32_t* keys, const void* vals, uint64_t n, int flags);
 /* Pull: out[i] = value of keys[i] (0 if never written).  Synchronous for host
  * `out` (PSKV_HOST), stream-ordered for device `out` (PSKV_DEVICE). */
