@@ -61,6 +61,15 @@ __device__ __forceinline__ void st16(void* p, u32x4 v) {
     *reinterpret_cast<u32x4*>(p) = v;
 }
 
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+template <bool NT>
+__device__ __forceinline__ void ld8_keys(const uint32_t* p, uint32_t (&k)[2]) {
+  const u32x2 t = NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(p))
+                     : *reinterpret_cast<const u32x2*>(p);
+  k[0] = t.x;
+  k[1] = t.y;
+}
+
 // Two 8-byte values as one 16-byte access.  Streams of 8-byte values go two
 // per lane (a wave covers 1 KiB contiguously per instruction) rather than four
 // per lane as two 16-byte accesses 32 bytes apart (each instruction then
@@ -220,49 +229,19 @@ __global__ __launch_bounds__(kBlock) void k_gather(GroupArgs ga, DenseView d, Ov
   const int tid = threadIdx.x;
   if constexpr (sizeof(VT) == 8) {
     if (VEC && base + CH <= n) {
-      // 16-byte key loads, four keys per lane (a wave's 256 elements are
-      // contiguous).  When the wave's 256 keys are ONE contiguous in-range run
-      // on an even offset (a dense pull; wave-uniform test), the 8-byte values
-      // move as PAIRS: lane l takes elements 2l, 2l+1 and 128+2l, 128+2l+1 of
-      // the wave's span, so every value load and store instruction covers
-      // 1 KiB contiguously.  Otherwise each lane gathers its own four keys.
-      using T = unsigned long long;
-      const int lane = tid & 63;
-      uint32_t k[U][4];
+      // two keys per lane per step (see Vec2x8): 8-byte key loads, 16-byte
+      // value loads and stores, every instruction one contiguous span.  (A
+      // form with 16-byte key loads and values moved as pairs over each wave's
+      // span measured no faster and needed 202 VGPRs against 80.)
+      constexpr int UU = 2 * U;
+      uint32_t k[UU][2];
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-        Vec4<uint32_t>::load<NT>(keys + base + (uint64_t)(u * kBlock + tid) * 4, k[u]);
-      T va[U][2], vb[U][2];
-      bool dense[U];
+      for (int u = 0; u < UU; ++u) ld8_keys<NT>(keys + base + (uint64_t)(u * kBlock + tid) * 2, k[u]);
+      VT v[UU][2];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)k[u][0]);
-        const uint32_t e0 = k0 + 4u * (uint32_t)lane;
-        const bool ok = (k[u][0] == e0) & (k[u][1] == e0 + 1u) & (k[u][2] == e0 + 2u) & (k[u][3] == e0 + 3u);
-        const uint32_t off = k0 - d.key_begin;
-        dense[u] = __all(ok) && (off & 1u) == 0u && (uint64_t)off + 255u < d.range;  // wave-uniform
-        if (dense[u]) {
-          const T* p = reinterpret_cast<const T*>(d.param) + off;
-          Vec2x8::load(p + 2 * lane, va[u]);
-          Vec2x8::load(p + 128 + 2 * lane, vb[u]);
-        } else {
-          const uint32_t k01[2] = {k[u][0], k[u][1]}, k23[2] = {k[u][2], k[u][3]};
-          gather2(d, o, k01, va[u]);
-          gather2(d, o, k23, vb[u]);
-        }
-      }
+      for (int u = 0; u < UU; ++u) gather2(d, o, k[u], v[u]);
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (dense[u]) {
-          T* w = out + base + (uint64_t)(u * kBlock + (tid & ~63)) * 4;  // the wave's span
-          Vec2x8::store<NT>(w + 2 * lane, va[u]);
-          Vec2x8::store<NT>(w + 128 + 2 * lane, vb[u]);
-        } else {
-          T* w = out + base + (uint64_t)(u * kBlock + tid) * 4;  // this lane's four elements
-          Vec2x8::store<NT>(w, va[u]);
-          Vec2x8::store<NT>(w + 2, vb[u]);
-        }
-      }
+      for (int u = 0; u < UU; ++u) Vec2x8::store<NT>(out + base + (uint64_t)(u * kBlock + tid) * 2, v[u]);
       return;
     }
   }
@@ -278,8 +257,27 @@ __global__ __launch_bounds__(kBlock) void k_gather(GroupArgs ga, DenseView d, Ov
     for (int u = 0; u < U; ++u)
       Vec4<VT>::template store<NT>(out + base + (uint64_t)(u * kBlock + tid) * 4, v[u]);
   } else {
+    // a partial (or unaligned) chunk: eight keys per lane loaded together,
+    // then their gathers, then the stores — one dependent round trip per
+    // eight elements instead of per element (it matters when the keys sit in
+    // host memory: the zero-copy Get runs K1 over pinned staging)
     const uint64_t end = n < base + CH ? n : base + CH;
-    for (uint64_t i = base + tid; i < end; i += kBlock) out[i] = load_one<VT>(d, o, keys[i]);
+    for (uint64_t i0 = base + tid; i0 < end; i0 += 8ull * kBlock) {
+      uint32_t kk[8];
+      VT vv[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const uint64_t i = i0 + (uint64_t)q * kBlock;
+        kk[q] = i < end ? keys[i] : 0u;
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) vv[q] = i0 + (uint64_t)q * kBlock < end ? load_one<VT>(d, o, kk[q]) : VT(0);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const uint64_t i = i0 + (uint64_t)q * kBlock;
+        if (i < end) out[i] = vv[q];
+      }
+    }
   }
 }
 

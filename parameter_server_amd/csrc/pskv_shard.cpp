@@ -258,6 +258,11 @@ struct pskv_shard {
   // the pinned staging copy
   size_t tune_dma_min_bytes = kDefaultDmaMinBytes;
   size_t tune_dma_min_bytes_get = kDefaultDmaMinBytesGet;
+  // PSKV_ZC_MAX_BYTES: pageable host Gets of at most this many bytes (keys +
+  // values) past the inline size go zero-copy through pinned staging (0: off).
+  // Measured (tools/micro/small_latency.cpp, f64): 4 Ki keys 18 us, 16 Ki 23,
+  // 64 Ki 43 against 28 / 40 / 63 us by DMA; DMA ahead at 256 Ki (101 vs 152)
+  size_t tune_zc_max_bytes = 1ull << 20;
   uint32_t tune_rb_tb = 0; // PSKV_RB_TB: K5 bucket bits (0 = by element count)
   uint32_t tune_rb_wbits = 0; // PSKV_RB_WBITS: K5 window bits (0 = 11; >= bucket shift: contiguous buckets)
   uint32_t tune_rb_nbd = 0;   // PSKV_RB_NBD: K5 dense bucket count (0 = by the rule; tuning)
@@ -1073,6 +1078,43 @@ int add_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
   return PSKV_OK;
 }
 
+// Zero-copy host Get of a medium batch: the keys are copied into pinned staging
+// by the calling thread, K1 reads them from there and writes the values into
+// pinned staging over PCIe (no DMA engine on either side), and the calling
+// thread copies the values out.  The staging is default (non-coherent) pinned
+// memory: the kernel's writes are visible once the stream is synchronised.
+int zero_copy_get(pskv_shard* s, const std::vector<pskv_batch>& v, bool vec) {
+  size_t kbytes = 0, obytes = 0;
+  for (const auto& b : v) {
+    kbytes += round16(b.n * 4);
+    obytes += round16(b.n * (size_t)s->vb);
+  }
+  int rc = ensure_hstage(s, kbytes + obytes);
+  if (rc) return rc;
+  char* h = static_cast<char*>(s->hstage);
+  std::vector<pskv_batch> hv = v;
+  size_t ko = 0, oo = kbytes;
+  for (size_t i = 0; i < v.size(); ++i) {
+    std::memcpy(h + ko, v[i].keys, v[i].n * 4);
+    hv[i].keys = reinterpret_cast<const uint32_t*>(h + ko);
+    hv[i].vals = h + oo;
+    ko += round16(v[i].n * 4);
+    oo += round16(v[i].n * (size_t)s->vb);
+  }
+  for (auto& g : split_groups(hv)) {
+    GroupArgs ga;
+    const uint32_t nwg = build_group(hv, g.first, g.second, stream_chunk(s->tune_unroll), &ga);
+    uint64_t elems = 0;
+    for (size_t i = g.first; i < g.second; ++i) elems += hv[i].n;
+    LaunchTimer t(s, PSKV_K_GATHER, elems);
+    PSKV_HIP(launch_gather(s->vb, vec, s->tune_unroll, s->tune_nt, ga, nwg, s->dview(), s->ovf, s->stream));
+    t.done();
+  }
+  PSKV_HIP(hipStreamSynchronize(s->stream));
+  for (size_t i = 0; i < v.size(); ++i) std::memcpy(v[i].vals, hv[i].vals, v[i].n * (size_t)s->vb);
+  return PSKV_OK;
+}
+
 int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
   std::vector<pskv_batch> v;
   for (auto& b : in) {
@@ -1094,6 +1136,11 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
   size_t out_off = 0;
   bool pinned = !device;
   for (const auto& b : v) pinned = pinned && is_pinned(b.keys) && is_pinned(b.vals);
+  if (!device && !pinned && s->tune_zc_max_bytes) {  // medium pageable Get: zero copy
+    size_t bytes = 0;
+    for (auto& b : v) bytes += round16(b.n * 4) + round16(b.n * (size_t)s->vb);
+    if (bytes <= s->tune_zc_max_bytes) return zero_copy_get(s, v, true);
+  }
   if (!device && !pinned && s->tune_pageable_dma) {  // pageable: direct DMA only when large
     size_t bytes = 0;
     for (auto& b : v) bytes += round16(b.n * 4) + round16(b.n * (size_t)s->vb);
@@ -1252,6 +1299,7 @@ int pskv_shard_create_ex(int device, uint32_t key_begin, uint64_t key_end, int d
   if (const char* e = std::getenv("PSKV_PAGEABLE_DMA")) s->tune_pageable_dma = std::atoi(e) != 0;
   if (const char* e = std::getenv("PSKV_DMA_MIN_BYTES")) s->tune_dma_min_bytes = (size_t)std::atoll(e);
   if (const char* e = std::getenv("PSKV_DMA_MIN_BYTES_GET")) s->tune_dma_min_bytes_get = (size_t)std::atoll(e);
+  if (const char* e = std::getenv("PSKV_ZC_MAX_BYTES")) s->tune_zc_max_bytes = (size_t)std::atoll(e);
   if (const char* e = std::getenv("PSKV_INLINE")) s->tune_inline = std::atoi(e) != 0;
   if (const char* e = std::getenv("PSKV_INLINE_ADD_CHUNKS"))
     s->tune_inline_add_chunks = std::max(1, std::min(kInlineMaxChunks, std::atoi(e)));

@@ -1102,3 +1102,36 @@ def test_batch_beyond_2_to_32_elements(cuda):
         if off >= 1 << 32:
             want[:] = 2                       # the repeated tail
         assert torch.equal(out[off:off + m], want), off
+
+
+@pytest.mark.parametrize("n", [1025, 1500, 4096, 8193, 70_000, 120_000])
+def test_zero_copy_get_sizes(cuda, oracle_mod, n, monkeypatch):
+    """Medium pageable host Gets (past the inline size, <= 1 MiB of keys and
+    values) run K1 over pinned staging: the keys read and the values written
+    across PCIe by the kernel.  Partial chunks, unaligned sizes, missing and
+    out-of-range keys, grouped and single; against the oracle and against the
+    DMA path (PSKV_ZC_MAX_BYTES=0)."""
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(n)
+    kb, ke = 5000, 5000 + 200_000
+    k = rng.integers(0, ke + 3000, size=300_000).astype(np.uint32)
+    v = rng.standard_normal(k.size)
+    ref = oracle_mod.MapStorageRef(np.float64)
+    ref.add(k, v)
+    q = rng.integers(0, ke + 3000, size=n).astype(np.uint32)
+    q[:3] = [0xFFFFFFFF, ke + 2999, kb]
+    res = {}
+    for zc in ("default", "0"):
+        if zc == "0":
+            monkeypatch.setenv("PSKV_ZC_MAX_BYTES", "0")
+        with ps.Shard(kb, ke, np.float64, overflow_slots=1 << 16) as sh:
+            sh.add(k, v)
+            parts = np.array_split(q, 3)
+            outs = [np.empty(p.size) for p in parts]
+            sh.get_grouped(list(zip(parts, outs)))
+            res[zc] = (sh.get(q), np.concatenate(outs))
+    want = ref.get(q)
+    for zc, (single, grouped) in res.items():
+        assert_bits_equal(single, want, f"single {zc}")
+        assert_bits_equal(grouped, want, f"grouped {zc}")

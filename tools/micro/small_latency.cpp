@@ -38,10 +38,15 @@ int main() {
   // inline Gets waiting on the stream (PSKV_ISPIN=0); no inline path with
   // every pageable buffer DMA'd directly; no inline path with every pageable
   // buffer copied into pinned staging
-  const char* names[] = {"default", "inline-sync", "dma-always", "copy-always"};
+  // and the defaults with medium Gets zero-copy (PSKV_ZC_MAX_BYTES = 4 MiB)
+  const char* names[] = {"default", "inline-sync", "dma-always", "copy-always", "zero-copy"};
   for (int pass = 0; pass < 2; ++pass)  // pass 0 warms the runtime up (its pageable-copy paths); pass 1 prints
-  for (int var = 0; var < 4; ++var) {
-    setenv("PSKV_INLINE", var < 2 ? "1" : "0", 1);
+  for (int var = 0; var < 5; ++var) {
+    if (var == 4)
+      setenv("PSKV_ZC_MAX_BYTES", "4194304", 1);
+    else
+      unsetenv("PSKV_ZC_MAX_BYTES");
+    setenv("PSKV_INLINE", (var < 2 || var == 4) ? "1" : "0", 1);
     setenv("PSKV_ISPIN", var != 1 ? "1" : "0", 1);
     const char* th = var == 2 ? "0" : var == 3 ? "1000000000000" : nullptr;  // nullptr: library defaults
     if (th) {
