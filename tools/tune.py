@@ -28,7 +28,8 @@ def main():
     V = 8 if f64 else 4
     space = 100_000_000
     dev = torch.device("cuda:0")
-    batches = workload.dense_batches(J, space, device=dev,
+    B = int(os.environ.get("TUNE_BATCH", "1000000"))  # TUNE_BATCH: keys per window
+    batches = workload.dense_batches(J, space, batch=B, device=dev,
                                      dtype=torch.float64 if f64 else torch.float32)
     outs = [torch.empty_like(v) for _, v in batches]
     shards = []
@@ -86,16 +87,16 @@ def main():
         torch.cuda.synchronize()
         ct.append((time.perf_counter() - t0) * 1e3)
     med = statistics.median(ct)
-    print(f"{f'torch copy_ ({2 * V} B/key)':40s}  {med:.4f}ms ({J * 1e6 * 2 * V / (med / 1e3) / 1e9:.0f} GB/s)")
+    print(f"{f'torch copy_ ({2 * V} B/key)':40s}  {med:.4f}ms ({J * B * 2 * V / (med / 1e3) / 1e9:.0f} GB/s)")
     for name, d in res.items():
         line = [f"{name:40s}"]
         for k, v in d.items():
             med = statistics.median(v)
             extra = ""
             if k in ("k_gather", "k_assign_group"):
-                extra = f" ({J * 1e6 * (4 + 2 * V) / (med / 1e3) / 1e9:.0f} GB/s)"
+                extra = f" ({J * B * (4 + 2 * V) / (med / 1e3) / 1e9:.0f} GB/s)"
             if k in ("step", "step_untimed"):
-                extra = f" ({J * 1e6 * (8 + 4 * V) / (med / 1e3) / 1e9:.0f} GB/s)"
+                extra = f" ({J * B * (8 + 4 * V) / (med / 1e3) / 1e9:.0f} GB/s)"
             line.append(f"{k}={med:.4f}ms{extra}")
         print("  ".join(line), flush=True)
 
