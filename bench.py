@@ -395,6 +395,29 @@ def side_measurements(dev, B):
     assert all(np.array_equal(o, hv[last[int(k[0])]]) for o, k in zip(po, hk))
     out["e2e_pinned_buffers"] = {"workload": "as e2e_host_buffers, from page-locked host memory (direct DMA)",
                                  "GB/s": (add_b + get_b) * reps / dt / 1e9}
+    # the same from the library's frame pool under PSKV_HOST_FRAME (the buffers
+    # are borrowed: the Adds return once queued)
+    frames = [ps.HostFrame(B * 4) for _ in range(3 * J)]
+    fk = [f.array(np.uint32, B) for f in frames[:J]]
+    fv = [f.array(np.float32, B) for f in frames[J:2 * J]]
+    fo = [f.array(np.float32, B) for f in frames[2 * J:]]
+    for a, b in zip(fk + fv, hk + hv):
+        a[:] = b
+    with ps.Shard(0, space, np.float32) as sh:
+        sh.add_grouped(list(zip(fk, fv)), frame=True)
+        sh.get_grouped(list(zip(fk, fo)), frame=True)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            sh.add_grouped(list(zip(fk, fv)), frame=True)
+            sh.get_grouped(list(zip(fk, fo)), frame=True)
+        sh.sync()
+        dt = time.perf_counter() - t0
+    assert all(np.array_equal(o, hv[last[int(k[0])]]) for o, k in zip(fo, hk))
+    for f in frames:
+        f.free()
+    out["e2e_frame_buffers"] = {"workload": "as e2e_host_buffers, from pskv_host_alloc frames under "
+                                            "PSKV_HOST_FRAME (borrowed: Adds return once queued)",
+                                "GB/s": (add_b + get_b) * reps / dt / 1e9}
     return out
 
 

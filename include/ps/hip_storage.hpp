@@ -15,6 +15,12 @@
 //   * called from one server thread; the device is selected inside every call
 //     because Engine::CreateTable constructs storages on another thread
 //     (driver/engine.hpp:100-109)
+// Page-locked frames (ps/host_frames.hpp): every call passes
+// PSKV_HOST_FRAME, so request payloads the mailbox received into frames are
+// read in place (an Add returns once queued; the frames stay alive through
+// the message's SArrays and the pool holds them until the work has run), and
+// Get replies are frames the kernel writes directly.  Payloads outside frames
+// take the ordinary host paths.
 #pragma once
 
 #include <cstdint>
@@ -23,6 +29,7 @@
 #include <vector>
 
 #include "pskv.h"
+#include "ps/host_frames.hpp"
 
 #ifdef PSKV_IN_REFERENCE_TREE
 #include "server/abstract_storage.hpp"
@@ -76,7 +83,8 @@ class HipStorage : public AbstractStorage {
                    (size_t)typed_keys.size(), (size_t)typed_vals.size());
       std::abort();
     }
-    pskv_check(pskv_add(shard_, typed_keys.data(), typed_vals.data(), typed_keys.size(), PSKV_HOST),
+    pskv_check(pskv_add(shard_, typed_keys.data(), typed_vals.data(), typed_keys.size(),
+                        PSKV_HOST | PSKV_HOST_FRAME),
                "pskv_add");
   }
 
@@ -100,14 +108,17 @@ class HipStorage : public AbstractStorage {
       }
       batches.push_back(pskv_batch{keep_k.back().data(), keep_v.back().data(), keep_k.back().size()});
     }
-    pskv_check(pskv_add_grouped(shard_, batches.data(), batches.size(), PSKV_HOST),
+    pskv_check(pskv_add_grouped(shard_, batches.data(), batches.size(), PSKV_HOST | PSKV_HOST_FRAME),
                "pskv_add_grouped");
   }
 #endif
 
   third_party::SArray<char> SubGet(const third_party::SArray<Key>& typed_keys) override {
-    third_party::SArray<Val> reply_vals(typed_keys.size());
-    pskv_check(pskv_get(shard_, typed_keys.data(), typed_keys.size(), reply_vals.data(), PSKV_HOST),
+    // the reply is a page-locked frame: written in place by the kernel when the
+    // request keys are a frame too, and sent zero-copy by the Sender
+    auto reply_vals = FrameArray<Val>(typed_keys.size());
+    pskv_check(pskv_get(shard_, typed_keys.data(), typed_keys.size(), reply_vals.data(),
+                        PSKV_HOST | PSKV_HOST_FRAME),
                "pskv_get");
     return third_party::SArray<char>(reply_vals);
   }

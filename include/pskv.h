@@ -15,6 +15,8 @@
  *   RangePartitionManager::Slice base/range_partition_manager.hpp:19-46,48-77  pskv_range_slice
  *   ConsistentHashingPartitionManager::JumpConsistentHash
  *                     base/consistent_hashing_partition_manager.hpp:81-89       pskv_jump_hash
+ *   zmq receive buffer of a data frame, Mailbox::Recv comm/mailbox.cpp:246-257,
+ *   and SubGet's reply allocation server/map_storage.hpp:30     pskv_host_alloc / pskv_host_free
  *
  * Semantics (PSKV_ASSIGN, the reference semantics; map_storage.hpp:22-23,
  * vector_storage.hpp:21-43): a shard is a last-write-wins key/value store with
@@ -87,6 +89,13 @@ enum pskv_mode {
                                 The kernel verifies the claim and repairs the result on the
                                 device if it was wrong, so a wrong hint costs time, never
                                 correctness. */
+#define PSKV_HOST_FRAME 0x4  /* host keys/vals/out that lie in pskv_host_alloc frames are
+                                BORROWED until pskv_host_free: the call reads and writes them
+                                in place (no staging copy) and an Add returns once its work
+                                is queued, without waiting for it.  The caller must not
+                                modify such a frame before freeing it; pskv_host_free holds
+                                it back from reuse until every queued call that reads it has
+                                run.  Host pointers outside frames ignore the flag. */
 
 typedef struct pskv_shard pskv_shard;
 
@@ -199,6 +208,21 @@ int pskv_range_slice(const uint64_t* range_begin, const uint64_t* range_end, int
  * driver/engine.hpp:143-150).  out_bucket[i] in [0, nbuckets); the slice of key
  * i goes to server_thread_ids[out_bucket[i]].  Host memory, any n. */
 int pskv_jump_hash(const uint32_t* keys, uint64_t n, int32_t nbuckets, int32_t* out_bucket);
+
+/* Page-locked host frames for message payloads (the mailbox
+ * receives data frames, comm/mailbox.cpp:211-261, into memory the GPU reads
+ * directly).  Pooled by power-of-two size class, so steady traffic allocates
+ * nothing; thread-safe; usable by every device.  *out is 4 KiB-aligned.  A
+ * freed frame whose queued reads (PSKV_HOST_FRAME Adds) have not run yet is
+ * held back until they have.  Free frames beyond PSKV_FRAME_CACHE_BYTES
+ * (default 1 GiB) are returned to the system. */
+int pskv_host_alloc(uint64_t bytes, void** out);
+int pskv_host_free(void* p);
+/* Bytes held by live frames, by cached free frames, and by freed frames still
+ * awaiting their queued reads. */
+int pskv_host_pool_stats(uint64_t* live_bytes, uint64_t* cached_bytes, uint64_t* held_bytes);
+/* Return every cached free frame to the system (waits for held ones first). */
+int pskv_host_pool_trim(void);
 
 const char* pskv_last_error(void);
 int pskv_abi_version(void);

@@ -6,10 +6,11 @@ Importing this package loads libpskv.so and raises if it is missing: there is
 no CPU fallback on the product path.
 """
 from ._lib import PskvError, lib  # noqa: F401  (fails loudly if the HIP library is absent)
-from .shard import Shard, device_count, jump_hash, range_slice  # noqa: F401
+from .shard import (HostFrame, Shard, device_count, host_pool_stats, host_pool_trim,  # noqa: F401
+                    jump_hash, range_slice)
 from .storage import (AbstractStorage, CheckError, ConsistentHashingPartitionManager, Flag,  # noqa: F401
                       HipStorage, Message, Meta, RangePartitionManager, typed)
 
 __all__ = ["Shard", "HipStorage", "AbstractStorage", "Message", "Meta", "Flag",
            "RangePartitionManager", "ConsistentHashingPartitionManager", "range_slice", "jump_hash",
-           "device_count", "CheckError", "PskvError"]
+           "device_count", "CheckError", "PskvError", "HostFrame", "host_pool_stats", "host_pool_trim"]

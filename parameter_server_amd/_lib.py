@@ -22,7 +22,7 @@ PSKV_ESTATE = -4
 
 PSKV_I32, PSKV_F32, PSKV_F64 = 0, 1, 2
 PSKV_ASSIGN, PSKV_ACCUMULATE = 0, 1
-PSKV_HOST, PSKV_DEVICE, PSKV_SORTED_HINT = 0x0, 0x1, 0x2
+PSKV_HOST, PSKV_DEVICE, PSKV_SORTED_HINT, PSKV_HOST_FRAME = 0x0, 0x1, 0x2, 0x4
 
 PSKV_K_GATHER = 0
 PSKV_K_ASSIGN_SORTED = 1
@@ -54,7 +54,8 @@ EXPORTED = [
     "pskv_add_grouped", "pskv_get_grouped", "pskv_sync", "pskv_clear", "pskv_set_stream",
     "pskv_get_stream", "pskv_dense_ptr", "pskv_shard_info", "pskv_set_timing", "pskv_set_timing_mask",
     "pskv_kernel_time", "pskv_reset_timing", "pskv_range_slice", "pskv_jump_hash", "pskv_last_error",
-    "pskv_abi_version", "pskv_device_count",
+    "pskv_abi_version", "pskv_device_count", "pskv_host_alloc", "pskv_host_free",
+    "pskv_host_pool_stats", "pskv_host_pool_trim",
 ]
 
 
@@ -110,6 +111,10 @@ def _load():
         "pskv_last_error": ([], ctypes.c_char_p),
         "pskv_abi_version": ([], i32),
         "pskv_device_count": ([], i32),
+        "pskv_host_alloc": ([u64, ctypes.POINTER(vp)], i32),
+        "pskv_host_free": ([vp], i32),
+        "pskv_host_pool_stats": ([ctypes.POINTER(u64)] * 3, i32),
+        "pskv_host_pool_trim": ([], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -16,7 +16,7 @@ INCLUDE = os.path.join(ROOT, "include")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-LIB_SOURCES = ["pskv_kernels.hip", "pskv_shard.cpp"]
+LIB_SOURCES = ["pskv_kernels.hip", "pskv_shard.cpp", "pskv_frames.cpp"]
 LIB_OUT = os.path.join(PKG, "libpskv.so")
 CPP_TESTS = {  # program -> (source in tests/cpp, links the oracle checker)
     "hip_storage_test": ("hip_storage_test.cpp", False),
@@ -43,7 +43,7 @@ def _stale(out, deps):
 
 def build_lib(force=False):
     srcs = [os.path.join(CSRC, s) for s in LIB_SOURCES]
-    deps = srcs + [os.path.join(CSRC, "pskv_internal.h"), os.path.join(INCLUDE, "pskv.h")]
+    deps = srcs + [os.path.join(CSRC, h) for h in ("pskv_internal.h", "pskv_frames.h")] + [os.path.join(INCLUDE, "pskv.h")]
     if force or _stale(LIB_OUT, deps):
         _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
               "-I", INCLUDE, "-I", CSRC, *srcs, "-o", LIB_OUT])

@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "pskv.h"
+#include "pskv_frames.h"
 #include "pskv_internal.h"
 
 using namespace pskv;
@@ -181,6 +182,7 @@ class HostPool {
 };
 
 constexpr size_t kPieceBytes = 1 << 20;   // one pool task
+constexpr size_t kCheckPieceBytes = 256 << 10;  // one pool task of a check without copy
 constexpr size_t kWindowBytes = 8 << 20;  // one H2D / D2H DMA while the next window is copied
 constexpr size_t kInlineCopyBytes = 256 << 10;  // smaller windows are copied by the calling thread
 
@@ -258,11 +260,21 @@ struct pskv_shard {
   // the pinned staging copy
   size_t tune_dma_min_bytes = kDefaultDmaMinBytes;
   size_t tune_dma_min_bytes_get = kDefaultDmaMinBytesGet;
+  // PSKV_DMA_MIN_BYTES_PINNED: page-locked host Adds of at least this many
+  // bytes are DMA'd straight from the caller's buffers (and wait for it);
+  // smaller ones take the pinned staging copy, which returns before its DMA.
+  // Measured (tools/micro/small_latency.cpp, f64): 16 Ki keys 9 us copied
+  // against 29 us DMA'd, 256 Ki keys 95 against 90
+  size_t tune_dma_min_bytes_pinned = 2ull << 20;
   // PSKV_ZC_MAX_BYTES: pageable host Gets of at most this many bytes (keys +
   // values) past the inline size go zero-copy through pinned staging (0: off).
   // Measured (tools/micro/small_latency.cpp, f64): 4 Ki keys 18 us, 16 Ki 23,
   // 64 Ki 43 against 28 / 40 / 63 us by DMA; DMA ahead at 256 Ki (101 vs 152)
   size_t tune_zc_max_bytes = 1ull << 20;
+  // PSKV_FRAME_ZC_MAX_BYTES: PSKV_HOST_FRAME Adds and page-locked Gets of at
+  // most this many bytes (keys + values) run the kernels on the host buffers
+  // in place; larger ones DMA
+  size_t tune_frame_zc_max_bytes = 8ull << 20;
   uint32_t tune_rb_tb = 0; // PSKV_RB_TB: K5 bucket bits (0 = by element count)
   uint32_t tune_rb_wbits = 0; // PSKV_RB_WBITS: K5 window bits (0 = 11; >= bucket shift: contiguous buckets)
   uint32_t tune_rb_nbd = 0;   // PSKV_RB_NBD: K5 dense bucket count (0 = by the rule; tuning)
@@ -703,51 +715,77 @@ struct Piece {
   uint64_t outside;
 };
 
+// The key check, written so the compiler vectorises it (no loop-carried
+// state but the or / sum reductions): 2-4x the rate of the sequential form.
+void check_keys(Piece& p, const uint32_t* k, size_t n, uint32_t key_begin, uint64_t range) {
+  p.sorted = p.dense = true;
+  p.first = p.last = 0;
+  p.outside = 0;
+  if (!n) return;
+  const uint32_t rmax = range ? (uint32_t)(range - 1) : 0u;  // in range: (x - key_begin) <= rmax
+  uint32_t unsorted = 0, gap = 0, out = (uint32_t)(k[0] - key_begin) > rmax;
+  for (size_t i = 1; i < n; ++i) {
+    const uint32_t a = k[i - 1], x = k[i];
+    unsorted |= (uint32_t)(a > x);
+    gap |= (uint32_t)(x != a + 1u);
+    out += (uint32_t)((uint32_t)(x - key_begin) > rmax);
+  }
+  p.sorted = unsorted == 0;
+  p.dense = gap == 0;
+  p.first = k[0];
+  p.last = k[n - 1];
+  p.outside = range ? out : n;  // pieces hold < 2^32 keys
+}
+
 void copy_piece(Piece& p, uint32_t key_begin, uint64_t range) {
   if (p.key_batch < 0) {
     std::memcpy(p.dst, p.src, p.bytes);
     return;
   }
-  const uint32_t* k = reinterpret_cast<const uint32_t*>(p.src);
-  uint32_t* o = reinterpret_cast<uint32_t*>(p.dst);
-  const size_t n = p.bytes / 4;
-  bool ok = true, dense = true;
-  uint64_t outside = 0;
-  uint32_t prev = n ? k[0] : 0;
-  auto scan = [&](auto store) {
-    for (size_t i = 0; i < n; ++i) {
-      const uint32_t x = k[i];
-      store(i, x);
-      outside += (uint64_t)(uint32_t)(x - key_begin) >= range;
-      ok &= prev <= x;
-      dense &= i == 0 || x == prev + 1u;
-      prev = x;
-    }
-  };
-  if (o)
-    scan([&](size_t i, uint32_t x) { o[i] = x; });
-  else
-    scan([](size_t, uint32_t) {});  // pinned caller buffer: check only, the DMA reads it
-  p.sorted = ok;
-  p.dense = dense;
-  p.first = n ? k[0] : 0;
-  p.last = n ? k[n - 1] : 0;
-  p.outside = outside;
+  if (p.dst) std::memcpy(p.dst, p.src, p.bytes);  // else a page-locked caller buffer: check only
+  check_keys(p, reinterpret_cast<const uint32_t*>(p.src), p.bytes / 4, key_begin, range);
 }
 
-// Cut [src, src+bytes) into pieces appended to `out`.
+// Cut [src, src+bytes) into pieces appended to `out`; check-only pieces
+// (dst null) are smaller, so a pool spreads a medium batch's check wider.
 void add_pieces(std::vector<Piece>& out, const void* src, char* dst, size_t bytes, int key_batch) {
   const char* s = static_cast<const char*>(src);
-  for (size_t off = 0; off < bytes; off += kPieceBytes) {
+  const size_t piece = dst ? kPieceBytes : kCheckPieceBytes;
+  for (size_t off = 0; off < bytes; off += piece) {
     Piece p{};
     p.src = s + off;
     p.dst = dst ? dst + off : nullptr;
-    p.bytes = std::min(kPieceBytes, bytes - off);
+    p.bytes = std::min(piece, bytes - off);
     p.key_batch = key_batch;
     p.sorted = true;
     p.dense = true;
     out.push_back(p);
   }
+}
+
+// Combine the per-piece key checks: every piece sorted, and each piece's first
+// key not below the previous piece's last key within the same batch.
+void combine_checks(const std::vector<Piece>& pieces, bool* all_sorted_in_range,
+                    uint64_t* n_outside, bool* all_dense_in_range) {
+  bool ok = true, dense = true;
+  uint64_t outside = 0;
+  int prev_batch = -1;
+  uint32_t prev_last = 0;
+  for (const auto& p : pieces) {
+    if (p.key_batch < 0) continue;
+    outside += p.outside;
+    ok &= p.sorted;
+    dense &= p.dense;
+    if (p.key_batch == prev_batch) {
+      ok &= prev_last <= p.first;
+      dense &= p.first == prev_last + 1u;
+    }
+    prev_batch = p.key_batch;
+    prev_last = p.last;
+  }
+  *all_sorted_in_range = ok && outside == 0;
+  if (all_dense_in_range) *all_dense_in_range = dense && outside == 0;
+  *n_outside = outside;
 }
 
 // Copy pieces window by window (pool in parallel) and DMA each window to the
@@ -769,13 +807,29 @@ int pipelined_h2d(pskv_shard* s, std::vector<Piece>& pieces, char* h, char* d) {
 
 // Page-locked (hipHostMalloc'd / registered) host memory: the DMA engine can
 // read or write it directly, so no staging copy is needed.
-bool is_pinned(const void* p) {
+bool is_pinned(const void* p, void** dev = nullptr) {
   hipPointerAttribute_t a;
   if (hipPointerGetAttributes(&a, p) != hipSuccess) {
     (void)hipGetLastError();
     return false;
   }
-  return a.type == hipMemoryTypeHost;
+  if (dev) *dev = a.devicePointer;
+  return a.type == hipMemoryTypeHost && (!dev || a.devicePointer);
+}
+
+// Device views of page-locked host batches (frames or any other pinned
+// memory), or false.
+bool pinned_views(const std::vector<pskv_batch>& in, std::vector<pskv_batch>* out) {
+  out->clear();
+  for (const auto& b : in) {
+    pskv_batch d = b;
+    void *k = nullptr, *v = nullptr;
+    if (!is_pinned(b.keys, &k) || !is_pinned(b.vals, &v)) return false;
+    d.keys = static_cast<const uint32_t*>(k);
+    d.vals = v;
+    out->push_back(d);
+  }
+  return true;
 }
 
 // Stage host batches into one device buffer (keys then values per batch,
@@ -792,6 +846,12 @@ int stage_host_batches(pskv_shard* s, const std::vector<pskv_batch>& in,
   // copy has a high fixed cost and blocks until done); smaller ones are copied
   // into pinned staging and DMA'd asynchronously (the call returns after the
   // host copy)
+  // page-locked buffers: DMA'd directly from tune_dma_min_bytes_pinned on
+  // (below it the copy, which returns before the DMA, is ahead); pageable
+  // buffers only when large (the runtime's pageable copy has a high fixed cost
+  // and blocks until done).  Smaller ones are copied into pinned staging and
+  // DMA'd asynchronously (the call returns after the host copy).
+  locked = locked && bytes >= s->tune_dma_min_bytes_pinned;
   const bool pinned = locked || (s->tune_pageable_dma && bytes >= s->tune_dma_min_bytes);
   int rc = pinned ? PSKV_OK : ensure_hstage(s, bytes);
   if (rc) return rc;
@@ -869,27 +929,72 @@ int stage_host_batches(pskv_shard* s, const std::vector<pskv_batch>& in,
     PSKV_HIP(hipEventRecord(s->hstage_free, s->stream));
     s->hstage_pending = true;
   }
-  // combine the per-piece checks: every piece sorted, and each piece's first
-  // key not below the previous piece's last key within the same batch
-  bool ok = true, dense = true;
-  uint64_t outside = 0;
-  int prev_batch = -1;
-  uint32_t prev_last = 0;
-  for (const auto& p : pieces) {
-    if (p.key_batch < 0) continue;
-    outside += p.outside;
-    ok &= p.sorted;
-    dense &= p.dense;
-    if (p.key_batch == prev_batch) {
-      ok &= prev_last <= p.first;
-      dense &= p.first == prev_last + 1u;
-    }
-    prev_batch = p.key_batch;
-    prev_last = p.last;
+  combine_checks(pieces, all_sorted_in_range, n_outside, all_dense_in_range);
+  return PSKV_OK;
+}
+
+// Device views of host batches that lie in pskv_host_alloc frames (every
+// keys and values range inside one live frame), or false.
+bool frame_views(const std::vector<pskv_batch>& in, size_t vb, std::vector<pskv_batch>* out) {
+  out->clear();
+  for (const auto& b : in) {
+    pskv_batch d = b;
+    d.keys = static_cast<const uint32_t*>(frames::device_view(b.keys, b.n * 4));
+    d.vals = frames::device_view(b.vals, b.n * vb);
+    if (!d.keys || !d.vals) return false;
+    out->push_back(d);
   }
-  *all_sorted_in_range = ok && outside == 0;
-  if (all_dense_in_range) *all_dense_in_range = dense && outside == 0;
-  *n_outside = outside;
+  return true;
+}
+
+// Host Add batches in borrowed frames (PSKV_HOST_FRAME): the CPU checks the
+// keys (sorted / dense / in range, as for staged inputs) without copying
+// anything; the kernels then read the frames in place across PCIe when the
+// call is at most tune_frame_zc_max_bytes, otherwise the frames are DMA'd
+// into device staging.  Either way nothing waits: the frames stay unmodified
+// until freed, and pskv_host_free holds them until this call's work has run
+// (note_frame_uses).
+int frame_batches(pskv_shard* s, const std::vector<pskv_batch>& in,
+                  const std::vector<pskv_batch>& views, std::vector<pskv_batch>* out,
+                  bool* all_sorted_in_range, uint64_t* n_outside, bool* all_dense_in_range) {
+  size_t bytes = 0;
+  for (auto& b : in) bytes += round16(b.n * 4) + round16(b.n * (size_t)s->vb);
+  std::vector<Piece> pieces;
+  for (size_t j = 0; j < in.size(); ++j) add_pieces(pieces, in[j].keys, nullptr, in[j].n * 4, (int)j);
+  if (bytes <= s->tune_frame_zc_max_bytes) {
+    *out = views;
+  } else {
+    int rc = ensure_dstage(s, bytes);
+    if (rc) return rc;
+    char* d = static_cast<char*>(s->dstage);
+    size_t off = 0;
+    out->clear();
+    for (const auto& b : in) {
+      pskv_batch db;
+      PSKV_HIP(hipMemcpyAsync(d + off, b.keys, b.n * 4, hipMemcpyHostToDevice, s->stream));
+      db.keys = reinterpret_cast<const uint32_t*>(d + off);
+      off += round16(b.n * 4);
+      PSKV_HIP(hipMemcpyAsync(d + off, b.vals, b.n * (size_t)s->vb, hipMemcpyHostToDevice, s->stream));
+      db.vals = d + off;
+      off += round16(b.n * (size_t)s->vb);
+      db.n = b.n;
+      out->push_back(db);
+    }
+  }
+  run_pieces(pieces, 0, pieces.size(), [&](Piece& p) { copy_piece(p, s->key_begin, s->range); });
+  combine_checks(pieces, all_sorted_in_range, n_outside, all_dense_in_range);
+  return PSKV_OK;
+}
+
+// The work queued so far reads the frames of `v` (host pointers).
+int note_frame_uses(pskv_shard* s, const std::vector<pskv_batch>& v) {
+  std::string err;
+  for (const auto& b : v) {
+    int rc = frames::note_use(b.keys, s->device, s->stream, &err);
+    if (!rc && b.vals != static_cast<const void*>(b.keys))
+      rc = frames::note_use(b.vals, s->device, s->stream, &err);
+    if (rc) return fail(rc, err);
+  }
   return PSKV_OK;
 }
 
@@ -1031,10 +1136,16 @@ int add_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
     if (total <= (uint64_t)kInlineMax * s->tune_inline_add_chunks) return inline_add(s, v);
   }
   bool host_verified = false, host_dense = false;
+  std::vector<pskv_batch> framed;  // the host batches, when they are borrowed frames
   if (!device) {
-    std::vector<pskv_batch> staged;
+    std::vector<pskv_batch> staged, views;
     uint64_t outside = 0;
-    rc = stage_host_batches(s, v, &staged, &host_verified, &outside, &host_dense);
+    if ((flags & PSKV_HOST_FRAME) && frame_views(v, (size_t)s->vb, &views)) {
+      framed = v;
+      rc = frame_batches(s, v, views, &staged, &host_verified, &outside, &host_dense);
+    } else {
+      rc = stage_host_batches(s, v, &staged, &host_verified, &outside, &host_dense);
+    }
     if (rc) return rc;
     if (outside) {
       // exact bound on new overflow keys: grow before the kernels can fill the table
@@ -1075,6 +1186,7 @@ int add_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
     }
     if (rc) return rc;
   }
+  if (!framed.empty()) return note_frame_uses(s, framed);
   return PSKV_OK;
 }
 
@@ -1083,6 +1195,24 @@ int add_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
 // pinned staging over PCIe (no DMA engine on either side), and the calling
 // thread copies the values out.  The staging is default (non-coherent) pinned
 // memory: the kernel's writes are visible once the stream is synchronised.
+// Frames (PSKV_HOST_FRAME) skip both copies: K1 reads the keys from and
+// writes the values into the caller's frames.
+int zero_copy_get_views(pskv_shard* s, const std::vector<pskv_batch>& hv) {
+  bool vec = true;
+  for (auto& b : hv) vec &= aligned16(b.keys) & aligned16(b.vals);
+  for (auto& g : split_groups(hv)) {
+    GroupArgs ga;
+    const uint32_t nwg = build_group(hv, g.first, g.second, stream_chunk(s->tune_unroll), &ga);
+    uint64_t elems = 0;
+    for (size_t i = g.first; i < g.second; ++i) elems += hv[i].n;
+    LaunchTimer t(s, PSKV_K_GATHER, elems);
+    PSKV_HIP(launch_gather(s->vb, vec, s->tune_unroll, s->tune_nt, ga, nwg, s->dview(), s->ovf, s->stream));
+    t.done();
+  }
+  PSKV_HIP(hipStreamSynchronize(s->stream));
+  return PSKV_OK;
+}
+
 int zero_copy_get(pskv_shard* s, const std::vector<pskv_batch>& v, bool vec) {
   size_t kbytes = 0, obytes = 0;
   for (const auto& b : v) {
@@ -1131,6 +1261,14 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
     uint64_t total = 0;
     for (const auto& b : v) total += b.n;
     if (total <= (uint64_t)kInlineGetMax * s->tune_inline_get_chunks) return inline_get(s, v, total);
+  }
+  if (!device) {  // page-locked keys and outputs (frames or not): zero copy in place
+    size_t bytes = 0;
+    for (auto& b : v) bytes += round16(b.n * 4) + round16(b.n * (size_t)s->vb);
+    std::vector<pskv_batch> views;
+    if (bytes <= s->tune_frame_zc_max_bytes &&
+        (((flags & PSKV_HOST_FRAME) && frame_views(v, (size_t)s->vb, &views)) || pinned_views(v, &views)))
+      return zero_copy_get_views(s, views);
   }
   std::vector<pskv_batch> dv = v;
   size_t out_off = 0;
@@ -1299,7 +1437,9 @@ int pskv_shard_create_ex(int device, uint32_t key_begin, uint64_t key_end, int d
   if (const char* e = std::getenv("PSKV_PAGEABLE_DMA")) s->tune_pageable_dma = std::atoi(e) != 0;
   if (const char* e = std::getenv("PSKV_DMA_MIN_BYTES")) s->tune_dma_min_bytes = (size_t)std::atoll(e);
   if (const char* e = std::getenv("PSKV_DMA_MIN_BYTES_GET")) s->tune_dma_min_bytes_get = (size_t)std::atoll(e);
+  if (const char* e = std::getenv("PSKV_DMA_MIN_BYTES_PINNED")) s->tune_dma_min_bytes_pinned = (size_t)std::atoll(e);
   if (const char* e = std::getenv("PSKV_ZC_MAX_BYTES")) s->tune_zc_max_bytes = (size_t)std::atoll(e);
+  if (const char* e = std::getenv("PSKV_FRAME_ZC_MAX_BYTES")) s->tune_frame_zc_max_bytes = (size_t)std::atoll(e);
   if (const char* e = std::getenv("PSKV_INLINE")) s->tune_inline = std::atoi(e) != 0;
   if (const char* e = std::getenv("PSKV_INLINE_ADD_CHUNKS"))
     s->tune_inline_add_chunks = std::max(1, std::min(kInlineMaxChunks, std::atoi(e)));
@@ -1570,6 +1710,29 @@ int pskv_jump_hash(const uint32_t* keys, uint64_t n, int32_t nbuckets, int32_t* 
     });
   }
   return PSKV_OK;
+}
+
+int pskv_host_alloc(uint64_t bytes, void** out) {
+  std::string err;
+  const int rc = frames::alloc((size_t)bytes, out, &err);
+  return rc ? fail(rc, err) : PSKV_OK;
+}
+
+int pskv_host_free(void* p) {
+  std::string err;
+  const int rc = frames::release(p, &err);
+  return rc ? fail(rc, err) : PSKV_OK;
+}
+
+int pskv_host_pool_stats(uint64_t* live_bytes, uint64_t* cached_bytes, uint64_t* held_bytes) {
+  frames::stats(live_bytes, cached_bytes, held_bytes);
+  return PSKV_OK;
+}
+
+int pskv_host_pool_trim(void) {
+  std::string err;
+  const int rc = frames::trim(&err);
+  return rc ? fail(rc, err) : PSKV_OK;
 }
 
 }  // extern "C"

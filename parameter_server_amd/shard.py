@@ -88,8 +88,10 @@ class Shard:
         return v
 
     # ------------------------------------------------------------ Add / Get
-    def add(self, keys, vals, sorted_hint: bool = False):
-        """Push one batch.  numpy -> host path; torch CUDA tensors -> device path."""
+    def add(self, keys, vals, sorted_hint: bool = False, frame: bool = False):
+        """Push one batch.  numpy -> host path; torch CUDA tensors -> device path.
+        frame=True: host arrays that live in HostFrames are borrowed until the
+        frames are freed (PSKV_HOST_FRAME): read in place, no wait."""
         if _is_torch(keys):
             self._check_dev(keys, vals)
             flags = _lib.PSKV_DEVICE | (_lib.PSKV_SORTED_HINT if sorted_hint else 0)
@@ -99,9 +101,10 @@ class Shard:
             return
         k = self._host_keys(keys)
         v = self._host_vals(vals, k.size)
-        check(lib.pskv_add(self._h, k.ctypes.data, v.ctypes.data, k.size, _lib.PSKV_HOST))
+        flags = _lib.PSKV_HOST_FRAME if frame else _lib.PSKV_HOST
+        check(lib.pskv_add(self._h, k.ctypes.data, v.ctypes.data, k.size, flags))
 
-    def get(self, keys, out=None):
+    def get(self, keys, out=None, frame: bool = False):
         """Pull one batch.  numpy keys -> returns a numpy array (synchronous);
         torch keys -> fills/returns a torch tensor (stream-ordered)."""
         if _is_torch(keys):
@@ -115,7 +118,8 @@ class Shard:
             return out
         k = self._host_keys(keys)
         res = np.empty(k.size, dtype=self.dtype) if out is None else out
-        check(lib.pskv_get(self._h, k.ctypes.data, k.size, res.ctypes.data, _lib.PSKV_HOST))
+        flags = _lib.PSKV_HOST_FRAME if frame else _lib.PSKV_HOST
+        check(lib.pskv_get(self._h, k.ctypes.data, k.size, res.ctypes.data, flags))
         return res
 
     def prepare(self, batches, is_get: bool = False) -> "BatchSet":
@@ -123,18 +127,23 @@ class Shard:
         arr, keep, flags = self._batch_array(batches, is_get=is_get)
         return BatchSet(arr, len(batches), flags, keep)
 
-    def add_grouped(self, batches, sorted_hint: bool = False):
+    def add_grouped(self, batches, sorted_hint: bool = False, frame: bool = False):
         """batches: list of (keys, vals) (all torch-device or all numpy-host) or a BatchSet."""
         bs = batches if isinstance(batches, BatchSet) else self.prepare(batches)
         flags = bs.flags
         if sorted_hint and flags & _lib.PSKV_DEVICE:
             flags |= _lib.PSKV_SORTED_HINT
+        if frame and not flags & _lib.PSKV_DEVICE:
+            flags |= _lib.PSKV_HOST_FRAME
         check(lib.pskv_add_grouped(self._h, bs.arr, bs.n, flags))
 
-    def get_grouped(self, batches):
+    def get_grouped(self, batches, frame: bool = False):
         """batches: list of (keys, out) pairs (out filled in place) or a BatchSet."""
         bs = batches if isinstance(batches, BatchSet) else self.prepare(batches, is_get=True)
-        check(lib.pskv_get_grouped(self._h, bs.arr, bs.n, bs.flags))
+        flags = bs.flags
+        if frame and not flags & _lib.PSKV_DEVICE:
+            flags |= _lib.PSKV_HOST_FRAME
+        check(lib.pskv_get_grouped(self._h, bs.arr, bs.n, flags))
 
     def _batch_array(self, batches, is_get):
         arr = (_lib.PskvBatch * max(1, len(batches)))()
@@ -241,6 +250,46 @@ def _tensor_from_ptr(ptr, n, tdtype, device):
 
     with torch.cuda.device(device):
         return torch.as_tensor(_Holder(), device=f"cuda:{device}")
+
+
+class HostFrame:
+    """A page-locked host frame from the library's pool (pskv_host_alloc): the
+    buffer a mailbox receives one message payload into (comm/mailbox.cpp:246-257).
+    `array(dtype, n, offset)` views it as numpy; `free()` returns it (the pool
+    holds it back until queued PSKV_HOST_FRAME reads of it have run)."""
+
+    def __init__(self, nbytes: int):
+        p = ctypes.c_void_p()
+        check(lib.pskv_host_alloc(int(nbytes), ctypes.byref(p)))
+        self.ptr, self.nbytes = p.value, int(nbytes)
+
+    def array(self, dtype, n: int, offset: int = 0) -> np.ndarray:
+        dt = np.dtype(dtype)
+        if self.ptr is None or offset < 0 or offset + n * dt.itemsize > self.nbytes:
+            raise ValueError("view outside the frame")
+        buf = (ctypes.c_char * (n * dt.itemsize)).from_address(self.ptr + offset)
+        return np.frombuffer(buf, dtype=dt, count=n)
+
+    def free(self):
+        if self.ptr is not None:
+            p, self.ptr = self.ptr, None
+            check(lib.pskv_host_free(p))
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.free()
+
+
+def host_pool_stats() -> dict:
+    v = [ctypes.c_uint64() for _ in range(3)]
+    check(lib.pskv_host_pool_stats(*[ctypes.byref(x) for x in v]))
+    return {"live_bytes": v[0].value, "cached_bytes": v[1].value, "held_bytes": v[2].value}
+
+
+def host_pool_trim():
+    check(lib.pskv_host_pool_trim())
 
 
 def range_slice(ranges, keys):

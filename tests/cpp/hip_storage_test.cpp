@@ -9,19 +9,26 @@
 //                                            Add{5:1,5:2,7:3}; Add{7:10}; Get{5,7,9} -> {2,10,0}
 //   SliceKeys / SliceKVs                     base/range_partition_manager_test.cpp:17-56
 //   SliceFallthrough                         SURVEY.md §0.4 probes
+//   FramedMessages                           SURVEY.md §8f-3: payloads received into page-locked
+//                                            frames (ps/host_frames.hpp), read in place; the
+//                                            frames dropped while their Adds may still be queued
 //   CreateTableHip                           driver/engine.hpp:93-131 with StorageType::Hip
 //                                            (ps/storage_factory.hpp): per-server ranges, the
 //                                            last server also stores the fall-through keys
 //
 // Needs a GPU for the storage cases (run by tests/test_gpu_parity.py);
 // `--host-only` runs the range-map cases alone.
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <memory>
+#include <random>
 #include <vector>
 
 #include "ps/hip_storage.hpp"
+#include "ps/host_frames.hpp"
 #include "ps/consistent_hashing_partition_manager.hpp"
 #include "ps/range_partition_manager.hpp"
 #include "ps/storage_factory.hpp"
@@ -166,6 +173,63 @@ static void HashSliceCases() {
   }
 }
 
+// Messages whose payloads sit in page-locked frames, as Mailbox::Recv delivers
+// them after the §8f-3 change (RecvIntoFrame per data frame): Adds of 3 to
+// 300 000 keys (sorted, unsorted with duplicates, out of range), each message
+// dropped right after Add -- its frames return to the pool while the Add may
+// still be queued -- and fresh frames of the same sizes scribbled over; then
+// a framed Get against a host map.
+template <typename V>
+static void FramedMessages(const char* name) {
+  std::printf("[ RUN ] %s\n", name);
+  std::unique_ptr<AbstractStorage> s(new HipStorage<V>(0, 1000, 501000));
+  std::mt19937 rng(11);
+  std::map<uint32_t, V> want;
+  const size_t sizes[] = {3, 1000, 5000, 70000, 300000};
+  for (size_t n : sizes) {
+    for (int form = 0; form < 2; ++form) {
+      std::vector<uint32_t> k(n);
+      std::vector<V> v(n);
+      for (size_t i = 0; i < n; ++i) {
+        k[i] = 900 + rng() % 500200;  // some below 1000 and past 501000: overflow keys
+        v[i] = V(int(rng() % 2000) - 1000);
+      }
+      if (form == 0) std::sort(k.begin(), k.end());
+      for (size_t i = 0; i < n; ++i) want[k[i]] = v[i];
+      {
+        Message m;
+        m.meta.flag = Flag::kAdd;
+        m.AddData(third_party::SArray<Key>(RecvIntoFrame(k.data(), n * sizeof(uint32_t))));
+        m.AddData(RecvIntoFrame(v.data(), n * sizeof(V)));
+        s->Add(m);
+      }  // the message and its frames are gone; the Add may still be queued
+      auto a = RecvIntoFrame(k.data(), n * sizeof(uint32_t));
+      auto b = RecvIntoFrame(v.data(), n * sizeof(V));
+      std::memset(a.data(), 0xA5, a.size());
+      std::memset(b.data(), 0x5A, b.size());
+    }
+  }
+  std::vector<uint32_t> q;
+  for (uint32_t x = 0; x < 502000; x += 3) q.push_back(x);
+  Message g;
+  g.meta.flag = Flag::kGet;
+  g.AddData(third_party::SArray<Key>(RecvIntoFrame(q.data(), q.size() * sizeof(uint32_t))));
+  Message rep = s->Get(g);
+  auto got = third_party::SArray<V>(rep.data[1]);
+  EXPECT(got.size() == q.size());
+  size_t bad = 0;
+  for (size_t i = 0; i < q.size() && i < got.size(); ++i) {
+    auto it = want.find(q[i]);
+    const V w = it == want.end() ? V(0) : it->second;
+    bad += std::memcmp(&got[i], &w, sizeof(V)) != 0;
+  }
+  EXPECT(bad == 0);
+  s->FinishIter();
+  uint64_t live = 0, cached = 0, held = 0;
+  EXPECT(pskv_host_pool_stats(&live, &cached, &held) == PSKV_OK);
+  EXPECT(held == 0);  // FinishIter synchronised the shard: every held frame is free
+}
+
 // CreateTable over three server threads: each server's HipStorage owns its
 // range; keys the slicer routes to the last server beyond its range land in
 // its overflow table.  Adds go through the models (ASP: immediate).
@@ -229,6 +293,8 @@ int main(int argc, char** argv) {
     LastWriteWins<int>(0, 1ull << 20, "LastWriteWinsInt");
     LastWriteWins<float>(0, 1ull << 20, "LastWriteWinsFloat");
     LastWriteWins<double>(6, 8, "LastWriteWinsDoubleOverflow");  // 5 and 9 live in the overflow table
+    FramedMessages<float>("FramedMessagesFloat");
+    FramedMessages<double>("FramedMessagesDouble");
     CreateTableHip();
   }
   std::printf("%d passed, %d failed\n", g_pass, g_fail);

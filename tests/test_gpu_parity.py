@@ -863,13 +863,20 @@ def _pinned(a):
     return out.view(np.uint32) if a.dtype == np.uint32 else out
 
 
+@pytest.mark.parametrize("pinned_path", ["dma", "default"])
 @pytest.mark.parametrize("pageable_path", ["dma", "staged"])
 @pytest.mark.parametrize("mode", ["assign", "accumulate"])
-def test_pinned_host_buffers_direct_dma(cuda, oracle_mod, mode, pageable_path, monkeypatch):
+def test_pinned_host_buffers_direct_dma(cuda, oracle_mod, mode, pageable_path, pinned_path, monkeypatch):
     """Page-locked caller buffers (the zmq frames after the SURVEY §8f-3 mailbox
-    change) are DMA'd directly, without the staging copy: same results as
-    pageable buffers, for sorted, dense and unsorted batches, Add and Get."""
+    change): same results as pageable buffers, for sorted, dense and unsorted
+    batches, Add and Get.  pinned_path "dma": Adds and Gets DMA'd directly
+    from / to them at every size; "default": Adds below 2 MiB take the staging
+    copy and Gets up to 8 MiB run K1 on them in place (zero copy)."""
     import parameter_server_amd as ps
+
+    if pinned_path == "dma":
+        monkeypatch.setenv("PSKV_DMA_MIN_BYTES_PINNED", "0")
+        monkeypatch.setenv("PSKV_FRAME_ZC_MAX_BYTES", "0")
 
     # pageable buffers go by direct DMA (forced at every size: by default only
     # calls of >= 32 MiB (Add) / 32 KiB (Get) do) or through pinned staging

@@ -18,6 +18,7 @@ CXX=/opt/rocm/llvm/bin/clang++
   -Xarch_host -fsanitize=$SAN -Xarch_host $NORECOVER -Xarch_host -fno-omit-frame-pointer \
   -I "$R/include" -I "$R/parameter_server_amd/csrc" \
   "$R/parameter_server_amd/csrc/pskv_kernels.hip" "$R/parameter_server_amd/csrc/pskv_shard.cpp" \
+  "$R/parameter_server_amd/csrc/pskv_frames.cpp" \
   -o "$O/libpskv.so"
 for p in hip_storage_test kv_client_table_test ssp_replay; do
   oracle_link=""  # ssp_replay links the oracle checker as well
