@@ -1006,6 +1006,15 @@ __device__ __forceinline__ uint32_t lds_insert(uint32_t* hk, uint32_t* sent,
   return own;
 }
 
+// An empty asm that reads x: the compiler's wait-count pass must have x's loads
+// complete here.  Used to place the wait for a software-pipelined register set
+// before the next set's loads are issued (see k_rb_bin, k_rb_resolve).
+template <typename T, int N>
+__device__ __forceinline__ void ready(const T (&x)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" ::"v"(x[i]));
+}
+
 // K5a k_rb_bin: one 1024-thread workgroup per CU, persistent over
 // super-chunks of SC keys of one batch (8 Ki keys for 4-byte values, 4 Ki for
 // 8-byte ones), the next super-chunk's loads in flight.  Per super-chunk:
@@ -1110,6 +1119,12 @@ __global__ __launch_bounds__(kBinBlock) void k_rb_bin(GroupArgs ga, DenseView d,
     load(cur, kc, vc);
   }
   for (uint32_t sc = blockIdx.x; sc < nsc; sc += gridDim.x) {
+    // this super-chunk's registers complete BEFORE the next one's loads go out:
+    // the wait-count pass cannot count the next loads (their number depends on
+    // the full / partial branch) and otherwise waited for ALL of them (vmcnt(0))
+    // at the first use of kc below, i.e. for the prefetch it had just issued
+    ready(kc);
+    ready(vc);
     if (sc + gridDim.x < nsc) {
       nxt = task(sc + gridDim.x);
       load(nxt, kn, vn);

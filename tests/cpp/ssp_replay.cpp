@@ -117,6 +117,7 @@ struct Config {
   bool cpu_only = false;
   bool bsp_ungrouped = false;
   bool threads = false;  // one ServerThread per shard (concurrent HipStorage use)
+  bool frames = false;   // payloads delivered in page-locked frames (HipStorage runs only)
   std::string partition = "range";  // range | hash
 };
 
@@ -273,8 +274,14 @@ class Replay {
     Rng rng{0};
   };
 
-  void deliver(const Message& m) {
+  void deliver(const Message& in) {
     ++out_.msgs;
+    Message m = in;
+    if (c_.frames && hip_) {
+      // the mailbox after SURVEY §8f-3: every data frame received into a
+      // page-locked frame (comm/mailbox.cpp:246-257)
+      for (auto& d : m.data) d = RecvIntoFrame(d.data(), d.size());
+    }
     if (c_.threads) {
       {
         std::lock_guard<std::mutex> lk(qm_);
@@ -619,6 +626,7 @@ int main(int argc, char** argv) {
     else if (a == "--cpu-only") c.cpu_only = true;
     else if (a == "--bsp-ungrouped") c.bsp_ungrouped = true;
     else if (a == "--threads") c.threads = true;
+    else if (a == "--frames") c.frames = true;
     else if (a == "--known-answers") ka = true;
     else if (a == "--partition") c.partition = nxt();
   }
@@ -633,9 +641,9 @@ int main(int argc, char** argv) {
   Run other = c.cpu_only ? Replay(c, false).run() : Replay(c, true).run();
   std::string why;
   const bool ok = same(ref, other, &why);
-  std::printf("replay model=%s partition=%s workers=%d shards=%d iters=%d batch=%d staleness=%d: msgs=%llu "
+  std::printf("replay model=%s partition=%s%s workers=%d shards=%d iters=%d batch=%d staleness=%d: msgs=%llu "
               "adds=%llu gets=%llu clocks=%llu ssp_releases=%llu replies=%zu\n",
-              c.model.c_str(), c.partition.c_str(), c.workers, c.shards, c.iters, c.batch, c.staleness,
+              c.model.c_str(), c.partition.c_str(), c.frames ? " frames" : "", c.workers, c.shards, c.iters, c.batch, c.staleness,
               (unsigned long long)ref.msgs, (unsigned long long)ref.adds, (unsigned long long)ref.gets,
               (unsigned long long)ref.clocks, (unsigned long long)ref.echoes, ref.log.size());
   std::printf("cpu %.3f s, %s %.3f s\n", ref.seconds, c.cpu_only ? "cpu" : "hip", other.seconds);
