@@ -156,8 +156,9 @@ int pskv_shard_destroy(pskv_shard* s);
  * travels inside the kernel arguments and returns once the launch is
  * enqueued; a host Get of at most 1024 keys likewise, 512 keys per launch,
  * its reply written by the kernels into page-locked memory (PSKV_INLINE=0
- * disables).  Larger pageable host Adds below 32 MiB are copied into pinned
- * staging and return once the copy is queued for DMA. */
+ * disables; PSKV_SERVE=1 sends them to a resident request-server kernel
+ * instead).  Larger pageable host Adds below 32 MiB are copied
+ * into pinned staging and return once the copy is queued for DMA. */
 int pskv_add(pskv_shard* s, const uint32_t* keys, const void* vals, uint64_t n, int flags);
 /* Pull: out[i] = value of keys[i] (0 if never written).  Synchronous for host
  * `out` (PSKV_HOST), stream-ordered for device `out` (PSKV_DEVICE). */

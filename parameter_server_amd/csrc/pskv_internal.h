@@ -10,6 +10,7 @@
 //   ovf.stat[2]         {occupied slots, sticky error bits}
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 namespace pskv {
@@ -59,6 +60,30 @@ struct InlineGet {
 };
 static_assert(sizeof(InlineAdd) + 128 <= 4096 && sizeof(InlineGet) + 128 <= 4096,
               "inline messages must fit the kernarg segment with the other arguments");
+
+// K9: the small-message server (PSKV_SERVE=1): one resident workgroup polls a
+// ring of requests in coherent page-locked host memory and applies them in
+// ring order, so a small Add or Get costs no kernel launch.
+constexpr int kSrvSlots = 64;
+constexpr uint32_t kSrvAdd = 1, kSrvGet = 2;
+struct SrvSlot {  // the kernel reads {kind, n} and {reply_off, pad} as 8-byte words
+  uint32_t kind;       // kSrvAdd / kSrvGet
+  uint32_t n;          // keys: <= kInlineMax (Add) / kInlineGetMax (Get)
+  uint32_t reply_off;  // Get: first reply element
+  uint32_t pad;
+  uint32_t keys[kInlineGetMax];
+  unsigned long long vals[kInlineMax];  // value bits (4-byte values in the low word)
+};
+struct SrvRing {  // the kernel polls {req_seq, stop} as one 8-byte word
+  uint32_t req_seq;    // host: number of the last request posted
+  uint32_t stop;       // host: 1 = leave the loop
+  uint32_t pad0[30];
+  uint32_t done_seq;   // device: number of the last request applied
+  uint32_t alive;      // device: 0 once the kernel has left its loop
+  uint32_t pad1[30];
+  SrvSlot slot[kSrvSlots];
+};
+static_assert(sizeof(SrvSlot) % 8 == 0 && offsetof(SrvRing, slot) % 8 == 0, "8-byte words in the ring");
 
 struct DenseView {
   void* param;
@@ -128,6 +153,12 @@ hipError_t launch_inline_add(int dtype, int mode, const InlineAdd& a, const Dens
                              const Ovf& o, hipStream_t st);
 hipError_t launch_inline_get(int vb, const InlineGet& a, const DenseView& d, const Ovf& o,
                              void* out, unsigned int* done, unsigned int seq, hipStream_t st);
+// K9: start the request server on `st` (one workgroup; requests start_seq+1..
+// are applied as they are posted).  It leaves its loop when ring->stop is set or
+// after idle_ticks wall-clock ticks without a request, and then clears alive.
+hipError_t launch_serve(int dtype, int mode, SrvRing* ring, const DenseView& d, const Ovf& o,
+                        void* reply, uint32_t start_seq, unsigned long long idle_ticks,
+                        hipStream_t st);
 size_t rb_entry_bytes(int vb);
 // K6: tag `flag` with `epoch` unless every batch is a dense in-range window
 // (chunk = kBlock * 4 * 8 keys per workgroup).

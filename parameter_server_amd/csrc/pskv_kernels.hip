@@ -1793,6 +1793,202 @@ __global__ __launch_bounds__(64) void k_inline_get(InlineGet a, DenseView d, Ovf
   }
 }
 
+// K9 k_serve: the small-message server.  One resident workgroup polls the
+// request ring (coherent page-locked host memory) and applies each request in
+// ring order with K8's semantics: a small Add or Get then costs the host a
+// ring slot and a sequence number instead of a kernel launch.  Lane 0 polls
+// req_seq with system-scope loads that bypass the caches; up to kSrvBatch
+// posted slots are then read in ONE round trip by all lanes (the host filled
+// them before publishing their numbers), and applied one by one from LDS
+// (assign: last occurrence by an LDS hash of the largest index; accumulate:
+// the first occurrence sums in index order).  Add requests need no release: only this
+// workgroup touches the parameters while it runs (the host stops it before any
+// other work on the shard, and its end is a release), and it reads its own
+// stores through its own L2.  A Get's reply goes to page-locked host memory,
+// released at system scope before done_seq.  The loop ends on `stop` or after
+// idle_ticks without a request, so the kernel always drains.
+// Workgroup barrier for LDS only: the wave's LDS operations complete, then
+// s_barrier.  __syncthreads would also wait for every outstanding global
+// store (vmcnt(0)), i.e. for the parameter stores' acknowledgements.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <typename T>
+__device__ __forceinline__ T sys_load(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <typename VT, int MODE>
+__global__ __launch_bounds__(kInlineMax) void k_serve(SrvRing* ring, DenseView d, Ovf o,
+                                                      void* reply, uint32_t start,
+                                                      unsigned long long idle_ticks) {
+  using BT = typename std::conditional<sizeof(VT) == 8, unsigned long long, uint32_t>::type;
+  __shared__ __attribute__((aligned(16))) uint32_t s_keys[kInlineGetMax];
+  __shared__ __attribute__((aligned(16))) unsigned long long s_vals[kInlineMax];
+  constexpr int kSrvHash = 2 * kInlineMax;  // assign dedup slots (load <= 1/2)
+  __shared__ uint32_t h_key[MODE == 0 ? kSrvHash + 1 : 1], h_idx[MODE == 0 ? kSrvHash + 1 : 1];
+  __shared__ uint32_t h_sent;
+  __shared__ uint32_t s_cmd, s_avail;
+  constexpr int kSrvBatch = 4;  // requests read per round trip
+  const int tid = threadIdx.x;
+  uint32_t next = start + 1;
+  unsigned long long t_idle = wall_clock64();
+  for (;;) {
+    if (tid == 0) {
+      // {req_seq, stop} in one 8-byte load: one PCIe round trip per poll
+      const unsigned long long* rs = reinterpret_cast<const unsigned long long*>(&ring->req_seq);
+      uint32_t cmd = 0, avail = 0;
+      for (;;) {
+        const unsigned long long w = sys_load(rs);
+        const int32_t ahead = (int32_t)((uint32_t)w - next);
+        if (ahead >= 0) {
+          avail = ahead + 1 < kSrvBatch ? (uint32_t)ahead + 1u : (uint32_t)kSrvBatch;
+          break;
+        }
+        if ((uint32_t)(w >> 32) != 0u || wall_clock64() - t_idle > idle_ticks) {
+          cmd = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      s_cmd = cmd;
+      s_avail = avail;
+    }
+    __syncthreads();
+    if (s_cmd) break;
+    const int m = (int)s_avail;
+    // one round trip for up to kSrvBatch posted requests: every lane loads each
+    // request's header and its share of the LARGEST payload at once (the unused
+    // part is ignored), with 16-byte volatile loads (system-coherent,
+    // cache-bypassing): lanes 0..127 take the keys, lanes 128..255 the values
+    static_assert(kInlineGetMax * 4 == 128 * 16 && kInlineMax * 8 == 128 * 16, "one 16-byte piece per lane");
+    u32x4 hdrs[kSrvBatch], pieces[kSrvBatch];
+#pragma unroll
+    for (int b = 0; b < kSrvBatch; ++b) {
+      if (b < m) {
+        const SrvSlot* sl = &ring->slot[(next + (uint32_t)b) % kSrvSlots];
+        hdrs[b] = *reinterpret_cast<const volatile u32x4*>(&sl->kind);
+        pieces[b] = tid < 128 ? *reinterpret_cast<const volatile u32x4*>(&sl->keys[4 * tid])
+                              : *reinterpret_cast<const volatile u32x4*>(&sl->vals[2 * (tid - 128)]);
+      }
+    }
+    uint32_t last_kind = 0;
+#pragma unroll
+    for (int b = 0; b < kSrvBatch; ++b) {
+    if (b >= m) break;  // uniform
+    const u32x4 hdr = hdrs[b], piece = pieces[b];
+    const uint32_t kind = hdr[0];
+    last_kind = kind;
+    const int n = (int)(hdr[1] < (uint32_t)kInlineGetMax ? hdr[1] : (uint32_t)kInlineGetMax);
+    const unsigned long long h1 = hdr[2];
+    if (MODE == 0) {  // the assign dedup table, cleared for this request
+      for (int i = tid; i <= kSrvHash; i += kInlineMax) {
+        h_key[i] = kEmpty32;
+        h_idx[i] = 0u;
+      }
+      if (tid == 0) h_sent = 0u;
+    }
+    if (tid < 128) {
+      u32x4 k4v = piece;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (4 * tid + e >= n) k4v[e] = 0u;  // zero past n: the walks read whole 16-byte groups
+      reinterpret_cast<u32x4*>(s_keys)[tid] = k4v;
+    } else {
+      reinterpret_cast<u32x4*>(s_vals)[tid - 128] = piece;
+    }
+    // a full barrier: besides the staged message, the previous request's
+    // parameter stores complete (vmcnt(0)) before this one's, so a later
+    // request's store to the same key lands last
+    __syncthreads();
+    const u32x4* k4 = reinterpret_cast<const u32x4*>(s_keys);
+    const int ng = (n + 3) >> 2;
+    if (kind == kSrvAdd) {
+      uint32_t win_slot = 0;
+      if (tid < n) {
+        const uint32_t k = s_keys[tid];
+        if (MODE == 0) {
+          // last occurrence: the largest index per key in an LDS hash (two LDS
+          // atomics per key; the O(n) walk of every lane over the message cost
+          // ~6 us at 256 keys)
+          uint32_t k1[1] = {k}, s1[1];
+          (void)lds_insert<1, kSrvHash>(h_key, &h_sent, k1, 1u, s1);
+          atomicMax(&h_idx[s1[0]], (uint32_t)tid + 1u);
+          win_slot = s1[0];
+        }
+      }
+      __syncthreads();
+      if (tid < n) {
+        const uint32_t k = s_keys[tid];
+        const uint32_t off = k - d.key_begin;
+        if (MODE == 0) {
+          if (h_idx[win_slot] == (uint32_t)tid + 1u) {  // the last occurrence stores
+            const BT v = (BT)s_vals[tid];
+            if ((uint64_t)off < d.range) {
+              reinterpret_cast<BT*>(d.param)[off] = v;
+            } else {
+              const long long slot = ovf_insert(o, k);
+              if (slot >= 0) reinterpret_cast<BT*>(o.vals)[slot] = v;
+            }
+          }
+        } else {
+          bool earlier = false;
+          for (int g = 0; g < ng; ++g) {
+            const u32x4 q = k4[g];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) earlier |= (4 * g + e < tid) & (q[e] == k);
+          }
+          if (!earlier) {  // the first occurrence sums them all, in index order
+            VT* p = nullptr;
+            if ((uint64_t)off < d.range) {
+              p = reinterpret_cast<VT*>(d.param) + off;
+            } else {
+              const long long slot = ovf_insert(o, k);
+              if (slot >= 0) p = reinterpret_cast<VT*>(o.vals) + slot;
+            }
+            if (p) {
+              VT acc = *p;
+              for (int j = tid; j < n; ++j)
+                if (s_keys[j] == k) acc = add_wrap<VT>(acc, from_bits<VT>(s_vals[j]));
+              *p = acc;
+            }
+          }
+        }
+      }
+      lds_barrier();  // the staged message is read before the next one is staged
+    } else {
+      __syncthreads();  // the parameter stores of earlier Adds complete before these loads
+      constexpr int PER = kInlineGetMax / kInlineMax;
+      const uint32_t roff = (uint32_t)h1;
+      BT v[PER];
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int i = tid + kInlineMax * q;
+        v[q] = i < n ? load_one<BT>(d, o, s_keys[i]) : BT(0);
+      }
+      BT* out = static_cast<BT*>(reply) + roff;
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int i = tid + kInlineMax * q;
+        if (i < n) out[i] = v[q];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the reply before done_seq
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    // a Get publishes its number (covering the Adds before it); Adds are
+    // published once per batch, below: a store to host memory per request cost
+    // its PCIe write acknowledgement at the next barrier
+    if (kind != kSrvAdd && tid == 0)
+      __hip_atomic_store(&ring->done_seq, next + (uint32_t)b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }  // request b
+    if (tid == 0 && last_kind == kSrvAdd)
+      __hip_atomic_store(&ring->done_seq, next + (uint32_t)m - 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    next += (uint32_t)m;
+    t_idle = wall_clock64();
+  }
+  if (tid == 0) __hip_atomic_store(&ring->alive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace
 
 // ------------------------------------------------------- launch wrappers
@@ -2019,6 +2215,24 @@ hipError_t launch_inline_add(int dtype, int mode, const InlineAdd& a, const Dens
     k_inline_add<float, 1><<<1, kInlineMax, 0, st>>>(a, d, o);
   } else {
     k_inline_add<double, 1><<<1, kInlineMax, 0, st>>>(a, d, o);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_serve(int dtype, int mode, SrvRing* ring, const DenseView& d, const Ovf& o,
+                        void* reply, uint32_t start_seq, unsigned long long idle_ticks,
+                        hipStream_t st) {
+  if (mode == 0) {
+    if (dtype == 2)
+      k_serve<double, 0><<<1, kInlineMax, 0, st>>>(ring, d, o, reply, start_seq, idle_ticks);
+    else
+      k_serve<float, 0><<<1, kInlineMax, 0, st>>>(ring, d, o, reply, start_seq, idle_ticks);
+  } else if (dtype == 0) {
+    k_serve<int, 1><<<1, kInlineMax, 0, st>>>(ring, d, o, reply, start_seq, idle_ticks);
+  } else if (dtype == 1) {
+    k_serve<float, 1><<<1, kInlineMax, 0, st>>>(ring, d, o, reply, start_seq, idle_ticks);
+  } else {
+    k_serve<double, 1><<<1, kInlineMax, 0, st>>>(ring, d, o, reply, start_seq, idle_ticks);
   }
   return hipGetLastError();
 }

@@ -293,6 +293,18 @@ struct pskv_shard {
   bool tune_ispin = true;  // PSKV_ISPIN: poll the reply's sequence word instead of a stream wait
   unsigned int ireply_seq = 0;
   int tune_rb_apply_log2 = 0; // PSKV_RB_APPLY_LOG2: 13 or 14 (0 = by bucket size)
+  // K9 request server (PSKV_SERVE=1): the inline-size messages go to a ring in
+  // coherent page-locked memory that one resident workgroup polls
+  // (PSKV_SERVE_IDLE_US: it leaves after this long without a request)
+  bool tune_serve = false;
+  uint32_t tune_serve_idle_us = 20000;
+  SrvRing* srv = nullptr;
+  hipStream_t srv_stream = nullptr;
+  hipEvent_t srv_dep = nullptr;  // the shard's stream up to the server's launch
+  bool srv_running = false;
+  uint32_t srv_posted = 0;
+  unsigned long long srv_idle_ticks = 0;
+  bool counted = false;  // in g_device_shards
 
   DenseView dview() const { return DenseView{dense, key_begin, range}; }
 };
@@ -354,6 +366,128 @@ int drain_timing(pskv_shard* s) {
   return PSKV_OK;
 }
 
+// ------------------------------------------------------- K9 request server
+// Protocol (host side).  Requests are numbered 1, 2, ...; the host fills slot
+// q % kSrvSlots, then publishes q in req_seq (release).  The kernel applies
+// requests in order and publishes each number in done_seq after it (a Get
+// after its reply is released).  The kernel runs ALONE on the shard: before
+// any other work is queued on the shard's stream (srv_stop: every posted
+// request applied, then `stop`, then the kernel's end, which releases its
+// stores), and it starts behind everything already queued on that stream
+// (srv_launch: stream wait on an event), so stream order is kept both ways.
+// A kernel that left on its idle timer is restarted from done_seq (srv_wait).
+
+// A resident server holds the hardware queue its stream maps to: work of any
+// other stream on that queue waits behind it until it idles out.  The process
+// has GPU_MAX_HW_QUEUES queues per device (HIP's default 4) and each served
+// shard uses two streams, so the server engages only while a device has at
+// most that many / 2 shards; beyond that the K8 launches serve instead.
+std::atomic<int> g_device_shards[64];
+
+bool serve_on(const pskv_shard* s) {
+  if (!s->tune_serve || s->device < 0 || s->device >= 64) return false;
+  static const int limit = [] {
+    const char* e = std::getenv("GPU_MAX_HW_QUEUES");
+    const int q = e ? std::atoi(e) : 4;
+    return std::max(1, (q > 0 ? q : 4) / 2);
+  }();
+  return g_device_shards[s->device].load(std::memory_order_relaxed) <= limit;
+}
+
+int ensure_ireply(pskv_shard* s, size_t cap) {
+  if (s->ireply) return PSKV_OK;
+  // the reply values, then the K8 reply's sequence word on its own line.
+  // Coherent (fine-grained) memory: the kernel's stores go straight to the
+  // host.  Measured alternatives (tools/micro/small_latency.cpp):
+  // non-coherent pinned memory the same, a device reply + D2H copy 3 us slower.
+  if (hipHostMalloc(&s->ireply, cap + 128, hipHostMallocCoherent) != hipSuccess) {
+    s->ireply = nullptr;
+    return fail(PSKV_ENOMEM, "inline reply buffer allocation failed");
+  }
+  return PSKV_OK;
+}
+
+int srv_launch(pskv_shard* s) {
+  SrvRing* r = s->srv;
+  const uint32_t start = __atomic_load_n(&r->done_seq, __ATOMIC_ACQUIRE);
+  __atomic_store_n(&r->stop, 0u, __ATOMIC_RELAXED);
+  __atomic_store_n(&r->alive, 1u, __ATOMIC_RELEASE);
+  PSKV_HIP(hipEventRecord(s->srv_dep, s->stream));
+  PSKV_HIP(hipStreamWaitEvent(s->srv_stream, s->srv_dep, 0));
+  PSKV_HIP(launch_serve(s->dtype, s->mode, r, s->dview(), s->ovf, s->ireply, start, s->srv_idle_ticks,
+                        s->srv_stream));
+  s->srv_running = true;
+  return PSKV_OK;
+}
+
+// The kernel has left (or is leaving) its loop: wait for its end.
+int srv_reap(pskv_shard* s) {
+  s->srv_running = false;
+  PSKV_HIP(hipStreamSynchronize(s->srv_stream));
+  return PSKV_OK;
+}
+
+// Wait until request `seq` has been applied.
+int srv_wait(pskv_shard* s, uint32_t seq) {
+  SrvRing* r = s->srv;
+  for (uint32_t it = 1;; ++it) {
+    if ((int32_t)(__atomic_load_n(&r->done_seq, __ATOMIC_ACQUIRE) - seq) >= 0) return PSKV_OK;
+    if ((it & 255u) == 0 && __atomic_load_n(&r->alive, __ATOMIC_ACQUIRE) == 0u) {
+      // it left on its idle timer as requests were being posted: restart it
+      if (int rc = srv_reap(s)) return rc;
+      if ((int32_t)(__atomic_load_n(&r->done_seq, __ATOMIC_ACQUIRE) - seq) >= 0) return PSKV_OK;
+      if (int rc = srv_launch(s)) return rc;
+    }
+    if ((it & 65535u) == 0) {  // a faulted kernel never publishes: surface the error
+      const hipError_t e = hipStreamQuery(s->srv_stream);
+      if (e != hipSuccess && e != hipErrorNotReady) PSKV_HIP(e);
+    }
+  }
+}
+
+// Every posted request applied and the kernel ended (before any other work).
+int srv_stop(pskv_shard* s) {
+  if (!s->srv_running) return PSKV_OK;
+  if (int rc = srv_wait(s, s->srv_posted)) return rc;
+  __atomic_store_n(&s->srv->stop, 1u, __ATOMIC_RELEASE);
+  return srv_reap(s);
+}
+
+int srv_ensure(pskv_shard* s) {
+  if (!s->srv) {
+    int rc = ensure_ireply(s, (size_t)kInlineGetMax * kInlineMaxChunks * 8);
+    if (rc) return rc;
+    void* p = nullptr;
+    if (hipHostMalloc(&p, sizeof(SrvRing), hipHostMallocCoherent) != hipSuccess)
+      return fail(PSKV_ENOMEM, "request ring allocation failed");
+    std::memset(p, 0, sizeof(SrvRing));
+    s->srv = static_cast<SrvRing*>(p);
+    PSKV_HIP(hipStreamCreateWithFlags(&s->srv_stream, hipStreamNonBlocking));
+    PSKV_HIP(hipEventCreateWithFlags(&s->srv_dep, hipEventDisableTiming | hipEventDisableSystemFence));
+    int khz = 0;
+    PSKV_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, s->device));
+    s->srv_idle_ticks = (unsigned long long)s->tune_serve_idle_us * (unsigned long long)std::max(khz, 1) / 1000ull;
+  }
+  if (s->srv_running && __atomic_load_n(&s->srv->alive, __ATOMIC_ACQUIRE) == 0u)
+    if (int rc = srv_reap(s)) return rc;
+  if (!s->srv_running) return srv_launch(s);
+  return PSKV_OK;
+}
+
+// The slot of the next request (waits while the ring is full).
+int srv_slot(pskv_shard* s, SrvSlot** slot) {
+  const uint32_t q = s->srv_posted + 1;
+  if ((int32_t)(q - __atomic_load_n(&s->srv->done_seq, __ATOMIC_ACQUIRE)) > kSrvSlots)
+    if (int rc = srv_wait(s, q - kSrvSlots)) return rc;
+  *slot = &s->srv->slot[q % kSrvSlots];
+  return PSKV_OK;
+}
+
+void srv_publish(pskv_shard* s) {
+  const uint32_t q = ++s->srv_posted;
+  __atomic_store_n(&s->srv->req_seq, q, __ATOMIC_RELEASE);
+}
+
 int alloc_overflow(Ovf* o, uint64_t cap, int vb, hipStream_t st) {
   *o = Ovf{};
   PSKV_HIP(hipMalloc(&o->keys, cap * sizeof(unsigned long long)));
@@ -378,6 +512,7 @@ void free_overflow(Ovf* o) {
 
 // Grow the overflow table to at least `need` occupied slots at load <= 1/2.
 int grow_overflow(pskv_shard* s, uint64_t need) {
+  if (int rc = srv_stop(s)) return rc;  // it holds the table by value
   uint64_t cap = s->ocap;
   while (cap < 2 * need) cap <<= 1;
   if (cap == s->ocap) return PSKV_OK;
@@ -397,6 +532,7 @@ int grow_overflow(pskv_shard* s, uint64_t need) {
 
 // Read {count, err} of the overflow table (synchronises the stream).
 int read_overflow_stat(pskv_shard* s, uint32_t* count, uint32_t* err) {
+  if (int rc = srv_stop(s)) return rc;
   uint32_t st[2] = {0, 0};
   PSKV_HIP(hipMemcpyAsync(st, s->ovf.stat, sizeof(st), hipMemcpyDeviceToHost, s->stream));
   PSKV_HIP(hipStreamSynchronize(s->stream));
@@ -1019,10 +1155,23 @@ int inline_add(pskv_shard* s, const std::vector<pskv_batch>& v) {
     }
     s->ocount_known += outside;
   }
+  const bool serve = serve_on(s);
+  if (int rc = serve ? srv_ensure(s) : srv_stop(s)) return rc;
   InlineAdd a;
   a.n = 0;
   auto flush = [&]() -> int {
     if (a.n == 0) return PSKV_OK;
+    if (serve) {  // K9: one ring slot instead of a launch
+      SrvSlot* sl = nullptr;
+      if (int rc = srv_slot(s, &sl)) return rc;
+      sl->kind = kSrvAdd;
+      sl->n = a.n;
+      std::memcpy(sl->keys, a.keys, a.n * sizeof(uint32_t));
+      std::memcpy(sl->vals, a.vals, a.n * sizeof(unsigned long long));
+      srv_publish(s);
+      a.n = 0;
+      return PSKV_OK;
+    }
     LaunchTimer t(s, PSKV_K_INLINE_ADD, a.n);
     PSKV_HIP(launch_inline_add(s->dtype, s->mode, a, s->dview(), s->ovf, s->stream));
     t.done();
@@ -1052,17 +1201,37 @@ int inline_add(pskv_shard* s, const std::vector<pskv_batch>& v) {
 // once the LAST launch has published (stream order: the earlier ones are done).
 int inline_get(pskv_shard* s, const std::vector<pskv_batch>& v, uint64_t total) {
   const size_t cap = (size_t)kInlineGetMax * kInlineMaxChunks * 8;
-  if (!s->ireply) {
-    // kInlineGetMax * kInlineMaxChunks values, then the reply's sequence word
-    // on its own line.  Coherent (fine-grained) memory: the kernel's stores go
-    // straight to the host.  Measured alternatives (tools/micro/small_latency.cpp,
-    // DESIGN.md §5): non-coherent pinned memory the same, a device reply + D2H
-    // copy 3 us slower.
-    if (hipHostMalloc(&s->ireply, cap + 128, hipHostMallocCoherent) != hipSuccess) {
-      s->ireply = nullptr;
-      return fail(PSKV_ENOMEM, "inline reply buffer allocation failed");
+  if (int rc = ensure_ireply(s, cap)) return rc;
+  if (serve_on(s)) {  // K9: ring slots of kInlineGetMax keys, then wait for the last
+    if (int rc = srv_ensure(s)) return rc;
+    uint64_t off = 0;
+    SrvSlot* sl = nullptr;
+    for (const auto& b : v) {
+      for (uint64_t e = 0; e < b.n; ++e) {
+        if (!sl) {
+          if (int rc = srv_slot(s, &sl)) return rc;
+          sl->kind = kSrvGet;
+          sl->n = 0;
+          sl->reply_off = (uint32_t)off;
+        }
+        sl->keys[sl->n++] = b.keys[e];
+        ++off;
+        if (sl->n == (uint32_t)kInlineGetMax) {
+          srv_publish(s);
+          sl = nullptr;
+        }
+      }
     }
+    if (sl) srv_publish(s);
+    if (int rc = srv_wait(s, s->srv_posted)) return rc;
+    const char* r = static_cast<const char*>(s->ireply);
+    for (const auto& b : v) {
+      std::memcpy(b.vals, r, b.n * (size_t)s->vb);
+      r += b.n * (size_t)s->vb;
+    }
+    return PSKV_OK;
   }
+  if (int rc = srv_stop(s)) return rc;  // the K8 launches run on the shard's stream
   unsigned int* done = reinterpret_cast<unsigned int*>(static_cast<char*>(s->ireply) + cap);
   const unsigned int seq = ++s->ireply_seq;
   InlineGet a;
@@ -1135,6 +1304,8 @@ int add_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
     for (const auto& b : v) total += b.n;
     if (total <= (uint64_t)kInlineMax * s->tune_inline_add_chunks) return inline_add(s, v);
   }
+  rc = srv_stop(s);
+  if (rc) return rc;
   bool host_verified = false, host_dense = false;
   std::vector<pskv_batch> framed;  // the host batches, when they are borrowed frames
   if (!device) {
@@ -1262,6 +1433,8 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
     for (const auto& b : v) total += b.n;
     if (total <= (uint64_t)kInlineGetMax * s->tune_inline_get_chunks) return inline_get(s, v, total);
   }
+  rc = srv_stop(s);
+  if (rc) return rc;
   if (!device) {  // page-locked keys and outputs (frames or not): zero copy in place
     size_t bytes = 0;
     for (auto& b : v) bytes += round16(b.n * 4) + round16(b.n * (size_t)s->vb);
@@ -1446,6 +1619,15 @@ int pskv_shard_create_ex(int device, uint32_t key_begin, uint64_t key_end, int d
   if (const char* e = std::getenv("PSKV_INLINE_GET_CHUNKS"))
     s->tune_inline_get_chunks = std::max(1, std::min(kInlineMaxChunks, std::atoi(e)));
   if (const char* e = std::getenv("PSKV_ISPIN")) s->tune_ispin = std::atoi(e) != 0;
+  if (const char* e = std::getenv("PSKV_SERVE")) s->tune_serve = std::atoi(e) != 0;
+  // a ring slot costs the host ~0.2 us where a K8 launch costs 3-7: with the
+  // server, Adds of up to 2 slots (512 keys) take it.  Measured
+  // (tools/micro/small_latency.cpp, Add then Get): 512 keys 17-18 us against
+  // 23-27 through the copy; from 1 Ki keys the server's per-slot work (~6 us
+  // per 256-key slot) is behind the copy (1 Ki: 31-34 against 28)
+  if (s->tune_serve && !std::getenv("PSKV_INLINE_ADD_CHUNKS")) s->tune_inline_add_chunks = 2;
+  if (const char* e = std::getenv("PSKV_SERVE_IDLE_US"))
+    s->tune_serve_idle_us = (uint32_t)std::max(1, std::min(10000000, std::atoi(e)));
   if (const char* e = std::getenv("PSKV_TILE_GRID")) {
     const int v = std::atoi(e);
     if (v >= 1 && v <= 65536) s->tune_tile_grid = (uint32_t)v;
@@ -1488,6 +1670,8 @@ int pskv_shard_create_ex(int device, uint32_t key_begin, uint64_t key_end, int d
   if (rc) return bail(rc);
   if (hipStreamSynchronize(s->stream) != hipSuccess)
     return bail(fail(PSKV_EHIP, "hipStreamSynchronize failed"));
+  if (device < 64) g_device_shards[device].fetch_add(1, std::memory_order_relaxed);
+  s->counted = true;
   *out = s;
   return PSKV_OK;
 }
@@ -1500,6 +1684,17 @@ int pskv_shard_create(int device, uint32_t key_begin, uint64_t key_end, int dtyp
 int pskv_shard_destroy(pskv_shard* s) {
   if (!s) return PSKV_OK;
   (void)hipSetDevice(s->device);
+  if (s->srv) {
+    (void)srv_stop(s);
+    if (s->srv_running) {  // srv_stop failed: make the kernel leave anyway
+      __atomic_store_n(&s->srv->stop, 1u, __ATOMIC_RELEASE);
+      (void)hipStreamSynchronize(s->srv_stream);
+    }
+    (void)hipHostFree(s->srv);
+  }
+  if (s->counted) g_device_shards[s->device].fetch_sub(1, std::memory_order_relaxed);
+  if (s->srv_stream) (void)hipStreamDestroy(s->srv_stream);
+  if (s->srv_dep) (void)hipEventDestroy(s->srv_dep);
   if (s->own_stream) (void)hipStreamSynchronize(s->own_stream);
   if (s->stream && s->stream != s->own_stream) (void)hipStreamSynchronize(s->stream);
   for (auto& t : s->pending) {
@@ -1569,6 +1764,8 @@ int pskv_clear(pskv_shard* s) {
   if (!s) return fail(PSKV_EINVAL, "pskv_clear: null shard");
   int rc = use_device(s);
   if (rc) return rc;
+  rc = srv_stop(s);
+  if (rc) return rc;
   PSKV_HIP(hipMemsetAsync(s->dense, 0, s->range * (size_t)s->vb, s->stream));
   PSKV_HIP(hipMemsetAsync(s->ovf.keys, 0xFF, s->ocap * sizeof(unsigned long long), s->stream));
   PSKV_HIP(hipMemsetAsync(s->ovf.vals, 0, s->ocap * (size_t)s->vb, s->stream));
@@ -1581,6 +1778,8 @@ int pskv_clear(pskv_shard* s) {
 int pskv_set_stream(pskv_shard* s, void* hip_stream) {
   if (!s) return fail(PSKV_EINVAL, "pskv_set_stream: null shard");
   int rc = use_device(s);
+  if (rc) return rc;
+  rc = srv_stop(s);
   if (rc) return rc;
   // order the switch: everything queued so far completes before the new stream's work
   PSKV_HIP(hipStreamSynchronize(s->stream));

@@ -1,0 +1,163 @@
+"""K9 request server (PSKV_SERVE=1): small host messages through a ring in
+page-locked memory that one resident workgroup polls, instead of one kernel
+launch per message.  Same bar as K8: assign bit-exact against
+the oracle, accumulate bit-identical to the sequential loop; plus the
+protocol's own edges: regular (large) calls between ring requests (the server
+is stopped before them and restarted behind them), a server that leaves on
+its idle timer while requests are posted, overflow growth (the server holds
+the table by value), several shards on one device, and teardown.
+"""
+import time
+
+import numpy as np
+import pytest
+
+from test_gpu_parity import _small_messages, assert_bits_equal
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def serve(monkeypatch):
+    monkeypatch.setenv("PSKV_SERVE", "1")
+    return monkeypatch
+
+
+@pytest.mark.parametrize("dt", [np.int32, np.float32, np.float64])
+def test_serve_messages_assign(cuda, oracle_mod, dt, serve):
+    """Adds and Gets of 0..256 / up to 1024 keys, duplicates, out-of-range and
+    sentinel keys, with a large Add and a large Get (the regular path) every
+    25 messages."""
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(4242)
+    kb, ke = 1000, 1000 + 50_000
+    msgs = _small_messages(rng, kb, ke, 150)
+    ref = oracle_mod.MapStorageRef(dt)
+    checks = []
+    with ps.Shard(kb, ke, dt, overflow_slots=64) as sh:
+        for i, k in enumerate(msgs):
+            v = (rng.standard_normal(k.size) * 100).astype(dt)
+            sh.add(k, v)
+            ref.add(k, v)
+            if i % 7 == 3:
+                q = np.concatenate([k[:300], rng.integers(kb - 60, ke + 60, size=int(rng.integers(1, 700)))])
+                q = q.astype(np.uint32)
+                checks.append((sh.get(q), ref.get(q)))
+            if i % 25 == 24:  # the regular path between ring requests
+                big_k = rng.integers(kb, ke, size=20_000).astype(np.uint32)
+                big_v = (rng.standard_normal(big_k.size) * 100).astype(dt)
+                sh.add(big_k, big_v)
+                ref.add(big_k, big_v)
+                q = rng.integers(kb - 60, ke + 60, size=5000).astype(np.uint32)
+                checks.append((sh.get(q), ref.get(q)))
+        q = np.concatenate([np.arange(kb - 60, ke + 60), [0xFFFFFFFF]]).astype(np.uint32)
+        checks.append((sh.get(q), ref.get(q)))
+        sh.sync()
+    for j, (got, want) in enumerate(checks):
+        assert_bits_equal(got, want, f"check {j}")
+
+
+@pytest.mark.parametrize("dt", [np.int32, np.float32, np.float64])
+def test_serve_accumulate_sequential_bits(cuda, dt, serve):
+    """Accumulate through the ring: the first occurrence adds every occurrence
+    in index order, so the result equals np.add.at in the value dtype."""
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(99)
+    kb, ke = 0, 2048
+    msgs = _small_messages(rng, kb, ke, 120)
+    want = np.zeros(ke - kb, dt)
+    want_ovf = {}
+    with ps.Shard(kb, ke, dt, mode="accumulate", overflow_slots=64) as sh:
+        for k in msgs:
+            v = (rng.integers(-2**31, 2**31 - 1, size=k.size, dtype=np.int64).astype(np.int32)
+                 if dt is np.int32 else rng.standard_normal(k.size).astype(dt))
+            sh.add(k, v)
+            inr = k < ke
+            np.add.at(want, k[inr].astype(np.int64) - kb, v[inr])
+            for key, val in zip(k[~inr], v[~inr]):
+                with np.errstate(over="ignore"):
+                    want_ovf[int(key)] = dt(want_ovf.get(int(key), dt(0)) + val)
+        got = sh.get(np.arange(kb, ke, dtype=np.uint32))
+        ok = np.array(sorted(want_ovf), np.uint32)
+        got_ovf = sh.get(ok)
+    assert_bits_equal(got, want, "served accumulate (dense)")
+    assert_bits_equal(got_ovf, np.array([want_ovf[int(x)] for x in ok], dt), "served accumulate (overflow)")
+
+
+def test_serve_idle_restart_and_ring_wrap(cuda, oracle_mod, serve):
+    """A 50 us idle timer: the server leaves between most calls and is
+    restarted, including while requests are queued; bursts longer than the
+    ring (64 slots) wrap it."""
+    import parameter_server_amd as ps
+
+    serve.setenv("PSKV_SERVE_IDLE_US", "50")
+    rng = np.random.default_rng(5)
+    ref = oracle_mod.MapStorageRef(np.float32)
+    with ps.Shard(0, 10_000, np.float32) as sh:
+        for i in range(40):
+            for _ in range(int(rng.integers(1, 150))):  # a burst of Adds, up to 2+ ring laps
+                k = rng.integers(0, 10_000, size=int(rng.integers(1, 40))).astype(np.uint32)
+                v = rng.standard_normal(k.size).astype(np.float32)
+                sh.add(k, v)
+                ref.add(k, v)
+            if i % 3 == 0:
+                time.sleep(0.001)  # idle: the server leaves
+            q = rng.integers(0, 10_000, size=300).astype(np.uint32)
+            assert_bits_equal(sh.get(q), ref.get(q), f"round {i}")
+
+
+def test_serve_overflow_growth(cuda, oracle_mod, serve):
+    """Small messages full of out-of-range keys grow the overflow table many
+    times (the server is stopped, the table rehashed, the server restarted
+    with the new table)."""
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(17)
+    ref = oracle_mod.MapStorageRef(np.float64)
+    with ps.Shard(0, 1000, np.float64, overflow_slots=64) as sh:
+        for _ in range(200):
+            k = rng.integers(0, 200_000, size=200).astype(np.uint32)
+            v = rng.standard_normal(k.size)
+            sh.add(k, v)
+            ref.add(k, v)
+        q = rng.integers(0, 200_000, size=1000).astype(np.uint32)
+        got = sh.get(q)
+        sh.sync()
+        assert sh.info()["overflow_capacity"] >= 2 * sh.info()["overflow_count"]
+    assert_bits_equal(got, ref.get(q), "overflow")
+
+
+@pytest.mark.parametrize("nshards", [2, 4])
+def test_serve_several_shards_one_device(cuda, oracle_mod, serve, nshards):
+    """Shards on one GPU, messages interleaved across them, and device-path
+    calls on some in between.  A resident server holds the hardware queue its
+    stream maps to, so the server engages only while a device has at most
+    GPU_MAX_HW_QUEUES / 2 shards (2 by default); with 4 the shards fall back
+    to the K8 launches, with the same results."""
+    import torch
+
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(8)
+    shards = [ps.Shard(s * 1000, (s + 1) * 1000, np.float64) for s in range(nshards)]
+    refs = [oracle_mod.MapStorageRef(np.float64) for _ in shards]
+    try:
+        for i in range(400):
+            s = int(rng.integers(0, nshards))
+            k = rng.integers(s * 1000, s * 1000 + 1100, size=int(rng.integers(1, 64))).astype(np.uint32)
+            v = rng.standard_normal(k.size)
+            shards[s].add(k, v)
+            refs[s].add(k, v)
+            if i % 50 == 49:
+                dk = torch.arange(s * 1000, s * 1000 + 1000, dtype=torch.int32, device=cuda)
+                dv = torch.full((1000,), float(i), dtype=torch.float64, device=cuda)
+                shards[s].add(dk, dv, sorted_hint=True)
+                refs[s].add(dk.cpu().numpy().view(np.uint32), dv.cpu().numpy())
+        for s, (sh, ref) in enumerate(zip(shards, refs)):
+            q = np.arange(s * 1000, s * 1000 + 1100, dtype=np.uint32)
+            assert_bits_equal(sh.get(q), ref.get(q), f"shard {s}")
+    finally:
+        for sh in shards:
+            sh.close()

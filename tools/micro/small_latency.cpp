@@ -7,6 +7,8 @@
 // The last two variants take the message from page-locked pool frames
 // (pskv_host_alloc): "pinned" passes them as plain host memory (direct DMA),
 // "frames" under PSKV_HOST_FRAME (read and written in place).
+// "serve": the defaults with the K9 request server (PSKV_SERVE=1) in place of
+// the K8 launches.
 //   g++ -O2 -std=c++11 -I include tools/micro/small_latency.cpp \
 //       -L parameter_server_amd -lpskv -Wl,-rpath,$PWD/parameter_server_amd -o /tmp/small_latency
 #include <algorithm>
@@ -64,11 +66,13 @@ int main() {
   // every pageable buffer DMA'd directly; no inline path with every pageable
   // buffer copied into pinned staging
   // and the defaults with medium Gets zero-copy (PSKV_ZC_MAX_BYTES = 4 MiB)
-  const char* names[] = {"default", "inline-sync", "dma-always", "copy-always", "zero-copy", "pinned", "frames"};
-  constexpr int kVariants = 7;
+  const char* names[] = {"default", "inline-sync", "dma-always", "copy-always", "zero-copy", "pinned", "frames",
+                         "serve"};
+  constexpr int kVariants = 8;
   for (int pass = 0; pass < 2; ++pass)  // pass 0 warms the runtime up (its pageable-copy paths); pass 1 prints
   for (int var = 0; var < kVariants; ++var) {
-    const bool framed = var >= 5;
+    const bool framed = var == 5 || var == 6;
+    setenv("PSKV_SERVE", var == 7 ? "1" : "0", 1);  // K9: the resident request server
     const int flags = var == 6 ? PSKV_HOST | PSKV_HOST_FRAME : PSKV_HOST;
     if (var == 4)
       setenv("PSKV_ZC_MAX_BYTES", "4194304", 1);
