@@ -1118,11 +1118,14 @@ __global__ __launch_bounds__(kBinBlock) void k_rb_bin(GroupArgs ga, DenseView d,
     cur = task(blockIdx.x);
     load(cur, kc, vc);
   }
+  ready(kc);  // complete on entry as on the back edge: no wait at the loop top
+  ready(vc);
   for (uint32_t sc = blockIdx.x; sc < nsc; sc += gridDim.x) {
-    // this super-chunk's registers complete BEFORE the next one's loads go out:
-    // the wait-count pass cannot count the next loads (their number depends on
-    // the full / partial branch) and otherwise waited for ALL of them (vmcnt(0))
-    // at the first use of kc below, i.e. for the prefetch it had just issued
+    // kc / vc are complete here (waited for at the end of the previous pass,
+    // before its copy-out stores; the prologue's loads by the compiler): the
+    // wait-count pass cannot count the next loads (their number depends on the
+    // full / partial branch), so a first wait for kc AFTER them would be a
+    // vmcnt(0) for the prefetch just issued
     ready(kc);
     ready(vc);
     if (sc + gridDim.x < nsc) {
@@ -1180,6 +1183,11 @@ __global__ __launch_bounds__(kBinBlock) void k_rb_bin(GroupArgs ga, DenseView d,
     // (hv zero, hk EMPTY; nobody else reads it), the pieces past the staged
     // ones are cleared in the same pass, and so are the bucket counters (last
     // read by the staging above): one barrier where copy and clear took two
+    // the next super-chunk's registers complete HERE, before the copy-out
+    // stores go out: waited for at the top of the next pass instead, the
+    // in-order counter would also wait for those stores' acknowledgements
+    ready(kn);
+    ready(vn);
     const uint32_t n16 = (uint32_t)((total * sizeof(Ent) + 15) / 16);
     u32x4* dst = reinterpret_cast<u32x4*>(tmp + (size_t)sc * SC);
     u32x4* src = reinterpret_cast<u32x4*>(stg);
