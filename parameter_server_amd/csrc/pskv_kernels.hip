@@ -1816,8 +1816,12 @@ __global__ __launch_bounds__(64) void k_inline_get(InlineGet a, DenseView d, Ovf
 // released at system scope before done_seq.  The loop ends on `stop` or after
 // idle_ticks without a request, so the kernel always drains.
 // Workgroup barrier for LDS only: the wave's LDS operations complete, then
-// s_barrier.  __syncthreads would also wait for every outstanding global
-// store (vmcnt(0)), i.e. for the parameter stores' acknowledgements.
+// s_barrier.  __syncthreads emits the same two instructions here, but it is
+// also a workgroup-scope release/acquire for global memory, so the compiler
+// keeps global accesses on their side of it; this one only orders LDS.
+// (Neither waits for outstanding global stores: on gfx950 outside
+// thread-group-split mode a CU's vector memory operations reach L2 in order,
+// so workgroup-scope ordering needs no vmcnt wait — checked in the ISA.)
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 template <typename T>
@@ -1905,8 +1909,8 @@ __global__ __launch_bounds__(kInlineMax) void k_serve(SrvRing* ring, DenseView d
       reinterpret_cast<u32x4*>(s_vals)[tid - 128] = piece;
     }
     // a full barrier: besides the staged message, the previous request's
-    // parameter stores complete (vmcnt(0)) before this one's, so a later
-    // request's store to the same key lands last
+    // parameter stores are ordered before this one's (workgroup-scope
+    // release/acquire), so a later request's store to the same key lands last
     __syncthreads();
     const u32x4* k4 = reinterpret_cast<const u32x4*>(s_keys);
     const int ng = (n + 3) >> 2;
@@ -1964,7 +1968,7 @@ __global__ __launch_bounds__(kInlineMax) void k_serve(SrvRing* ring, DenseView d
       }
       lds_barrier();  // the staged message is read before the next one is staged
     } else {
-      __syncthreads();  // the parameter stores of earlier Adds complete before these loads
+      __syncthreads();  // the parameter stores of earlier Adds are ordered before these loads
       constexpr int PER = kInlineGetMax / kInlineMax;
       const uint32_t roff = (uint32_t)h1;
       BT v[PER];
