@@ -1,0 +1,209 @@
+"""Differential fuzzing of the HIP path against the oracle.
+
+Each scenario draws a shard (key range incl. the ends of the uint32 space and a
+one-key shard, dtype, mode, a tuning knob that selects another host or kernel
+path) and a random sequence of calls — single, grouped (beyond the 64-batch
+launch group), host, device (unaligned pointers, right and WRONG sorted hints),
+inline-sized and large, uniform / Zipf / sorted / dense-window / out-of-range /
+sentinel keys, empty batches, clears — and checks every Get against the
+reference state right away:
+
+  assign      the oracle's MapStorage restatement (server/map_storage.hpp:17-45),
+              bit-exact
+  accumulate  a float64 running sum per key with the recursive-summation bound
+              of DESIGN.md §2; int32 exact (wrap-around)
+
+Seeded: a failure names its scenario and step, and reruns identically.
+"""
+
+import os
+
+import numpy as np
+import pytest
+
+from test_gpu_parity import assert_bits_equal, tdev
+
+pytestmark = pytest.mark.gpu
+
+# scenarios in the default suite (~30 s on MI355X); FUZZ_SCENARIOS=N runs more
+N_SCENARIOS = int(os.environ.get("FUZZ_SCENARIOS", "160"))
+N_STEPS = 18
+KNOBS = [{}, {}, {}, {"PSKV_SERVE": "1"}, {"PSKV_GENERAL": "stamps"}, {"PSKV_INLINE": "0"},
+         {"PSKV_UNROLL": "4"}, {"PSKV_PAGEABLE_DMA": "1"}, {"PSKV_ZC_MAX_BYTES": "0"},
+         {"PSKV_RB_APPLY_LOG2": "13"}]
+SIZES = [0, 1, 5, 100, 256, 257, 1024, 2049, 5000, 40_000, 300_000]
+U32 = 1 << 32
+
+
+class AccRef:
+    """Accumulate reference over any uint32 key: float64 sums, |v| sums and
+    push counts (the tolerance), int64 sums for int32 (wrap at the end)."""
+
+    def __init__(self, dt):
+        self.dt = dt
+        self.clear()
+
+    def clear(self):
+        self.sum, self.abs, self.cnt = {}, {}, {}
+
+    def add(self, keys, vals):
+        if keys.size == 0:
+            return
+        v = vals.astype(np.int64 if self.dt is np.int32 else np.float64)
+        u, inv = np.unique(keys, return_inverse=True)
+        s = np.zeros(u.size, v.dtype)
+        a = np.zeros(u.size, np.float64)
+        c = np.zeros(u.size, np.int64)
+        np.add.at(s, inv, v)  # any order: the tolerance covers every order
+        np.add.at(a, inv, np.abs(v.astype(np.float64)))
+        np.add.at(c, inv, 1)
+        for k, sk, ak, ck in zip(u.tolist(), s.tolist(), a.tolist(), c.tolist()):
+            self.sum[k] = self.sum.get(k, 0) + sk
+            self.abs[k] = self.abs.get(k, 0.0) + ak
+            self.cnt[k] = self.cnt.get(k, 0) + ck
+
+    def check(self, keys, got, what):
+        ks = keys.tolist()
+        if self.dt is np.int32:
+            want = np.array([((self.sum.get(k, 0) + 2**31) % 2**32) - 2**31 for k in ks], np.int64)
+            assert_bits_equal(got, want.astype(np.int32), what)
+            return
+        u = 2.0**-24 if self.dt is np.float32 else 2.0**-53
+        want = np.array([self.sum.get(k, 0.0) for k in ks], np.float64)
+        tol = np.array([1.01 * (self.cnt.get(k, 0) + 1) * u * self.abs.get(k, 0.0) for k in ks])
+        err = np.abs(np.asarray(got, np.float64) - want)
+        bad = np.nonzero(~(err <= tol))[0]
+        assert bad.size == 0, f"{what}: {bad.size} keys beyond tolerance, first {[ks[i] for i in bad[:5]]}"
+
+
+def _keys(rng, kb, ke, n, kind):
+    size = ke - kb
+    if n == 0:
+        return np.empty(0, np.uint32)
+    if kind == "dense" and n <= size:
+        first = int(rng.integers(kb, ke - n + 1))
+        return np.arange(first, first + n, dtype=np.uint64).astype(np.uint32)
+    if kind == "zipf":
+        hot = rng.integers(kb, ke, size=min(size, 64), dtype=np.int64)
+        k = hot[(rng.zipf(1.3, size=n) - 1) % hot.size]
+    else:
+        k = rng.integers(kb, ke, size=n, dtype=np.int64)
+    if kind in ("sorted", "dense"):
+        k = np.sort(k)
+    if kind == "oor":
+        # a few keys outside the shard (both sides when they exist), the
+        # sentinel 0xFFFFFFFF and 0, repeated
+        m = max(1, min(n // 8, 300))
+        pool = [U32 - 1, 0]
+        if kb > 0:
+            pool += [kb - 1] + rng.integers(0, kb, size=8, dtype=np.int64).tolist()
+        if ke < U32:
+            pool += [ke] + rng.integers(ke, U32, size=8, dtype=np.int64).tolist()
+        idx = rng.choice(n, size=m, replace=False)
+        k[idx] = rng.choice(np.array(pool, np.int64), size=m)
+    return k.astype(np.uint32)
+
+
+def _vals(rng, dt, n):
+    if dt is np.int32:
+        return rng.integers(-2**31, 2**31, size=n, dtype=np.int64).astype(np.int32)
+    return (rng.standard_normal(n) * 10.0 ** rng.integers(-3, 4)).astype(dt)
+
+
+def _scenario(seed):
+    rng = np.random.default_rng(1_000_003 * seed + 17)
+    dt = [np.int32, np.float32, np.float64][seed % 3]
+    mode = "accumulate" if seed % 5 in (1, 3) else "assign"
+    size = int(rng.choice([1, 17, 4096, 65_536, 250_000]))
+    kb = int(rng.choice([0, 1000, 2**31 - 7, U32 - size]))
+    knobs = KNOBS[seed % len(KNOBS)]
+    return rng, dt, mode, kb, kb + size, knobs
+
+
+@pytest.mark.parametrize("seed", range(N_SCENARIOS))
+def test_fuzz_against_oracle(cuda, oracle_mod, seed, monkeypatch):
+    import torch
+
+    import parameter_server_amd as ps
+
+    rng, dt, mode, kb, ke, knobs = _scenario(seed)
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    ref = oracle_mod.MapStorageRef(dt) if mode == "assign" else AccRef(dt)
+    keep = []  # device buffers stay alive until the final sync (stream-ordered use)
+    kinds = ["uniform", "zipf", "sorted", "dense", "oor"]
+    where = f"seed {seed} ({np.dtype(dt).name} {mode} [{kb}, {ke}) {knobs})"
+
+    def check(q, got, step):
+        what = f"{where} step {step}"
+        if mode == "assign":
+            assert_bits_equal(got, ref.get(q), what)
+        else:
+            ref.check(q, got, what)
+
+    with ps.Shard(kb, ke, dt, mode=mode, overflow_slots=1 << 14) as sh:
+        for step in range(N_STEPS):
+            op = rng.choice(["add", "add", "add_dev", "add_grouped", "add_grouped_dev",
+                             "get", "get_dev", "get_grouped", "clear"],
+                            p=[.16, .08, .16, .12, .12, .12, .1, .1, .04])
+            kind = str(rng.choice(kinds))
+            if op == "clear":
+                sh.clear()
+                if mode == "assign":
+                    ref.close()
+                ref = oracle_mod.MapStorageRef(dt) if mode == "assign" else AccRef(dt)
+            elif op in ("add", "add_dev"):
+                n = int(rng.choice(SIZES))
+                k, v = _keys(rng, kb, ke, n, kind), _vals(rng, dt, n)
+                if op == "add":
+                    sh.add(k, v)
+                else:
+                    off = int(rng.choice([0, 0, 1, 3]))
+                    hint = bool(rng.random() < 0.6)  # also WRONG hints: repaired
+                    dk, dv = tdev(k, cuda, off), tdev(v, cuda, off)
+                    keep += [dk, dv]
+                    sh.add(dk, dv, sorted_hint=hint)
+                    sh.sync()  # grows the overflow table between device calls
+                ref.add(k, v)
+            elif op in ("add_grouped", "add_grouped_dev"):
+                nb = int(rng.choice([1, 2, 7, 64, 65, 70]))
+                dense = kind == "dense"
+                batches = []
+                for _ in range(nb):
+                    n = int(rng.choice([0, 1, 33, 1000, 8192, 20_001] if not dense else [1, 1000, 8192, 30_000]))
+                    batches.append((_keys(rng, kb, ke, n, kind if dense else str(rng.choice(kinds))),
+                                    None))
+                batches = [(k, _vals(rng, dt, k.size)) for k, _ in batches]
+                if op == "add_grouped":
+                    sh.add_grouped(batches)
+                else:
+                    dev = [(tdev(k, cuda), tdev(v, cuda)) for k, v in batches]
+                    keep += [t for kv in dev for t in kv]
+                    sh.add_grouped(dev, sorted_hint=bool(rng.random() < 0.7))
+                    sh.sync()
+                for k, v in batches:
+                    ref.add(k, v)
+            elif op == "get":
+                q = _keys(rng, kb, ke, int(rng.choice(SIZES)), kind)
+                check(q, sh.get(q), step)
+            elif op == "get_dev":
+                q = _keys(rng, kb, ke, int(rng.choice(SIZES)), kind)
+                out = sh.get(tdev(q, cuda, int(rng.choice([0, 1]))))
+                check(q, out.cpu().numpy(), step)
+            else:
+                nb = int(rng.choice([1, 3, 64, 66]))
+                qs = [_keys(rng, kb, ke, int(rng.choice([0, 1, 300, 5000])), str(rng.choice(kinds)))
+                      for _ in range(nb)]
+                outs = [np.empty(q.size, dt) for q in qs]
+                sh.get_grouped(list(zip(qs, outs)))
+                for q, o in zip(qs, outs):
+                    check(q, o, step)
+        # the whole state at the end: every key of a small shard (or a sample)
+        # plus every out-of-range key any call used
+        q = np.arange(kb, ke, dtype=np.uint64).astype(np.uint32) if ke - kb <= 65_536 else \
+            _keys(rng, kb, ke, 100_000, "uniform")
+        check(q, sh.get(q), "final")
+        sh.sync()
+        torch.cuda.synchronize()
+    if mode == "assign":
+        ref.close()
