@@ -132,12 +132,23 @@ struct VecN<unsigned long long> : Vec2x8 {
   static constexpr int N = 2;
 };
 
-// Which batch of a grouped launch this workgroup serves (wave-uniform scan of
-// the kernarg prefix table; nb <= 64).
+// Which batch of a grouped launch this workgroup serves: the last batch whose
+// first workgroup is at or before `wg` (the prefix table in the kernarg
+// segment is non-decreasing; empty batches repeat a prefix; nb <= 64).  A
+// binary search: at most 6 dependent scalar loads, where a scan that stops at
+// the batch waits for one per batch it passes (~63 for the last batch of a
+// full group) before the workgroup's first memory access.  (Loading the whole
+// table at once needs ~100 SGPRs and costs the gather a wave per SIMD.)
 __device__ __forceinline__ int batch_of(const GroupArgs& ga, uint32_t wg) {
-  int j = 0;
-  while (j + 1 < ga.nb && ga.wg_prefix[j + 1] <= wg) ++j;
-  return j;
+  int lo = 0, hi = ga.nb;  // prefix[lo] <= wg (prefix[0] = 0); the answer is < hi
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (ga.wg_prefix[mid] <= wg)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  return lo;
 }
 
 // ------------------------------------------------------- overflow table
