@@ -96,6 +96,8 @@ enum pskv_mode {
                                 modify such a frame before freeing it; pskv_host_free holds
                                 it back from reuse until every queued call that reads it has
                                 run.  Host pointers outside frames ignore the flag. */
+/* Any other flag bit, or PSKV_HOST_FRAME together with PSKV_DEVICE, is
+ * rejected with PSKV_EINVAL (the call does nothing). */
 
 typedef struct pskv_shard pskv_shard;
 

@@ -1719,14 +1719,23 @@ int pskv_shard_destroy(pskv_shard* s) {
   return PSKV_OK;
 }
 
+// Flag bits a call accepts (pskv.h): a mistyped or foreign flag fails the call
+// instead of silently selecting the host path.
+static bool bad_flags(int flags) {
+  return (flags & ~(PSKV_DEVICE | PSKV_SORTED_HINT | PSKV_HOST_FRAME)) != 0 ||
+         ((flags & PSKV_DEVICE) && (flags & PSKV_HOST_FRAME));
+}
+
 int pskv_add(pskv_shard* s, const uint32_t* keys, const void* vals, uint64_t n, int flags) {
   if (!s) return fail(PSKV_EINVAL, "pskv_add: null shard");
+  if (bad_flags(flags)) return fail(PSKV_EINVAL, "pskv_add: unknown flags");
   pskv_batch b{keys, const_cast<void*>(vals), n};
   return add_impl(s, std::vector<pskv_batch>{b}, flags);
 }
 
 int pskv_get(pskv_shard* s, const uint32_t* keys, uint64_t n, void* out, int flags) {
   if (!s) return fail(PSKV_EINVAL, "pskv_get: null shard");
+  if (bad_flags(flags)) return fail(PSKV_EINVAL, "pskv_get: unknown flags");
   pskv_batch b{keys, out, n};
   return get_impl(s, std::vector<pskv_batch>{b}, flags);
 }
@@ -1734,12 +1743,14 @@ int pskv_get(pskv_shard* s, const uint32_t* keys, uint64_t n, void* out, int fla
 int pskv_add_grouped(pskv_shard* s, const pskv_batch* batches, uint64_t nb, int flags) {
   if (!s) return fail(PSKV_EINVAL, "pskv_add_grouped: null shard");
   if (nb && !batches) return fail(PSKV_EINVAL, "pskv_add_grouped: null batches");
+  if (bad_flags(flags)) return fail(PSKV_EINVAL, "pskv_add_grouped: unknown flags");
   return add_impl(s, std::vector<pskv_batch>(batches, batches + nb), flags);
 }
 
 int pskv_get_grouped(pskv_shard* s, const pskv_batch* batches, uint64_t nb, int flags) {
   if (!s) return fail(PSKV_EINVAL, "pskv_get_grouped: null shard");
   if (nb && !batches) return fail(PSKV_EINVAL, "pskv_get_grouped: null batches");
+  if (bad_flags(flags)) return fail(PSKV_EINVAL, "pskv_get_grouped: unknown flags");
   return get_impl(s, std::vector<pskv_batch>(batches, batches + nb), flags);
 }
 

@@ -1142,3 +1142,62 @@ def test_zero_copy_get_sizes(cuda, oracle_mod, n, monkeypatch):
     for zc, (single, grouped) in res.items():
         assert_bits_equal(single, want, f"single {zc}")
         assert_bits_equal(grouped, want, f"grouped {zc}")
+
+
+def test_c_abi_error_paths_leave_the_shard_usable(cuda, oracle_mod):
+    """Every argument error of the C ABI returns PSKV_EINVAL with a message and
+    changes nothing (the reference aborts on these through CHECK,
+    abstract_storage.hpp:15,20 / map_storage.hpp:20; HipStorage keeps that by
+    aborting on a non-zero status): null pointers with n > 0, null batch arrays,
+    unknown or contradictory flags, bad timing ids, bad create arguments.  The
+    shard then still answers exactly like the oracle."""
+    import ctypes
+
+    import parameter_server_amd as ps
+    from parameter_server_amd import _lib
+
+    L = _lib.lib
+    rng = np.random.default_rng(5)
+    kb, ke = 100, 100 + 10_000
+    ref = oracle_mod.MapStorageRef(np.float32)
+    k = rng.integers(0, 20_000, size=3000).astype(np.uint32)
+    v = rng.standard_normal(3000).astype(np.float32)
+    out = np.zeros(3000, np.float32)
+    with ps.Shard(kb, ke, np.float32) as sh:
+        sh.add(k, v)
+        ref.add(k, v)
+        h = sh.handle
+        kp, vp, op = k.ctypes.data, v.ctypes.data, out.ctypes.data
+        bad = [
+            ("pskv_add: null keys", lambda: L.pskv_add(h, None, vp, 10, _lib.PSKV_HOST)),
+            ("pskv_add: null keys", lambda: L.pskv_add(h, kp, None, 10, _lib.PSKV_HOST)),
+            ("pskv_get: null keys", lambda: L.pskv_get(h, None, 10, op, _lib.PSKV_HOST)),
+            ("pskv_get: null keys", lambda: L.pskv_get(h, kp, 10, None, _lib.PSKV_HOST)),
+            ("unknown flags", lambda: L.pskv_add(h, kp, vp, 10, 0x8)),
+            ("unknown flags", lambda: L.pskv_add(h, kp, vp, 10, _lib.PSKV_DEVICE | _lib.PSKV_HOST_FRAME)),
+            ("unknown flags", lambda: L.pskv_get(h, kp, 10, op, 0x40)),
+            ("null batches", lambda: L.pskv_add_grouped(h, None, 3, _lib.PSKV_HOST)),
+            ("null batches", lambda: L.pskv_get_grouped(h, None, 3, _lib.PSKV_HOST)),
+            ("bad argument", lambda: L.pskv_kernel_time(h, 999, None, None, None)),
+            ("null argument", lambda: L.pskv_shard_info(h, None)),
+        ]
+        for msg, call in bad:
+            assert call() == _lib.PSKV_EINVAL, msg
+            assert msg.encode() in L.pskv_last_error(), (msg, L.pskv_last_error())
+        arr = (_lib.PskvBatch * 2)(_lib.PskvBatch(kp, vp, 5), _lib.PskvBatch(None, vp, 5))
+        assert L.pskv_add_grouped(h, arr, 2, _lib.PSKV_HOST) == _lib.PSKV_EINVAL
+        # nothing above changed the shard; empty calls are legal no-ops
+        assert L.pskv_add(h, None, None, 0, _lib.PSKV_HOST) == _lib.PSKV_OK
+        assert L.pskv_get(h, None, 0, None, _lib.PSKV_HOST) == _lib.PSKV_OK
+        sh.sync()
+        q = np.concatenate([k, rng.integers(0, 2**32, size=500).astype(np.uint32)])
+        assert_bits_equal(sh.get(q), ref.get(q), "after rejected calls")
+    hh = ctypes.c_void_p()
+    for args, msg in [((0, 5, 5, _lib.PSKV_F32, 0), b"key_begin"),
+                      ((0, 0, 2**32 + 1, _lib.PSKV_F32, 0), b"key_begin"),
+                      ((0, 0, 100, 9, 0), b"dtype"),
+                      ((0, 0, 100, _lib.PSKV_F32, 5), b"mode"),
+                      ((1000, 0, 100, _lib.PSKV_F32, 0), b"device")]:
+        assert L.pskv_shard_create(*args, ctypes.byref(hh)) == _lib.PSKV_EINVAL, args
+        assert msg in L.pskv_last_error(), (args, L.pskv_last_error())
+    ref.close()
