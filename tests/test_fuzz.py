@@ -28,6 +28,7 @@ pytestmark = pytest.mark.gpu
 # scenarios in the default suite (~30 s on MI355X); FUZZ_SCENARIOS=N runs more
 N_SCENARIOS = int(os.environ.get("FUZZ_SCENARIOS", "160"))
 N_STEPS = 18
+N_GROUPS = int(os.environ.get("FUZZ_GROUPS", "4"))  # concurrent groups of 6 shards
 KNOBS = [{}, {}, {}, {"PSKV_SERVE": "1"}, {"PSKV_GENERAL": "stamps"}, {"PSKV_INLINE": "0"},
          {"PSKV_UNROLL": "4"}, {"PSKV_PAGEABLE_DMA": "1"}, {"PSKV_ZC_MAX_BYTES": "0"},
          {"PSKV_RB_APPLY_LOG2": "13"}]
@@ -122,13 +123,45 @@ def _scenario(seed):
 
 @pytest.mark.parametrize("seed", range(N_SCENARIOS))
 def test_fuzz_against_oracle(cuda, oracle_mod, seed, monkeypatch):
+    rng, dt, mode, kb, ke, knobs = _scenario(seed)
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    _run(cuda, oracle_mod, seed, rng, dt, mode, kb, ke, knobs)
+
+
+@pytest.mark.parametrize("group", range(N_GROUPS))
+def test_fuzz_concurrent_shards(cuda, oracle_mod, group):
+    """Six scenarios at once, each on its own shard of the same GPU from its
+    own host thread (pskv.h: distinct handles may be used concurrently — the
+    reference runs one storage per ServerThread, simple_id_mapper.cpp:28-31):
+    the shared host staging pool, frame pool and device must not mix them up.
+    ctypes releases the GIL for every library call, so the calls overlap."""
+    import threading
+
+    errs = []
+
+    def worker(seed):
+        try:
+            rng, dt, mode, kb, ke, _ = _scenario(seed)
+            _run(cuda, oracle_mod, seed, rng, dt, mode, kb, ke, {})
+        except BaseException as e:  # noqa: B902 - re-raised in the main thread
+            errs.append(e)
+
+    ts = [threading.Thread(target=worker, args=(100_000 + 6 * group + i,)) for i in range(6)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=100)
+    assert not any(t.is_alive() for t in ts), "a worker thread did not finish"
+    if errs:
+        raise errs[0]
+
+
+def _run(cuda, oracle_mod, seed, rng, dt, mode, kb, ke, knobs):
     import torch
 
     import parameter_server_amd as ps
 
-    rng, dt, mode, kb, ke, knobs = _scenario(seed)
-    for k, v in knobs.items():
-        monkeypatch.setenv(k, v)
     ref = oracle_mod.MapStorageRef(dt) if mode == "assign" else AccRef(dt)
     keep = []  # device buffers stay alive until the final sync (stream-ordered use)
     kinds = ["uniform", "zipf", "sorted", "dense", "oor"]
