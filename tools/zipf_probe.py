@@ -23,7 +23,7 @@ def main():
     variants = sys.argv[1:] or [""]
     J = int(os.environ.get("PROBE_J", "8"))
     rounds = int(os.environ.get("PROBE_ROUNDS", "5"))
-    space, B = 100_000_000, 1_000_000
+    space, B = int(float(os.environ.get("PROBE_SPACE", "1e8"))), 1_000_000
     dev = torch.device("cuda:0")
     if os.environ.get("PROBE_WORKLOAD", "zipf") == "dense":
         zb = workload.dense_batches(J, space, batch=B, device=dev)
