@@ -70,6 +70,7 @@ __device__ __forceinline__ bool chunk_of(const Win& w, uint32_t c, int& j, uint3
 // MODE 6: MODE 3 behind a K2g-style prologue: waves 0-1 load the first and last
 //         key of every window (128 dependent scattered loads) and the workgroup
 //         waits for them (barrier) before its chunk loads
+// MODE 7: MODE 3 checking all four keys of every 16-byte group (as K2g does)
 template <int MODE, int U, bool STNT, bool KNT = true, bool VNT = true>
 __global__ __launch_bounds__(kB) void k_mix(const uint32_t* __restrict__ keys,
                                             const uint32_t* __restrict__ vals,
@@ -119,7 +120,7 @@ __global__ __launch_bounds__(kB) void k_mix(const uint32_t* __restrict__ keys,
       st<STNT>(param + k0, v[u]);
     }
   } else {
-    const bool cov = (MODE == 3 || MODE == 6) && w.covered[j];
+    const bool cov = (MODE == 3 || MODE == 6 || MODE == 7) && w.covered[j];
     u32x4 k[U], v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) k[u] = ld<KNT>(keys + g0 + (u * kB + t) * 4);
@@ -130,7 +131,10 @@ __global__ __launch_bounds__(kB) void k_mix(const uint32_t* __restrict__ keys,
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t k0 = first + base + (u * kB + t) * 4;
-      b |= k[u].x != k0 || k[u].w != k0 + 3;
+      if (MODE == 7)
+        b |= (k[u].x != k0) | (k[u].y != k0 + 1) | (k[u].z != k0 + 2) | (k[u].w != k0 + 3);
+      else
+        b |= k[u].x != k0 || k[u].w != k0 + 3;
       if (!cov) {
         if (MODE == 5)
           st<STNT>(out + g0 + (u * kB + t) * 4, v[u]);
@@ -175,8 +179,10 @@ int main() {
   CK(hipEventCreate(&ev0));
   CK(hipEventCreate(&ev1));
   std::printf("%d of %d windows covered by a later one\n", ncov, kJ);
+  // lds > 0: dynamic LDS per workgroup that caps the workgroups per CU (30 KiB:
+  // 5 per CU = 5 waves per SIMD, K2g's register-limited occupancy)
   auto run = [&](const char* name, auto kern, int U, double bytes_per_key_full, double bytes_cov,
-                 bool sorted = false) {
+                 bool sorted = false, size_t lds = 0) {
     const uint32_t CH = kB * 4 * U;
     const uint32_t grid = kJ * (kN / CH);
     const double keys_done = (double)grid * CH;
@@ -185,7 +191,7 @@ int main() {
     std::vector<float> ts;
     for (int r = 0; r < 30; ++r) {
       CK(hipEventRecord(ev0, 0));
-      kern<<<grid, kB, 0, 0>>>(keys, vals, param, out, sorted ? ws : w, bad);
+      kern<<<grid, kB, lds, 0>>>(keys, vals, param, out, sorted ? ws : w, bad);
       CK(hipEventRecord(ev1, 0));
       CK(hipEventSynchronize(ev1));
       float ms;
@@ -218,6 +224,10 @@ int main() {
     run("vals->param only, windows in base order", k_mix<2, 8, false>, 8, 8, 8, true);
     run("K1 gather, windows in base order", k_mix<0, 8, false>, 8, 12, 12, true);
     run("K1 gather U=4", k_mix<0, 4, false>, 4, 12, 12);
+    run("K2g covered-skip, all four keys checked", k_mix<7, 8, false>, 8, 12, 4);
+    run("K2g covered-skip, all keys, 5 waves/SIMD", k_mix<7, 8, false>, 8, 12, 4, false, 30 << 10);
+    run("K2g covered-skip, 5 waves/SIMD", k_mix<3, 8, false>, 8, 12, 4, false, 30 << 10);
+    run("K1 gather, 5 waves/SIMD", k_mix<0, 8, false>, 8, 12, 12, false, 30 << 10);
   }
   uint32_t hb = 0;
   CK(hipMemcpy(&hb, bad, 4, hipMemcpyDeviceToHost));
