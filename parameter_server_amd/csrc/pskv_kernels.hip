@@ -558,10 +558,27 @@ __device__ __forceinline__ bool dense_chunk(const GroupArgs& ga, const DenseView
       }
     }
   } else {
-    for (uint64_t i = base + tid; i < end; i += kBlock) {
-      const uint32_t k = keys[i];
-      bad |= k != first + (uint32_t)i;
-      if (!shadowed(first + (uint32_t)i)) param[(first + (uint32_t)i) - d.key_begin] = vals[i];
+    // a partial (or unaligned) chunk — the last one of every window: eight
+    // elements per lane loaded together, then checked and stored, so the
+    // chunk costs one dependent round trip per eight elements per lane rather
+    // than one per element (a window's 576-key tail took three in a row)
+    for (uint64_t i0 = base + tid; i0 < end; i0 += 8ull * kBlock) {
+      uint32_t kk[8];
+      VT vv[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const uint64_t i = i0 + (uint64_t)q * kBlock;
+        kk[q] = i < end ? keys[i] : 0u;
+        vv[q] = i < end ? vals[i] : VT(0);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const uint64_t i = i0 + (uint64_t)q * kBlock;
+        if (i >= end) continue;
+        const uint32_t k = first + (uint32_t)i;
+        bad |= kk[q] != k;
+        if (!shadowed(k)) param[k - d.key_begin] = vv[q];
+      }
     }
   }
   return bad;

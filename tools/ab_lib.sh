@@ -1,0 +1,17 @@
+#!/bin/bash
+# A/B two builds of libpskv.so on one box (ab/libpskv_base.so, ab/libpskv_new.so,
+# built beforehand): alternate them under bench.py
+# (swapping the in-tree library file), N rounds each.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$PWD}
+OUT=$R/gpurun_out/${1:-ab}
+ARGS=${2:-"--no-extra --no-cpu-baseline --no-zipf"}
+mkdir -p "$OUT"
+for i in 1 2 3; do
+  for v in base new; do
+    cp "$R/ab/libpskv_$v.so" "$R/parameter_server_amd/libpskv.so" || exit 1
+    timeout -k 10 200 python3 "$R/bench.py" $ARGS > "$OUT/$v$i.json" 2> "$OUT/$v$i.err" || exit 2
+  done
+done
+cp "$R/ab/libpskv_new.so" "$R/parameter_server_amd/libpskv.so"
+echo "ab done"
