@@ -27,6 +27,7 @@ pytestmark = pytest.mark.gpu
 
 # scenarios in the default suite (~30 s on MI355X); FUZZ_SCENARIOS=N runs more
 N_SCENARIOS = int(os.environ.get("FUZZ_SCENARIOS", "160"))
+SEED0 = int(os.environ.get("FUZZ_SEED0", "0"))  # first scenario seed (longer runs: new seeds)
 N_STEPS = 18
 N_GROUPS = int(os.environ.get("FUZZ_GROUPS", "4"))  # concurrent groups of 6 shards
 KNOBS = [{}, {}, {}, {"PSKV_SERVE": "1"}, {"PSKV_GENERAL": "stamps"}, {"PSKV_INLINE": "0"},
@@ -121,7 +122,7 @@ def _scenario(seed):
     return rng, dt, mode, kb, kb + size, knobs
 
 
-@pytest.mark.parametrize("seed", range(N_SCENARIOS))
+@pytest.mark.parametrize("seed", range(SEED0, SEED0 + N_SCENARIOS))
 def test_fuzz_against_oracle(cuda, oracle_mod, seed, monkeypatch):
     rng, dt, mode, kb, ke, knobs = _scenario(seed)
     for k, v in knobs.items():
