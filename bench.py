@@ -1,22 +1,38 @@
 """bench.py — device-resident KV Add+Get throughput (BASELINE.json metric).
 
-One step = one pass of the hot path over one batch set: a grouped Add of J
-push batches (1M keys each) followed by a grouped Get of the same J pull
-batches, on every rank's shard.  Inputs are resident in HBM before timing.
-Consecutive steps rotate over R window sets (--sets, default 4; set r drawn
-with seed set_seed(r), set 0 being the config's own seed), so a step never
-re-pushes the windows of the step before it: the parameters a step touches are
-not left in the 256 MB Infinity Cache by the previous step.  (The round-1 form,
-the same set every step, is kept as extra.fixed_set_step, labelled cache-warm.)
+One step = one pass of the hot path over one push set and one pull set: a
+grouped Add of the step's push batches, then a grouped Get of the batches the
+NEXT step will push — the parameter-server worker loop, pipelined: push this
+round's parameters, pull the ones the next round updates.  Consecutive steps
+rotate over R window sets (--sets, default 4; set r drawn with seed
+set_seed(r), set 0 being the config's own seed).  The Get therefore reads
+parameters the step did not just write (the windows both sets share aside), and
+a step touches more than 256 MB of parameters (push set ∪ pull set, reported as
+config.param_bytes_touched_per_step), so the Infinity Cache cannot hold them
+from the Add to the Get.  The round-2 form (the Get pulls the windows it just
+pushed: 192 MB of parameters, Infinity-Cache warm) is kept as
+extra.cache_warm_step.  Inputs are resident in HBM before timing.
 
   N = 1: configs[1] (cfg 2) — 1e8-key float shard, J x 1M contiguous-key
          windows at uniform 1M-aligned bases (seed 42 for set 0), vals U(-1,1),
          assign mode.
   N > 1: configs[3] (cfg 4) — 1e9 keys range-partitioned over N GPUs (one
-         shard per rank, base/range_partition_manager.hpp's map); each rank's
-         producers push J x 1M windows routed to it by the range map
-         (weak scaling: per-GPU work fixed).  No collective on the data path;
-         torch.distributed (RCCL) only for the barrier and the max-time reduce.
+         shard per rank, base/range_partition_manager.hpp's map).  J = 64
+         producer streams; stream s pushes a contiguous 1M window at a uniformly
+         random base in [0, 1e9 - 1M] (seed 1000 + s for set 0), which the range
+         map slices — a window straddling a boundary splits in two.  Each rank
+         applies the slices routed to it, in producer order, as one grouped
+         Add (the server's grouped flush), and pulls likewise.  The total work
+         per step is fixed (64 windows): "scaling": "strong".  The weak-scaled
+         form (64 windows inside every rank's own range) is extra.weak_scaled.
+         No collective on the data path; torch.distributed (RCCL) only for the
+         barrier and the max-time / sum-bytes reductions.
+
+Bytes per step (counting what the step must move):
+  Add (assign)  n*4 keys + u*V values + u*V parameter writes, u = distinct keys
+                pushed (only the last push of a key needs its value read: a
+                window shadowed by a later one in the step costs its keys only)
+  Get           q*(4+2V) (key read + parameter read + value write)
 
 Prints ONE JSON line on rank 0 with roofline (dominant kernel, HIP events on
 the launch stream) and cpu_baseline (the oracle restatement of the reference
@@ -38,25 +54,21 @@ sys.path.insert(0, ROOT)
 METRIC = "device-resident KV Add+Get GB/s (grad+param bytes) at 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
 V = 4  # f32 values
-# Algorithmic bytes, counted conservatively per step:
-#   Add (assign): n*(4+V) input + u*V param write, u = DISTINCT keys pushed in the
-#                 step (a window pushed twice in one step is written once: the
-#                 grouped Add skips writes a later batch overwrites)
-#   Get:          q*(4+2V) (key read + param read + value write)
 
 
-def step_bytes(n_push, u_push, n_pull):
-    add = n_push * (4 + V) + u_push * V
-    get = n_pull * (4 + 2 * V)
+def step_bytes(n_push, u_push, n_pull, vb=V):
+    """Algorithmic bytes of one step's Add and Get (module docstring)."""
+    add = n_push * 4 + 2 * u_push * vb
+    get = n_pull * (4 + 2 * vb)
     return add, get
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--batches", type=int, default=64, help="push/pull batches per step per GPU")
+    p.add_argument("--batches", type=int, default=64, help="push batches (N=1) / producer streams (N>1) per step")
     p.add_argument("--batch-keys", type=int, default=1_000_000)
     p.add_argument("--sets", type=int, default=4, help="window sets rotated over the steps")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -64,14 +76,16 @@ def parse():
     p.add_argument("--no-zipf", action="store_true", help="skip the cfg-3 sparse (Zipf) measurement")
     p.add_argument("--cpu-batches", type=int, default=64,
                    help="1M-key windows in the 1-thread CPU baseline sample (~10 s)")
-    return p.parse_args()
+    p.add_argument("--vector-sizes", default="100000,200000,300000",
+                   help="VectorStorage restatement sample sizes (quadratic fit to 1e6)")
+    return p.parse_args(argv)
 
 
 def dist_init(args):
     """One process per GPU (torchrun).  RCCL ("nccl") carries only the barrier and
-    the two scalar reductions.  Rehearsal knobs for a 1-GPU box (never used by the
+    the scalar reductions.  Rehearsal knobs for a 1-GPU box (never used by the
     driver): PSKV_BENCH_BACKEND=gloo and PSKV_BENCH_SHARE_GPU=1 put every rank on
-    cuda:0 and synchronise over gloo."""
+    cuda:0 and synchronise over gloo (tests/test_dist_gpu.py)."""
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -128,10 +142,19 @@ def sum_over_ranks(x, world, dev):
     return float(t.item())
 
 
-def plan_rank(rank, world, J, B, r=0):
-    """Key range and push-window bases (window set r) of one rank (pure host
-    logic; tested with gloo in tests/test_dist.py).  N = 1: cfg 2.  N > 1: cfg 4
-    weak scaling."""
+# ------------------------------------------------------------------ planning
+
+
+def plan_rank(rank, world, J, B, r=0, weak=False, bases=None):
+    """Key range and window slices (window set r) of one rank — pure host logic,
+    tested on CPU (tests/test_oracle.py, tests/test_dist.py with gloo).
+
+    Returns (key_space, lo, hi, slices, bases): slices = [(window w, first key,
+    length)] routed to this rank, in producer order; bases = the set's window
+    bases (every rank's).  N = 1: cfg 2.  N > 1: cfg 4 (global producer windows
+    through the range map), or with weak=True the weak-scaled form (J aligned
+    windows inside this rank's range).  `bases` (N > 1) replaces the drawn
+    producer windows (tests)."""
     from parameter_server_amd import workload
 
     seed = workload.set_seed(r, world)
@@ -139,37 +162,182 @@ def plan_rank(rank, world, J, B, r=0):
         key_space = 100_000_000
         lo, hi = 0, key_space
         bases = workload.dense_bases(J, key_space, B, seed=seed)
-    else:
-        key_space = 1_000_000_000
-        ranges = workload.rank_ranges(key_space, world)
-        lo, hi = ranges[rank]
+        slices = [(j, int(b), B) for j, b in enumerate(bases)]
+        return key_space, lo, hi, slices, bases
+    key_space = 1_000_000_000
+    ranges = workload.rank_ranges(key_space, world)
+    lo, hi = ranges[rank]
+    if weak:
         bases = workload.rank_windows(rank, world, key_space, J, B, seed=seed)
         routed = workload.route_windows(bases, B, ranges)
-        # every window of this rank's producers is routed to this rank, whole
-        assert all(len(routed[r]) == 0 for r in range(world) if r != rank)
+        # every window of this rank's producers lands on this rank, whole
+        assert all(len(routed[q]) == 0 for q in range(world) if q != rank)
         assert len(routed[rank]) == J and all(n == B for _, _, n in routed[rank])
-    return key_space, lo, hi, bases
+    else:
+        if bases is None:
+            bases = workload.global_windows(J, key_space, B, seed=seed)
+        routed = workload.route_windows(bases, B, ranges)
+    slices = [(w, int(bases[w]) + off, n) for w, off, n in routed[rank]]
+    return key_space, lo, hi, slices, bases
 
 
-def make_workload(rank, world, J, B, dev, r=0):
-    """Window set r of this rank: J (keys, vals) push batches in HBM."""
+def window_vals(w, r, B, dev, rank=0, weak=False, dtype=None):
+    """The value stream of producer w in window set r: U(-1, 1), seed
+    42 + w + 100000 r (+ 1000 rank in the weak-scaled form, whose producers
+    are per rank).  Every rank draws a window's values alike, so a straddling
+    window's two slices carry its values."""
     import torch
 
-    key_space, lo, hi, bases = plan_rank(rank, world, J, B, r)
+    g = torch.Generator(device=dev)
+    g.manual_seed(42 + w + 100_000 * r + (1000 * rank if weak else 0))
+    return torch.rand(B, generator=g, device=dev, dtype=dtype or torch.float32) * 2 - 1
+
+
+def make_set(rank, world, J, B, dev, r=0, weak=False, dtype=None, bases=None):
+    """Window set r of this rank in HBM: (slices, [(keys, vals)], distinct keys)."""
+    import torch
+
+    _, lo, hi, slices, bases = plan_rank(rank, world, J, B, r, weak, bases)
     batches = []
-    for j, b in enumerate(bases):
-        keys = torch.arange(int(b), int(b) + B, dtype=torch.int64, device=dev).to(torch.int32)
-        g = torch.Generator(device=dev)
-        g.manual_seed(42 + j + 1000 * rank + 100_000 * r)
-        vals = torch.rand(B, generator=g, device=dev, dtype=torch.float32) * 2 - 1
+    for w, first, n in slices:
+        keys = torch.arange(first, first + n, dtype=torch.int64, device=dev).to(torch.int32)
+        off = first - int(bases[w])
+        vals = window_vals(w, r, B, dev, rank, weak, dtype)[off:off + n].clone()  # own, aligned buffer
         batches.append((keys, vals))
-    return key_space, lo, hi, bases, batches
+    from parameter_server_amd import workload
+
+    u = workload.interval_union([(f, n) for _, f, n in slices])
+    return {"slices": slices, "batches": batches, "u": u, "r": r}
 
 
-def cpu_baseline(bases, B, n_batches):
+class Form:
+    """One way of running the step over R window sets on a shard: step i pushes
+    set i % R and pulls set (i + shift) % R (shift 1: the headline; 0: the
+    cache-warm round-2 form)."""
+
+    def __init__(self, shard, sets, shift, dev, vb=V, sorted_hint=True):
+        import torch
+
+        self.shard, self.sets, self.shift, self.R, self.vb = shard, sets, shift, len(sets), vb
+        self.hint = sorted_hint
+        tdt = {4: torch.float32, 8: torch.float64}[vb]
+        self.outs = [[torch.empty(k.numel(), dtype=tdt, device=dev) for k, _ in s["batches"]] for s in sets]
+        self.adds = [shard.prepare(s["batches"]) for s in sets]
+        self.gets = [shard.prepare([(k, o) for (k, _), o in zip(s["batches"], outs)], is_get=True)
+                     for s, outs in zip(sets, self.outs)]
+        self.add_b = [step_bytes(sum(n for _, _, n in s["slices"]), s["u"], 0, vb)[0] for s in sets]
+        self.get_b = [step_bytes(0, 0, sum(n for _, _, n in s["slices"]), vb)[1] for s in sets]
+
+    def pull_of(self, i):
+        return (i + self.shift) % self.R
+
+    def step(self, i):
+        self.shard.add_grouped(self.adds[i % self.R], sorted_hint=self.hint)
+        self.shard.get_grouped(self.gets[self.pull_of(i)])
+
+    def bytes(self, steps):
+        """(add bytes, get bytes) of steps 0..steps-1."""
+        a = sum(self.add_b[i % self.R] for i in range(steps))
+        g = sum(self.get_b[self.pull_of(i)] for i in range(steps))
+        return a, g
+
+    def touched(self, i):
+        """Distinct parameter bytes step i reads or writes (push set ∪ pull set)."""
+        from parameter_server_amd import workload
+
+        iv = [(f, n) for s in (self.sets[i % self.R], self.sets[self.pull_of(i)]) for _, f, n in s["slices"]]
+        return workload.interval_union(iv) * self.vb
+
+    def self_check(self, lo, hi, dev):
+        """From a cleared shard, run one rotation and compare every pull with a
+        torch model of the shard (sequential last-write-wins slice assigns,
+        map_storage.hpp:22-23) — the benchmarked state is the reference's."""
+        import torch
+
+        self.shard.clear()
+        ref = torch.zeros(hi - lo, dtype={4: torch.float32, 8: torch.float64}[self.vb], device=dev)
+        for i in range(self.R):
+            for (_, first, n), (_, v) in zip(self.sets[i % self.R]["slices"], self.sets[i % self.R]["batches"]):
+                ref[first - lo:first - lo + n] = v
+            self.step(i)
+            torch.cuda.synchronize()
+            t = self.pull_of(i)
+            for (_, first, n), o in zip(self.sets[t]["slices"], self.outs[t]):
+                if not torch.equal(o, ref[first - lo:first - lo + n]):
+                    raise AssertionError(f"bench self-check failed: step {i}, pull of set {t}, key {first}")
+        del ref
+
+
+def timed(form, steps, world, dev):
+    """Exactly `steps` steps bracketed by barrier + synchronize on both sides.
+    Returns (max over ranks of this rank's elapsed time, own elapsed)."""
+    import torch
+
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        form.step(i)
+    torch.cuda.synchronize()
+    own = time.perf_counter() - t0
+    barrier(world)
+    return max_over_ranks(own, world, dev), own
+
+
+def evented(form, steps, world, dev):
+    """The same steps again with HIP events around the two streaming kernels on
+    their launch stream: per-kernel launches and average duration, and the
+    algorithmic bytes per launch (this rank's)."""
+    import torch
+
+    from parameter_server_amd import _lib
+
+    sh = form.shard
+    sh.reset_timing()
+    sh.set_timing(True, kernels=[_lib.PSKV_K_GATHER, _lib.PSKV_K_ASSIGN_TILES])
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    for i in range(steps):
+        form.step(i)
+    torch.cuda.synchronize()
+    t3 = time.perf_counter()
+    sh.set_timing(False)
+    add_b, get_b = form.bytes(steps)
+    ktimes = {}
+    for k, name in _lib.KERNEL_NAMES.items():
+        t = sh.kernel_time(k)
+        if t["launches"]:
+            b = get_b if k == _lib.PSKV_K_GATHER else add_b
+            rec = {"launches": t["launches"], "avg_ms": t["total_ms"] / t["launches"],
+                   "keys_per_launch": t["elements"] / t["launches"],
+                   "algorithmic_bytes": b / t["launches"]}
+            rec["GB/s"] = rec["algorithmic_bytes"] / (rec["avg_ms"] / 1e3) / 1e9
+            ktimes[name] = rec
+    sh.sync()
+    return ktimes, max_over_ranks(t3 - t2, world, dev)
+
+
+def run_form(form, steps, warmup, world, dev):
+    """Warm up, time, and sum the bytes over ranks: the aggregate GB/s of a form."""
+    import torch
+
+    for i in range(warmup):
+        form.step(i)
+    torch.cuda.synchronize()
+    elapsed, own = timed(form, steps, world, dev)
+    a, g = form.bytes(steps)
+    total = sum_over_ranks(float(a + g), world, dev)
+    return {"GB/s": total / elapsed / 1e9, "ms_per_step": elapsed / steps * 1e3, "elapsed": elapsed,
+            "own_GB/s": (a + g) / own / 1e9, "bytes": total}
+
+
+# ------------------------------------------------------------ CPU baseline
+
+
+def cpu_baseline(bases, B, n_batches, vector_sizes):
     """The oracle (C++ restatement of server/map_storage.hpp, 1 thread) on a
-    bounded sample of the same workload; plus VectorStorage at 1e5 keys (cfg 1
-    sample; it is O(stored x queried))."""
+    bounded sample of the same workload; VectorStorage (cfg 1) at several sizes
+    with the quadratic fit extrapolated to config 1's 1e6 keys."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test infrastructure: the CPU baseline leg
 
@@ -184,15 +352,7 @@ def cpu_baseline(bases, B, n_batches):
     for k in ks:
         m.get(k)
     t_map = time.perf_counter() - t0
-    n = 100_000
-    vec = oracle.VectorStorageRef(np.float32)
-    k = np.arange(n, dtype=np.uint32)
-    v = (0.5 * k).astype(np.float32)
-    t0 = time.perf_counter()
-    vec.add(k, v)
-    got = vec.get(k)
-    t_vec = time.perf_counter() - t0
-    assert np.array_equal(got, v)
+    vector = vector_storage_fit(oracle, vector_sizes)
     # 8 server threads with 8 storages (the reference runs one
     # storage per server thread); ctypes drops the GIL inside the oracle calls
     import threading
@@ -217,26 +377,55 @@ def cpu_baseline(bases, B, n_batches):
     for x in th:
         x.join()
     t_mt = time.perf_counter() - t0
-    # same byte accounting as the GPU value (u = distinct keys pushed)
-    add_b, get_b = step_bytes(B * len(ks), B * len(set(int(b) for b in bases[:n_batches])), B * len(ks))
+    # same byte accounting as the GPU value (u = distinct keys pushed; the Get
+    # of the same windows)
+    u = B * len(set(int(b) for b in bases[:n_batches]))
+    add_b, get_b = step_bytes(B * len(ks), u, B * len(ks))
+    u_mt = B * len(set(int(b) for b in bases[:mt_batches]))
     return {
         "value": (add_b + get_b) / t_map / 1e9,
         "unit": "GB/s",
         "cores": 1,
         "kind": "port",
         "sample": f"MapStorage restatement (std::map, 1 thread), {len(ks)} x {B} contiguous float keys of the "
-                  f"same workload, Add then Get, {t_map:.2f} s",
-        "vector_storage": {
-            "value": 24.0 * n / t_vec / 1e9, "unit": "GB/s", "seconds": t_vec,
-            "sample": f"VectorStorage restatement (append + O(stored x queried) scan), 1e5 contiguous float "
-                      f"keys (config 1 at 1/10 size; the 1e6 case is ~100x longer, quadratic)",
-        },
+                  f"same workload (window set 0), Add then Get, {t_map:.2f} s",
+        "vector_storage": vector,
         "eight_threads": {
-            "value": sum(step_bytes(B * mt_batches, B * len(set(int(b) for b in bases[:mt_batches])),
-                                    B * mt_batches)) * T / t_mt / 1e9, "unit": "GB/s", "cores": T, "seconds": t_mt,
+            "value": sum(step_bytes(B * mt_batches, u_mt, B * mt_batches)) * T / t_mt / 1e9, "unit": "GB/s",
+            "cores": T, "seconds": t_mt,
             "sample": f"{T} threads x one MapStorage restatement each, {mt_batches} x {B} keys per thread"},
         "host_cpu": _cpu_model(),
     }
+
+
+def vector_storage_fit(oracle, sizes):
+    """Config 1 (VectorStorage Add+Get of n contiguous float keys,
+    server/vector_storage_test.cpp's shape) timed at several n; Get is the
+    O(stored x queried) scan of vector_storage.hpp:34-43, so t(n) is fitted with
+    a quadratic and extrapolated to the config's 1e6 keys."""
+    pts = []
+    for n in sizes:
+        vec = oracle.VectorStorageRef(np.float32)
+        k = np.arange(n, dtype=np.uint32)
+        v = (0.5 * k).astype(np.float32)
+        t0 = time.perf_counter()
+        vec.add(k, v)
+        got = vec.get(k)
+        t = time.perf_counter() - t0
+        assert np.array_equal(got, v)
+        pts.append((n, t))
+        vec.close()
+    ns = np.array([p[0] for p in pts], dtype=np.float64)
+    ts = np.array([p[1] for p in pts], dtype=np.float64)
+    coef = np.polyfit(ns, ts, 2) if len(pts) >= 3 else np.array([ts[-1] / ns[-1] ** 2, 0.0, 0.0])
+    t1e6 = float(np.polyval(coef, 1e6))
+    return {"samples": [{"n": int(n), "seconds": t, "GB/s": 24.0 * n / t / 1e9} for n, t in pts],
+            "fit_seconds": {"a_n2": float(coef[0]), "b_n": float(coef[1]), "c": float(coef[2])},
+            "extrapolated_1e6_seconds": t1e6,
+            "value": 24.0 * 1e6 / t1e6 / 1e9, "unit": "GB/s",
+            "sample": "VectorStorage restatement (append + O(stored x queried) last-match scan), config 1's "
+                      "contiguous float keys at the sizes listed, 1 thread; value = the quadratic fit at 1e6 keys "
+                      "(a measured 1e6 run: profiles/r03_vector_storage_1e6.log)"}
 
 
 def _cpu_model():
@@ -287,9 +476,13 @@ def _zipf_cpu_sample(zb, B):
             "sample": f"{len(ks)} x {B} Zipf keys of the same workload, Add then Get"}
 
 
+# --------------------------------------------------------- side measurements
+
+
 def side_measurements(dev, B):
-    """Secondary numbers (same JSON line, under "extra"): cfg 3 Zipf through the
-    general path, and the end-to-end rate with host (pageable) buffers."""
+    """Secondary numbers (same JSON line, under "extra"): cfg 3 Zipf in
+    accumulate mode, cfg-2 windows in accumulate mode (Add only), and the
+    end-to-end rate from host buffers."""
     import torch
 
     import parameter_server_amd as ps
@@ -343,7 +536,8 @@ def side_measurements(dev, B):
         kt = {_lib.KERNEL_NAMES[k]: sh.kernel_time(k) for k in (_lib.PSKV_K_DENSE_CHECK, _lib.PSKV_K_ACC_DENSE)}
         sh.set_timing(False)
         sh.set_stream(None)
-    # accumulate Add bytes: n*(4+V) input + 2*u*V parameter read-modify-write
+    # accumulate Add bytes: n*(4+V) input (every value is summed) + 2*u*V
+    # parameter read-modify-write
     u_acc = len(set(int(b) for b in workload.dense_bases(J, space, B))) * B
     acc_b = J * B * (4 + V) + 2 * u_acc * V
     k_ms = {n: t["total_ms"] / max(1, t["launches"]) for n, t in kt.items()}
@@ -355,193 +549,66 @@ def side_measurements(dev, B):
         "k_acc_dense_GB/s": (J * B * V + 2 * u_acc * V) / (k_ms["k_acc_dense"] * 1e-3) / 1e9,
         "k_dense_check_GB/s": (J * B * 4) / (k_ms["k_dense_check"] * 1e-3) / 1e9}
     del db
-    # end-to-end: keys/vals start in pageable host memory (the zmq frames), outputs return to host
+    out.update(e2e_measurements(B, space))
+    return out
+
+
+def e2e_measurements(B, space):
+    """End to end: keys/vals start in host memory (the zmq frames), outputs
+    return to host.  Algorithmic GB/s as the device figure, and the PCIe bytes
+    per second the same calls moved (Add: keys + values H2D; Get: keys H2D,
+    values D2H)."""
+    import torch
+
+    import parameter_server_amd as ps
+    from parameter_server_amd import workload
+
+    out = {}
     rng = np.random.default_rng(0)
     J = 8
     hk = [np.arange(b, b + B, dtype=np.uint32) for b in workload.dense_bases(J, space, B)]
     hv = [rng.random(B, dtype=np.float32) for _ in hk]
     ho = [np.empty(B, np.float32) for _ in hk]
-    with ps.Shard(0, space, np.float32) as sh:
-        sh.add_grouped(list(zip(hk, hv)))
-        sh.get_grouped(list(zip(hk, ho)))
-        reps = 3
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            sh.add_grouped(list(zip(hk, hv)))
-            sh.get_grouped(list(zip(hk, ho)))
-        sh.sync()
-        dt = time.perf_counter() - t0
     last = {int(k[0]): j for j, k in enumerate(hk)}  # repeated windows: the later push wins
-    assert all(np.array_equal(o, hv[last[int(k[0])]]) for o, k in zip(ho, hk))
-    add_b, get_b = step_bytes(J * B, len(set(int(k[0]) for k in hk)) * B, J * B)
-    out["e2e_host_buffers"] = {"workload": "8 x 1M contiguous float keys from pageable host memory, Add then Get "
-                                           "(H2D + kernels + D2H, host sortedness check included)",
-                               "GB/s": (add_b + get_b) * reps / dt / 1e9}
-    # the same from page-locked buffers (zmq frames received into pinned memory,
-    # SURVEY §8f-3): direct DMA, no staging copy
+    u = len(last) * B
+    add_b, get_b = step_bytes(J * B, u, J * B)
+    pcie = J * B * (4 + V) + J * B * (4 + V)  # Add H2D keys+vals, Get H2D keys + D2H values
+
+    def measure(name, what, k, v, o, frame=False):
+        reps = 3
+        with ps.Shard(0, space, np.float32) as sh:
+            sh.add_grouped(list(zip(k, v)), frame=frame)
+            sh.get_grouped(list(zip(k, o)), frame=frame)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                sh.add_grouped(list(zip(k, v)), frame=frame)
+                sh.get_grouped(list(zip(k, o)), frame=frame)
+            sh.sync()
+            dt = time.perf_counter() - t0
+        assert all(np.array_equal(x, hv[last[int(kk[0])]]) for x, kk in zip(o, k))
+        out[name] = {"workload": what, "GB/s": (add_b + get_b) * reps / dt / 1e9,
+                     "pcie_GB/s": pcie * reps / dt / 1e9, "ms_per_step": dt / reps * 1e3}
+
+    measure("e2e_host_buffers", "8 x 1M contiguous float keys from pageable host memory, Add then Get "
+                                "(H2D + kernels + D2H, host sortedness check included)", hk, hv, ho)
+
     def pin(a):
         t = torch.from_numpy(a.view(np.int32) if a.dtype == np.uint32 else a).pin_memory()
         return t.numpy().view(a.dtype)
-    pk, pv, po = [pin(k) for k in hk], [pin(v) for v in hv], [pin(o) for o in ho]
-    with ps.Shard(0, space, np.float32) as sh:
-        sh.add_grouped(list(zip(pk, pv)))
-        sh.get_grouped(list(zip(pk, po)))
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            sh.add_grouped(list(zip(pk, pv)))
-            sh.get_grouped(list(zip(pk, po)))
-        sh.sync()
-        dt = time.perf_counter() - t0
-    assert all(np.array_equal(o, hv[last[int(k[0])]]) for o, k in zip(po, hk))
-    out["e2e_pinned_buffers"] = {"workload": "as e2e_host_buffers, from page-locked host memory (direct DMA)",
-                                 "GB/s": (add_b + get_b) * reps / dt / 1e9}
-    # the same from the library's frame pool under PSKV_HOST_FRAME (the buffers
-    # are borrowed: the Adds return once queued)
+
+    measure("e2e_pinned_buffers", "as e2e_host_buffers, from page-locked host memory (direct DMA)",
+            [pin(k) for k in hk], [pin(v) for v in hv], [pin(o) for o in ho])
     frames = [ps.HostFrame(B * 4) for _ in range(3 * J)]
     fk = [f.array(np.uint32, B) for f in frames[:J]]
     fv = [f.array(np.float32, B) for f in frames[J:2 * J]]
     fo = [f.array(np.float32, B) for f in frames[2 * J:]]
     for a, b in zip(fk + fv, hk + hv):
         a[:] = b
-    with ps.Shard(0, space, np.float32) as sh:
-        sh.add_grouped(list(zip(fk, fv)), frame=True)
-        sh.get_grouped(list(zip(fk, fo)), frame=True)
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            sh.add_grouped(list(zip(fk, fv)), frame=True)
-            sh.get_grouped(list(zip(fk, fo)), frame=True)
-        sh.sync()
-        dt = time.perf_counter() - t0
-    assert all(np.array_equal(o, hv[last[int(k[0])]]) for o, k in zip(fo, hk))
+    measure("e2e_frame_buffers", "as e2e_host_buffers, from pskv_host_alloc frames under PSKV_HOST_FRAME "
+                                 "(borrowed: Adds return once queued)", fk, fv, fo, frame=True)
     for f in frames:
         f.free()
-    out["e2e_frame_buffers"] = {"workload": "as e2e_host_buffers, from pskv_host_alloc frames under "
-                                            "PSKV_HOST_FRAME (borrowed: Adds return once queued)",
-                                "GB/s": (add_b + get_b) * reps / dt / 1e9}
     return out
-
-
-def dense_f64_step(batches, bases, J, B, dev, steps):
-    """The headline step with 8-byte values (the reference apps' Val = double,
-    app/logistic_regression.cpp): same keys and windows, f64 shard; bytes
-    counted with V = 8."""
-    import torch
-
-    import parameter_server_amd as ps
-
-    b64 = [(k, v.to(torch.float64)) for k, v in batches]
-    o64 = [torch.empty(B, dtype=torch.float64, device=dev) for _ in range(J)]
-    with ps.Shard(0, 100_000_000, np.float64) as sh:
-        sh.set_stream(torch.cuda.current_stream().cuda_stream)
-        adds = sh.prepare(b64)
-        gets = sh.prepare([(k, o) for (k, _), o in zip(b64, o64)], is_get=True)
-        for _ in range(2):
-            sh.add_grouped(adds, sorted_hint=True)
-            sh.get_grouped(gets)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            sh.add_grouped(adds, sorted_hint=True)
-            sh.get_grouped(gets)
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        last = {int(b): j for j, b in enumerate(bases)}
-        assert all(torch.equal(o64[j], b64[last[int(b)]][1]) for j, b in enumerate(bases))
-        sh.set_stream(None)
-    u = len(set(int(b) for b in bases)) * B
-    step_b = J * B * (4 + 8) + u * 8 + J * B * (4 + 2 * 8)
-    return {"workload": f"cfg 2 step with float64 values ({J} x {B} windows, assign)",
-            "GB/s": step_b * steps / dt / 1e9, "ms_per_step": dt / steps * 1e3}
-
-
-def dense_accumulate_step(plans, J, B, dev, steps):
-    """The headline step in ACCUMULATE mode (the north star's gradient push:
-    param[k] += v, then the pull of the updated parameters), over the same
-    rotating window sets: K6 density proof + K7 one read-modify-write per key
-    (sums in call order) + K1.  Bytes: Add n*(4+V) + 2*u*V (the RMW), Get
-    q*(4+2V).  A self-check compares one window with a float64 reference of
-    the sequential sums before timing."""
-    import torch
-
-    import parameter_server_amd as ps
-
-    R = len(plans)
-    outs = [torch.empty(B, dtype=torch.float32, device=dev) for _ in range(J)]
-    with ps.Shard(0, 100_000_000, np.float32, mode="accumulate") as sh:
-        sh.set_stream(torch.cuda.current_stream().cuda_stream)
-        prepared = [(sh.prepare(p[1]), sh.prepare([(k, o) for (k, _), o in zip(p[1], outs)], is_get=True))
-                    for p in plans]
-        # self-check on set 0, from a zeroed shard: window j's pulled values
-        # equal the sum of every push of that window in call order
-        sh.add_grouped(prepared[0][0], sorted_hint=True)
-        sh.get_grouped(prepared[0][1])
-        torch.cuda.synchronize()
-        bases0, batches0 = plans[0][0], plans[0][1]
-        b0 = int(bases0[0])
-        want = torch.zeros(B, dtype=torch.float32, device=dev)
-        for (k, v), b in zip(batches0, bases0):
-            if int(b) == b0:
-                want += v
-        assert torch.equal(outs[0], want), "accumulate self-check failed"
-        for i in range(2):
-            sh.add_grouped(prepared[i % R][0], sorted_hint=True)
-            sh.get_grouped(prepared[i % R][1])
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for i in range(steps):
-            sh.add_grouped(prepared[i % R][0], sorted_hint=True)
-            sh.get_grouped(prepared[i % R][1])
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        sh.set_stream(None)
-    tot = 0
-    for i in range(steps):
-        u = len(set(int(b) for b in plans[i % R][0])) * B
-        tot += J * B * (4 + V) + 2 * u * V + J * B * (4 + 2 * V)
-    return {"workload": f"cfg 2 step in accumulate mode (gradient push += then pull), {J} x {B} windows, "
-                        f"{R} rotating window sets (K6 + K7 + K1)",
-            "GB/s": tot / dt / 1e9, "ms_per_step": dt / steps * 1e3}
-
-
-def cold_get_step(shard, adds, bases, J, B, dev, steps):
-    """The headline step pulls the windows it just pushed: 48 distinct 4 MB
-    windows = 192 MB of parameters, which the Infinity Cache (256 MB) can still
-    hold when the Get reads them.  This variant pulls J windows that the step
-    did NOT push (seed 4242, pushed bases excluded), so K1's parameter reads
-    come from HBM: the cache-cold figure SURVEY §8d asks to keep apart."""
-    import torch
-
-    from parameter_server_amd import _lib, workload
-
-    pushed = set(int(b) for b in bases)
-    cand = [int(b) for b in workload.dense_bases(4 * J, 100_000_000, B, seed=4242) if int(b) not in pushed]
-    other = sorted(set(cand))[:J] if len(set(cand)) >= J else cand[:J]
-    pulls = [torch.arange(b, b + B, dtype=torch.int64, device=dev).to(torch.int32) for b in other]
-    outs = [torch.empty(B, dtype=torch.float32, device=dev) for _ in pulls]
-    gets = shard.prepare(list(zip(pulls, outs)), is_get=True)
-    for _ in range(2):
-        shard.add_grouped(adds, sorted_hint=True)
-        shard.get_grouped(gets)
-    torch.cuda.synchronize()
-    shard.reset_timing()
-    shard.set_timing(True, kernels=[_lib.PSKV_K_GATHER, _lib.PSKV_K_ASSIGN_TILES])
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        shard.add_grouped(adds, sorted_hint=True)
-        shard.get_grouped(gets)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    shard.set_timing(False)
-    g = shard.kernel_time(_lib.PSKV_K_GATHER)
-    a = shard.kernel_time(_lib.PSKV_K_ASSIGN_TILES)
-    u_push = len(pushed) * B
-    add_b, get_b = step_bytes(J * B, u_push, len(pulls) * B)
-    k1_ms = g["total_ms"] / max(1, g["launches"])
-    return {"workload": f"cfg 2 step with the Get pulling {len(pulls)} windows not pushed in the step "
-                        "(parameters read from HBM, not from the Infinity Cache)",
-            "GB/s": (add_b + get_b) * steps / dt / 1e9, "ms_per_step": dt / steps * 1e3,
-            "k_gather_ms": k1_ms, "k_gather_GB/s": get_b / (k1_ms * 1e-3) / 1e9,
-            "k_assign_group_ms": a["total_ms"] / max(1, a["launches"])}
 
 
 def zipf_sparse(rank, world, dev, lo, hi, B, steps, J=8):
@@ -590,7 +657,7 @@ def zipf_sparse(rank, world, dev, lo, hi, B, steps, J=8):
         torch.cuda.synchronize()
         t_own = time.perf_counter() - t0
         barrier(world)
-        elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
+        elapsed = max_over_ranks(t_own, world, dev)
         sh.set_timing(True, kernels=[_lib.PSKV_K_RADIX, _lib.PSKV_K_GATHER])
         for _ in range(steps):
             sh.add_grouped(adds)
@@ -625,44 +692,58 @@ def zipf_sparse(rank, world, dev, lo, hi, B, steps, J=8):
         "bytes_per_step_per_gpu": add_b + get_b}, zb
 
 
-def fixed_set_step(shard, adds, gets, bases, J, B, steps):
-    """The round-1 headline form: the SAME window set every step.  The 48
-    distinct windows (192 MB of parameters) then stay largely resident in the
-    256 MB Infinity Cache from one step to the next, so this is the cache-warm
-    figure, reported apart from the rotating-set `value`."""
+def variant_f64(rank, world, J, B, dev, R, steps, lo, hi):
+    """The headline step with 8-byte values (the reference apps' Val = double,
+    app/logistic_regression.cpp): same windows, f64 shard, V = 8 bytes."""
     import torch
 
-    from parameter_server_amd import _lib
+    import parameter_server_amd as ps
 
-    for _ in range(2):
-        shard.add_grouped(adds, sorted_hint=True)
-        shard.get_grouped(gets)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        shard.add_grouped(adds, sorted_hint=True)
-        shard.get_grouped(gets)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    shard.reset_timing()
-    shard.set_timing(True, kernels=[_lib.PSKV_K_GATHER, _lib.PSKV_K_ASSIGN_TILES])
-    for _ in range(steps):
-        shard.add_grouped(adds, sorted_hint=True)
-        shard.get_grouped(gets)
-    torch.cuda.synchronize()
-    shard.set_timing(False)
-    g = shard.kernel_time(_lib.PSKV_K_GATHER)
-    a = shard.kernel_time(_lib.PSKV_K_ASSIGN_TILES)
-    add_b, get_b = step_bytes(J * B, len(set(int(b) for b in bases)) * B, J * B)
-    return {"workload": f"cfg 2 step over ONE window set ({J} x {B}, seed 42) every step: cache-warm "
-                        "(the step's parameters stay in the Infinity Cache between steps)",
-            "GB/s": (add_b + get_b) * steps / dt / 1e9, "ms_per_step": dt / steps * 1e3,
-            "k_gather_ms": g["total_ms"] / max(1, g["launches"]),
-            "k_assign_group_ms": a["total_ms"] / max(1, a["launches"])}
+    sets = [make_set(rank, world, J, B, dev, r, dtype=torch.float64) for r in range(R)]
+    with ps.Shard(lo, hi, np.float64, device=dev.index) as sh:
+        sh.set_stream(torch.cuda.current_stream().cuda_stream)
+        f = Form(sh, sets, 1, dev, vb=8)
+        f.self_check(lo, hi, dev)
+        res = run_form(f, steps, 2, world, dev)
+        sh.set_stream(None)
+    return {"workload": f"the headline step with float64 values ({J} x {B} windows, pull of the next set, assign)",
+            "GB/s": res["GB/s"], "ms_per_step": res["ms_per_step"]}
 
 
-def main():
-    args = parse()
+def variant_accumulate(rank, world, J, B, dev, sets, steps, lo, hi):
+    """The headline step in ACCUMULATE mode (the north star's gradient push:
+    param[k] += v, then the pull): K6 density proof + K7 one read-modify-write
+    per key (sums in call order) + K1.  Bytes: Add n*(4+V) + 2*u*V (every value
+    is summed, and the RMW), Get q*(4+2V).  A self-check compares one rotation
+    with a torch model of the sequential sums first."""
+    import torch
+
+    import parameter_server_amd as ps
+
+    with ps.Shard(lo, hi, np.float32, mode="accumulate", device=dev.index) as sh:
+        sh.set_stream(torch.cuda.current_stream().cuda_stream)
+        f = Form(sh, sets, 1, dev)
+        # accumulate bytes: every pushed value is read
+        f.add_b = [sum(n for _, _, n in s["slices"]) * (4 + V) + 2 * s["u"] * V for s in sets]
+        ref = torch.zeros(hi - lo, dtype=torch.float32, device=dev)
+        for i in range(f.R):
+            for (_, first, n), (_, v) in zip(sets[i]["slices"], sets[i]["batches"]):
+                ref[first - lo:first - lo + n] += v
+            f.step(i)
+            torch.cuda.synchronize()
+            t = f.pull_of(i)
+            for (_, first, n), o in zip(sets[t]["slices"], f.outs[t]):
+                assert torch.equal(o, ref[first - lo:first - lo + n]), "accumulate self-check failed"
+        del ref
+        res = run_form(f, steps, 2, world, dev)
+        sh.set_stream(None)
+    return {"workload": f"the headline step in accumulate mode (gradient push += then pull of the next set), "
+                        f"{J} x {B} windows (K6 + K7 + K1)",
+            "GB/s": res["GB/s"], "ms_per_step": res["ms_per_step"]}
+
+
+def main(argv=None):
+    args = parse(argv)
     # the JSON line is the only thing on stdout: everything else the run prints
     # (torch.distributed / gloo / RCCL banners, library notices) goes to stderr
     sys.stdout.flush()
@@ -671,163 +752,137 @@ def main():
     import torch
 
     import parameter_server_amd as ps
-    from parameter_server_amd import _lib, workload
+    from parameter_server_amd import workload
 
     rank, world, local = dist_init(args)
     dev = torch.device(f"cuda:{local}")
-    J, B, R = args.batches, args.batch_keys, max(1, args.sets)
-    sets = [make_workload(rank, world, J, B, dev, r) for r in range(R)]
-    key_space, lo, hi = sets[0][:3]
-    outs = [torch.empty(B, dtype=torch.float32, device=dev) for _ in range(J)]  # shared by the sets
+    J, B, R = args.batches, args.batch_keys, max(2, args.sets)
+    # planning rank / world: the process's own, or (probe knob, one process,
+    # never used by the driver) PSKV_BENCH_EMULATE="r/N" = rank r's share of
+    # the N-GPU cfg-4 workload alone on this GPU
+    prank, pworld = rank, world
+    if os.environ.get("PSKV_BENCH_EMULATE") and world == 1:
+        prank, pworld = (int(x) for x in os.environ["PSKV_BENCH_EMULATE"].split("/"))
+    sets = [make_set(prank, pworld, J, B, dev, r) for r in range(R)]
+    key_space, lo, hi = plan_rank(prank, pworld, J, B)[:3]
     stream = torch.cuda.current_stream()
     shard = ps.Shard(lo, hi, np.float32, device=local)
     shard.set_stream(stream.cuda_stream)  # torch events and the kernels share one stream
-    plans = []  # per set: (bases, batches, prepared adds, prepared gets, step bytes)
-    for _, _, _, bases_r, batches_r in sets:
-        u_r = len(set(int(b) for b in bases_r)) * B  # distinct keys pushed by the set
-        plans.append((bases_r, batches_r, shard.prepare(batches_r),
-                      shard.prepare([(k, o) for (k, _), o in zip(batches_r, outs)], is_get=True),
-                      sum(step_bytes(J * B, u_r, J * B)), u_r))
-    bases, batches, adds, gets = plans[0][:4]
+    form = Form(shard, sets, 1, dev)
+    # correctness guard on the benchmarked state: one rotation from a cleared
+    # shard, every pull against a model of the shard
+    form.self_check(lo, hi, dev)
+    head = run_form(form, args.steps, max(args.warmup, R), world, dev)
+    ktimes, evented_s = evented(form, args.steps, world, dev)
+    touched = min(form.touched(i) for i in range(R))
+    a_b, g_b = form.bytes(args.steps)
+    own_bytes = a_b + g_b
+    n_push = sum(n for s in sets for _, _, n in s["slices"]) / R  # keys this rank receives per step
+    per_gpu = {"mean_GB/s": head["GB/s"] / world,
+               "min_GB/s": -max_over_ranks(-head["own_GB/s"], world, dev),
+               "max_GB/s": max_over_ranks(head["own_GB/s"], world, dev),
+               "min_keys_pushed_per_step": -max_over_ranks(-n_push, world, dev),
+               "max_keys_pushed_per_step": max_over_ranks(n_push, world, dev)}
 
-    def step(i):
-        p = plans[i % R]
-        shard.add_grouped(p[2], sorted_hint=True)
-        shard.get_grouped(p[3])
-
-    def bytes_of(k):  # algorithmic bytes of steps 0..k-1
-        return sum(plans[i % R][4] for i in range(k))
-
-    for i in range(max(args.warmup, R)):
-        step(i)
-    torch.cuda.synchronize()
-    # correctness guard on the benchmarked state: every pull returns the last
-    # push of its window, for every window set
-    for r, (bases_r, batches_r, *_rest) in enumerate(plans):
-        step(r)
-        torch.cuda.synchronize()
-        last = {int(b): j for j, b in enumerate(bases_r)}
-        for j, b in enumerate(bases_r):
-            assert torch.equal(outs[j], batches_r[last[int(b)]][1]), "bench self-check failed"
-
-    # timed region: exactly K steps, barrier + synchronize on both sides, no
-    # instrumentation inside (each HIP event record on the stream costs ~4.6 us
-    # of dispatch gap: 4 per step inflated the step by 9.5 us, 4 %)
-    barrier(world)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
-    torch.cuda.synchronize()
-    t_own = time.perf_counter()  # this rank's own work done
-    barrier(world)
-    t1 = time.perf_counter()
-    elapsed = max_over_ranks(t1 - t0, world, dev)
-
-    # roofline pass: the same K steps again, live, with HIP events bracketing
-    # the two streaming kernels on their launch stream -> per-launch durations
-    shard.reset_timing()
-    shard.set_timing(True, kernels=[_lib.PSKV_K_GATHER, _lib.PSKV_K_ASSIGN_TILES])
-    torch.cuda.synchronize()
-    t2 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
-    torch.cuda.synchronize()
-    t3 = time.perf_counter()
-    shard.set_timing(False)
-    evented = max_over_ranks(t3 - t2, world, dev)
-
-    ktimes = {}
-    for k, name in _lib.KERNEL_NAMES.items():
-        t = shard.kernel_time(k)
-        if t["launches"]:
-            ktimes[name] = {"launches": t["launches"], "avg_ms": t["total_ms"] / t["launches"],
-                            "keys_per_launch": t["elements"] / t["launches"]}
-    shard.sync()
     zipf_res = None
     if not args.no_zipf:
-        zipf_res, zb = zipf_sparse(rank, world, dev, lo, hi, B, args.steps)
-    # per-step bytes, averaged over the rotation as the steps ran it
-    u_push = sum(plans[i % R][5] for i in range(args.steps)) / args.steps  # distinct keys pushed per step
-    add_b, get_b = step_bytes(J * B, u_push, J * B)
-    own_bytes = float(bytes_of(args.steps))
-    total_bytes = sum_over_ranks(own_bytes, world, dev)
-    value = total_bytes / elapsed / 1e9
-    own = own_bytes / (t_own - t0) / 1e9
-    per_gpu = {"mean_GB/s": value / world, "min_GB/s": -max_over_ranks(-own, world, dev),
-               "max_GB/s": max_over_ranks(own, world, dev)}
+        zipf_res, zb = zipf_sparse(prank, world, dev, lo, hi, B, args.steps)
 
-    # dominant kernel: the one with the most time in the timed region
+    # dominant kernel: the one with the most time in the evented pass
     dom = max(ktimes.items(), key=lambda kv: kv[1]["avg_ms"] * kv[1]["launches"])
-    launch_bytes = get_b if dom[0] == "k_gather" else add_b  # one launch = one step's Add or Get
-    achieved = launch_bytes / (dom[1]["avg_ms"] / 1e3) / 1e9
-    traffic, traffic_src = load_pmc(dom[0], {"n_gpus": world, "batches": J, "batch_keys": B, "sets": R})
-    for name, kt in ktimes.items():
-        kt["algorithmic_bytes"] = get_b if name == "k_gather" else add_b
-        kt["GB/s"] = kt["algorithmic_bytes"] / (kt["avg_ms"] / 1e3) / 1e9
+    achieved = dom[1]["GB/s"]
+    cfg_key = {"n_gpus": world, "batches": J, "batch_keys": B, "sets": R, "form": "pull-next-set"}
+    traffic, traffic_src = load_pmc(dom[0], cfg_key)
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": dom[0],
-            "algorithmic_bytes_per_launch": launch_bytes,
-            "bytes_per_unit": "Add n*(4+V)+u*V, Get q*(4+2V); V=4, u=distinct pushed keys",
+            "algorithmic_bytes_per_launch": dom[1]["algorithmic_bytes"],
+            "bytes_per_unit": "Add n*4 + 2*u*V (keys, last values, parameter writes), Get q*(4+2V); V=4, "
+                              "u = distinct pushed keys",
             "timing": "HIP events on the launch stream around each launch of the two streaming "
                       "kernels, over a second pass of the same K steps run right after the "
                       "event-free timed region",
-            "ms_per_step_evented": evented / args.steps * 1e3,
+            "ms_per_step_evented": evented_s / args.steps * 1e3,
             "kernels": ktimes}
     if traffic_src:
         roof["traffic_source"] = traffic_src
+        roof["traffic_over_algorithmic"] = traffic / dom[1]["algorithmic_bytes"]
 
     result = {
         "metric": METRIC,
-        "value": value,
+        "value": head["GB/s"],
         "unit": "GB/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step": head["ms_per_step"],
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic",
         "config": {
-            "workload": ("cfg 2 dense: 1e8-key float shard" if world == 1 else
-                         f"cfg 4 ranges: 1e9 keys over {world} range shards") +
-                        f", {J} x {B} contiguous-key push batches then the same pulls per step per GPU, "
-                        f"assign (last-write-wins) mode, grouped launches, {R} window sets rotated over the steps",
+            "workload": (f"cfg 2 dense: 1e8-key float shard, {J} x {B} contiguous-key windows at 1M-aligned bases "
+                         if pworld == 1 else
+                         f"cfg 4 ranges: 1e9 keys over {pworld} range shards, {J} producer streams each pushing one "
+                         f"{B}-key contiguous window at a uniformly random base, sliced by the range map ") +
+                        "pushed, then the windows of the next set pulled, per step; assign (last-write-wins) mode, "
+                        f"grouped launches, {R} window sets rotated over the steps",
             "key_space": key_space,
             "shard_keys_per_gpu": hi - lo,
-            "batches_per_step_per_gpu": J,
+            "windows_per_step": J,
             "batch_keys": B,
             "window_sets": R,
-            "window_set_seeds": [workload.set_seed(r, world) for r in range(R)],
-            "bytes_per_step_per_gpu": add_b + get_b,
-            "distinct_pushed_keys_per_step": u_push,
-            "parallelism": f"range-sharded x{world} (no collective)",
+            "window_set_seeds": [workload.set_seed(r, pworld) for r in range(R)],
+            "keys_pushed_per_step_per_gpu": n_push,
+            "distinct_pushed_keys_per_step_per_gpu": sum(s["u"] for s in sets) / R,
+            "bytes_per_step_per_gpu": own_bytes / args.steps,
+            "param_bytes_touched_per_step_per_gpu": touched,
+            "parallelism": f"range-sharded x{pworld} (no collective)",
         },
         "roofline": roof,
         # cfg 4 reports per-GPU next to aggregate: each rank's own
         # bytes over its own time, min / max over ranks
         "per_gpu": per_gpu,
     }
+    if (prank, pworld) != (rank, world):
+        result["config"]["emulated_rank"] = f"{prank}/{pworld} (probe: one rank's share alone on one GPU)"
     if zipf_res is not None:
         result["zipf_sparse"] = zipf_res
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(bases, B, args.cpu_batches)
+    extra = {}
+    if not args.no_extra:
+        warm = Form(shard, sets, 0, dev)
+        w = run_form(warm, args.steps, 2, world, dev)
+        extra["cache_warm_step"] = {
+            "workload": "the round-2 headline form: the Get pulls the windows the step just pushed (their "
+                        "parameters are still in the 256 MB Infinity Cache)", "GB/s": w["GB/s"],
+            "ms_per_step": w["ms_per_step"]}
+        del warm
+        if pworld > 1:
+            wsets = [make_set(prank, pworld, J, B, dev, r, weak=True) for r in range(R)]
+            wf = Form(shard, wsets, 1, dev)
+            wf.self_check(lo, hi, dev)
+            wr = run_form(wf, args.steps, 2, world, dev)
+            extra["weak_scaled"] = {
+                "workload": f"weak scaling: every rank's own {J} producers push 1M-aligned windows inside its "
+                            "range (per-GPU work fixed), pull of the next set", "GB/s": wr["GB/s"],
+                "ms_per_step": wr["ms_per_step"],
+                "per_gpu_min_GB/s": -max_over_ranks(-wr["own_GB/s"], world, dev)}
+            del wf, wsets
+    shard.set_stream(None)
+    shard.close()
+    if rank == 0 and pworld == 1 and not args.no_cpu_baseline:
+        sizes = [int(x) for x in args.vector_sizes.split(",") if x]
+        result["cpu_baseline"] = cpu_baseline([f for _, f, _ in sets[0]["slices"]], B, args.cpu_batches, sizes)
         if zipf_res is not None:  # cfg 3's own CPU baseline: the same Zipf batches
             result["cpu_baseline"]["zipf"] = _zipf_cpu_sample(zb[:2], B)
     if zipf_res is not None:
         del zb
-    if rank == 0 and world == 1 and not args.no_extra:
-        cold = cold_get_step(shard, adds, bases, J, B, dev, args.steps)
-        fixed = fixed_set_step(shard, adds, gets, bases, J, B, args.steps)
-        shard.set_stream(None)
-        result["extra"] = side_measurements(dev, B)
-        result["extra"]["cold_get_step"] = cold
-        result["extra"]["fixed_set_step"] = fixed
-        result["extra"]["dense_f64_step"] = dense_f64_step(batches, bases, J, B, dev, args.steps)
-        result["extra"]["dense_accumulate_step"] = dense_accumulate_step(plans, J, B, dev, args.steps)
-    shard.close()
+    if pworld == 1 and not args.no_extra:
+        extra["dense_f64_step"] = variant_f64(rank, world, J, B, dev, R, args.steps, lo, hi)
+        extra["dense_accumulate_step"] = variant_accumulate(rank, world, J, B, dev, sets, args.steps, lo, hi)
+        extra.update(side_measurements(dev, B))
+    if extra:
+        result["extra"] = extra
     if rank == 0:
         json_out.write(json.dumps(result) + "\n")
         json_out.flush()

@@ -79,8 +79,9 @@ struct SrvRing {  // the kernel polls {req_seq, stop} as one 8-byte word
   uint32_t stop;       // host: 1 = leave the loop
   uint32_t pad0[30];
   uint32_t done_seq;   // device: number of the last request applied
-  uint32_t alive;      // device: 0 once the kernel has left its loop
-  uint32_t pad1[30];
+  uint32_t alive;      // host sets 1 at launch; device: 0 once the kernel has left its loop
+  uint32_t started;    // device: the launch generation now running (stored on entry)
+  uint32_t pad1[29];
   SrvSlot slot[kSrvSlots];
 };
 static_assert(sizeof(SrvSlot) % 8 == 0 && offsetof(SrvRing, slot) % 8 == 0, "8-byte words in the ring");
@@ -154,11 +155,12 @@ hipError_t launch_inline_add(int dtype, int mode, const InlineAdd& a, const Dens
 hipError_t launch_inline_get(int vb, const InlineGet& a, const DenseView& d, const Ovf& o,
                              void* out, unsigned int* done, unsigned int seq, hipStream_t st);
 // K9: start the request server on `st` (one workgroup; requests start_seq+1..
-// are applied as they are posted).  It leaves its loop when ring->stop is set or
-// after idle_ticks wall-clock ticks without a request, and then clears alive.
+// are applied as they are posted).  It stores `gen` in ring->started on entry,
+// leaves its loop when ring->stop is set or after idle_ticks wall-clock ticks
+// without a request, and then clears alive.
 hipError_t launch_serve(int dtype, int mode, SrvRing* ring, const DenseView& d, const Ovf& o,
                         void* reply, uint32_t start_seq, unsigned long long idle_ticks,
-                        hipStream_t st);
+                        uint32_t gen, hipStream_t st);
 size_t rb_entry_bytes(int vb);
 // K6: tag `flag` with `epoch` unless every batch is a dense in-range window
 // (chunk = kBlock * 4 * 8 keys per workgroup).

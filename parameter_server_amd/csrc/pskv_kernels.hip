@@ -1860,7 +1860,7 @@ __device__ __forceinline__ T sys_load(const T* p) {
 template <typename VT, int MODE>
 __global__ __launch_bounds__(kInlineMax) void k_serve(SrvRing* ring, DenseView d, Ovf o,
                                                       void* reply, uint32_t start,
-                                                      unsigned long long idle_ticks) {
+                                                      unsigned long long idle_ticks, uint32_t gen) {
   using BT = typename std::conditional<sizeof(VT) == 8, unsigned long long, uint32_t>::type;
   __shared__ __attribute__((aligned(16))) uint32_t s_keys[kInlineGetMax];
   __shared__ __attribute__((aligned(16))) unsigned long long s_vals[kInlineMax];
@@ -1872,6 +1872,9 @@ __global__ __launch_bounds__(kInlineMax) void k_serve(SrvRing* ring, DenseView d
   const int tid = threadIdx.x;
   uint32_t next = start + 1;
   unsigned long long t_idle = wall_clock64();
+  // tell the host this launch is running (a launch queued behind other work on
+  // its hardware queue has not started: the host's wait for it is bounded)
+  if (tid == 0) __hip_atomic_store(&ring->started, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   for (;;) {
     if (tid == 0) {
       // {req_seq, stop} in one 8-byte load: one PCIe round trip per poll
@@ -1882,6 +1885,10 @@ __global__ __launch_bounds__(kInlineMax) void k_serve(SrvRing* ring, DenseView d
         const int32_t ahead = (int32_t)((uint32_t)w - next);
         if (ahead >= 0) {
           avail = ahead + 1 < kSrvBatch ? (uint32_t)ahead + 1u : (uint32_t)kSrvBatch;
+          // pairs with the host's release store of req_seq: the slots it
+          // published are read after this (system scope; the other lanes after
+          // the barrier below)
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
           break;
         }
         if ((uint32_t)(w >> 32) != 0u || wall_clock64() - t_idle > idle_ticks) {
@@ -2261,18 +2268,18 @@ hipError_t launch_inline_add(int dtype, int mode, const InlineAdd& a, const Dens
 
 hipError_t launch_serve(int dtype, int mode, SrvRing* ring, const DenseView& d, const Ovf& o,
                         void* reply, uint32_t start_seq, unsigned long long idle_ticks,
-                        hipStream_t st) {
+                        uint32_t gen, hipStream_t st) {
   if (mode == 0) {
     if (dtype == 2)
-      k_serve<double, 0><<<1, kInlineMax, 0, st>>>(ring, d, o, reply, start_seq, idle_ticks);
+      k_serve<double, 0><<<1, kInlineMax, 0, st>>>(ring, d, o, reply, start_seq, idle_ticks, gen);
     else
-      k_serve<float, 0><<<1, kInlineMax, 0, st>>>(ring, d, o, reply, start_seq, idle_ticks);
+      k_serve<float, 0><<<1, kInlineMax, 0, st>>>(ring, d, o, reply, start_seq, idle_ticks, gen);
   } else if (dtype == 0) {
-    k_serve<int, 1><<<1, kInlineMax, 0, st>>>(ring, d, o, reply, start_seq, idle_ticks);
+    k_serve<int, 1><<<1, kInlineMax, 0, st>>>(ring, d, o, reply, start_seq, idle_ticks, gen);
   } else if (dtype == 1) {
-    k_serve<float, 1><<<1, kInlineMax, 0, st>>>(ring, d, o, reply, start_seq, idle_ticks);
+    k_serve<float, 1><<<1, kInlineMax, 0, st>>>(ring, d, o, reply, start_seq, idle_ticks, gen);
   } else {
-    k_serve<double, 1><<<1, kInlineMax, 0, st>>>(ring, d, o, reply, start_seq, idle_ticks);
+    k_serve<double, 1><<<1, kInlineMax, 0, st>>>(ring, d, o, reply, start_seq, idle_ticks, gen);
   }
   return hipGetLastError();
 }

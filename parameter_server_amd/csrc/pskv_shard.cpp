@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -299,6 +300,7 @@ struct pskv_shard {
   bool tune_serve = false;
   uint32_t tune_serve_idle_us = 20000;
   SrvRing* srv = nullptr;
+  uint32_t srv_gen = 0;  // launch generation (the kernel stores it in ring->started on entry)
   hipStream_t srv_stream = nullptr;
   hipEvent_t srv_dep = nullptr;  // the shard's stream up to the server's launch
   bool srv_running = false;
@@ -379,20 +381,28 @@ int drain_timing(pskv_shard* s) {
 
 // A resident server holds the hardware queue its stream maps to: work of any
 // other stream on that queue waits behind it until it idles out.  The process
-// has GPU_MAX_HW_QUEUES queues per device (HIP's default 4) and each served
-// shard uses two streams, so the server engages only while a device has at
-// most that many / 2 shards; beyond that the K8 launches serve instead.
+// has GPU_MAX_HW_QUEUES queues per device (HIP's default 4); HIP deals streams
+// to them round-robin.  Every shard on the device holds a stream and a served
+// one a second (the server's), and the null stream takes one more, so the
+// server engages only while 2 * shards + 1 streams fit the queues (one shard
+// at the default 4) — it then holds a queue of its own, provided the process
+// creates no further streams on the device (torch's default stream is the null
+// stream).  Beyond that the K8 launches serve.  A launch that is nevertheless
+// queued behind other work does not hang its caller: srv_wait bounds the wait
+// for it to start (kSrvStartTimeoutMs) and fails the call.
 std::atomic<int> g_device_shards[64];
 
 bool serve_on(const pskv_shard* s) {
   if (!s->tune_serve || s->device < 0 || s->device >= 64) return false;
-  static const int limit = [] {
+  static const int queues = [] {
     const char* e = std::getenv("GPU_MAX_HW_QUEUES");
     const int q = e ? std::atoi(e) : 4;
-    return std::max(1, (q > 0 ? q : 4) / 2);
+    return q > 0 ? q : 4;
   }();
-  return g_device_shards[s->device].load(std::memory_order_relaxed) <= limit;
+  return 2 * g_device_shards[s->device].load(std::memory_order_relaxed) + 1 <= queues;
 }
+
+constexpr int kSrvStartTimeoutMs = 2000;
 
 int ensure_ireply(pskv_shard* s, size_t cap) {
   if (s->ireply) return PSKV_OK;
@@ -404,6 +414,10 @@ int ensure_ireply(pskv_shard* s, size_t cap) {
     s->ireply = nullptr;
     return fail(PSKV_ENOMEM, "inline reply buffer allocation failed");
   }
+  // the sequence word the host polls (ireply_seq counts from 1): page-locked
+  // memory may come back holding a former owner's bytes, so clear it
+  std::memset(static_cast<char*>(s->ireply) + cap, 0, 128);
+  s->ireply_seq = 0;
   return PSKV_OK;
 }
 
@@ -412,10 +426,11 @@ int srv_launch(pskv_shard* s) {
   const uint32_t start = __atomic_load_n(&r->done_seq, __ATOMIC_ACQUIRE);
   __atomic_store_n(&r->stop, 0u, __ATOMIC_RELAXED);
   __atomic_store_n(&r->alive, 1u, __ATOMIC_RELEASE);
+  ++s->srv_gen;
   PSKV_HIP(hipEventRecord(s->srv_dep, s->stream));
   PSKV_HIP(hipStreamWaitEvent(s->srv_stream, s->srv_dep, 0));
   PSKV_HIP(launch_serve(s->dtype, s->mode, r, s->dview(), s->ovf, s->ireply, start, s->srv_idle_ticks,
-                        s->srv_stream));
+                        s->srv_gen, s->srv_stream));
   s->srv_running = true;
   return PSKV_OK;
 }
@@ -430,6 +445,7 @@ int srv_reap(pskv_shard* s) {
 // Wait until request `seq` has been applied.
 int srv_wait(pskv_shard* s, uint32_t seq) {
   SrvRing* r = s->srv;
+  auto t_start = std::chrono::steady_clock::now();  // since the current launch was seen queued
   for (uint32_t it = 1;; ++it) {
     if ((int32_t)(__atomic_load_n(&r->done_seq, __ATOMIC_ACQUIRE) - seq) >= 0) return PSKV_OK;
     if ((it & 255u) == 0 && __atomic_load_n(&r->alive, __ATOMIC_ACQUIRE) == 0u) {
@@ -437,10 +453,18 @@ int srv_wait(pskv_shard* s, uint32_t seq) {
       if (int rc = srv_reap(s)) return rc;
       if ((int32_t)(__atomic_load_n(&r->done_seq, __ATOMIC_ACQUIRE) - seq) >= 0) return PSKV_OK;
       if (int rc = srv_launch(s)) return rc;
+      t_start = std::chrono::steady_clock::now();
     }
     if ((it & 65535u) == 0) {  // a faulted kernel never publishes: surface the error
       const hipError_t e = hipStreamQuery(s->srv_stream);
       if (e != hipSuccess && e != hipErrorNotReady) PSKV_HIP(e);
+      // a launch that has not started is queued behind other work on its
+      // hardware queue: fail the call rather than wait without bound
+      if (__atomic_load_n(&r->started, __ATOMIC_ACQUIRE) != s->srv_gen &&
+          std::chrono::steady_clock::now() - t_start > std::chrono::milliseconds(kSrvStartTimeoutMs))
+        return fail(PSKV_ESTATE,
+                    "request server did not start within 2 s: its hardware queue is held by other work "
+                    "(more streams on the device than GPU_MAX_HW_QUEUES); run without PSKV_SERVE");
     }
   }
 }
@@ -953,14 +977,33 @@ bool is_pinned(const void* p, void** dev = nullptr) {
   return a.type == hipMemoryTypeHost && (!dev || a.devicePointer);
 }
 
+// Device view of [p, p + bytes) when the whole range lies in ONE page-locked
+// allocation (hipHostMalloc'd or registered), else null: a kernel reads and
+// writes through the view, so a range that runs past its registration (a
+// sub-range registration, a slice across two) must take the DMA path instead.
+void* pinned_range_view(const void* p, size_t bytes) {
+  void* dev = nullptr;
+  if (!is_pinned(p, &dev)) return nullptr;
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  if (hipMemGetAddressRange(&base, &size, reinterpret_cast<hipDeviceptr_t>(dev)) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  const uintptr_t b = reinterpret_cast<uintptr_t>(base), d = reinterpret_cast<uintptr_t>(dev);
+  if (d < b || d + bytes > b + size) return nullptr;
+  return dev;
+}
+
 // Device views of page-locked host batches (frames or any other pinned
 // memory), or false.
-bool pinned_views(const std::vector<pskv_batch>& in, std::vector<pskv_batch>* out) {
+bool pinned_views(const std::vector<pskv_batch>& in, size_t vb, std::vector<pskv_batch>* out) {
   out->clear();
   for (const auto& b : in) {
     pskv_batch d = b;
-    void *k = nullptr, *v = nullptr;
-    if (!is_pinned(b.keys, &k) || !is_pinned(b.vals, &v)) return false;
+    void* k = pinned_range_view(b.keys, b.n * 4);
+    void* v = pinned_range_view(b.vals, b.n * vb);
+    if (!k || !v) return false;
     d.keys = static_cast<const uint32_t*>(k);
     d.vals = v;
     out->push_back(d);
@@ -978,10 +1021,6 @@ int stage_host_batches(pskv_shard* s, const std::vector<pskv_batch>& in,
   for (auto& b : in) bytes += round16(b.n * 4) + round16(b.n * (size_t)s->vb);
   bool locked = true;
   for (const auto& b : in) locked = locked && is_pinned(b.keys) && is_pinned(b.vals);
-  // pageable buffers: DMA'd directly only when large (the runtime's pageable
-  // copy has a high fixed cost and blocks until done); smaller ones are copied
-  // into pinned staging and DMA'd asynchronously (the call returns after the
-  // host copy)
   // page-locked buffers: DMA'd directly from tune_dma_min_bytes_pinned on
   // (below it the copy, which returns before the DMA, is ahead); pageable
   // buffers only when large (the runtime's pageable copy has a high fixed cost
@@ -1308,57 +1347,73 @@ int add_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
   if (rc) return rc;
   bool host_verified = false, host_dense = false;
   std::vector<pskv_batch> framed;  // the host batches, when they are borrowed frames
-  if (!device) {
-    std::vector<pskv_batch> staged, views;
-    uint64_t outside = 0;
-    if ((flags & PSKV_HOST_FRAME) && frame_views(v, (size_t)s->vb, &views)) {
-      framed = v;
-      rc = frame_batches(s, v, views, &staged, &host_verified, &outside, &host_dense);
-    } else {
-      rc = stage_host_batches(s, v, &staged, &host_verified, &outside, &host_dense);
-    }
-    if (rc) return rc;
-    if (outside) {
-      // exact bound on new overflow keys: grow before the kernels can fill the table
-      if (2 * (s->ocount_known + outside) > s->ocap) {
-        uint32_t cnt, err;
-        rc = read_overflow_stat(s, &cnt, &err);
-        if (rc) return rc;
-        rc = grow_overflow(s, cnt + outside);
-        if (rc) return rc;
-      }
-      s->ocount_known += outside;
-    }
-    v.swap(staged);
-  }
-  bool vec = true;
-  for (auto& b : v) vec &= aligned16(b.keys) & aligned16(b.vals);
-  for (auto& g : split_groups(v)) {
-    const uint32_t epoch = next_epoch(s);
-    if (s->mode == PSKV_ACCUMULATE) {
-      if (!device && host_dense) {
-        // the CPU proved every batch a dense in-range window while staging it
-        rc = dense_accumulate(s, v, g.first, g.second, epoch, /*verify=*/false);
-      } else if (device && (flags & PSKV_SORTED_HINT)) {
-        rc = dense_accumulate(s, v, g.first, g.second, epoch, /*verify=*/true);
+  // Every exit records the frames' queued uses (pskv_host_free holds a frame
+  // until they have run): a failure after some work was queued must not let
+  // the frame be reused while that work still reads it.
+  auto run = [&]() -> int {
+    int rc = PSKV_OK;
+    if (!device) {
+      std::vector<pskv_batch> staged, views;
+      uint64_t outside = 0;
+      if ((flags & PSKV_HOST_FRAME) && frame_views(v, (size_t)s->vb, &views)) {
+        framed = v;
+        rc = frame_batches(s, v, views, &staged, &host_verified, &outside, &host_dense);
       } else {
-        // K5 (no global atomics) measured faster than K4a (LDS sums + one
-        // atomic add per distinct key per chunk) on cfg 3: 322 vs 380 us per
-        // 8M Zipf keys; PSKV_GENERAL=stamps selects K4a
+        rc = stage_host_batches(s, v, &staged, &host_verified, &outside, &host_dense);
+      }
+      if (rc) return rc;
+      if (outside) {
+        // exact bound on new overflow keys: grow before the kernels can fill the table
+        if (2 * (s->ocount_known + outside) > s->ocap) {
+          uint32_t cnt, err;
+          rc = read_overflow_stat(s, &cnt, &err);
+          if (rc) return rc;
+          rc = grow_overflow(s, cnt + outside);
+          if (rc) return rc;
+        }
+        s->ocount_known += outside;
+      }
+      v.swap(staged);
+    }
+    bool vec = true;
+    for (auto& b : v) vec &= aligned16(b.keys) & aligned16(b.vals);
+    for (auto& g : split_groups(v)) {
+      const uint32_t epoch = next_epoch(s);
+      if (s->mode == PSKV_ACCUMULATE) {
+        if (!device && host_dense) {
+          // the CPU proved every batch a dense in-range window while staging it
+          rc = dense_accumulate(s, v, g.first, g.second, epoch, /*verify=*/false);
+        } else if (device && (flags & PSKV_SORTED_HINT)) {
+          rc = dense_accumulate(s, v, g.first, g.second, epoch, /*verify=*/true);
+        } else {
+          // K5 (no global atomics) measured faster than K4a (LDS sums + one
+          // atomic add per distinct key per chunk) on cfg 3: 322 vs 380 us per
+          // 8M Zipf keys; PSKV_GENERAL=stamps selects K4a
+          rc = general_add(s, v, g.first, g.second, epoch, nullptr);
+        }
+      } else if (!device && host_verified) {
+        // the CPU proved the batches sorted and in range while staging them
+        rc = sorted_add(s, v, g.first, g.second, vec, epoch, /*repair=*/false);
+      } else if (device && (flags & PSKV_SORTED_HINT)) {
+        rc = sorted_add(s, v, g.first, g.second, vec, epoch, /*repair=*/true);
+      } else {
         rc = general_add(s, v, g.first, g.second, epoch, nullptr);
       }
-    } else if (!device && host_verified) {
-      // the CPU proved the batches sorted and in range while staging them
-      rc = sorted_add(s, v, g.first, g.second, vec, epoch, /*repair=*/false);
-    } else if (device && (flags & PSKV_SORTED_HINT)) {
-      rc = sorted_add(s, v, g.first, g.second, vec, epoch, /*repair=*/true);
-    } else {
-      rc = general_add(s, v, g.first, g.second, epoch, nullptr);
+      if (rc) return rc;
     }
-    if (rc) return rc;
+    return PSKV_OK;
+  };
+  rc = run();
+  if (!framed.empty()) {
+    std::string err = rc ? g_last_error : std::string();
+    const int rn = note_frame_uses(s, framed);
+    if (rc) {
+      g_last_error = err;  // report the first failure
+      return rc;
+    }
+    return rn;
   }
-  if (!framed.empty()) return note_frame_uses(s, framed);
-  return PSKV_OK;
+  return rc;
 }
 
 // Zero-copy host Get of a medium batch: the keys are copied into pinned staging
@@ -1440,7 +1495,8 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
     for (auto& b : v) bytes += round16(b.n * 4) + round16(b.n * (size_t)s->vb);
     std::vector<pskv_batch> views;
     if (bytes <= s->tune_frame_zc_max_bytes &&
-        (((flags & PSKV_HOST_FRAME) && frame_views(v, (size_t)s->vb, &views)) || pinned_views(v, &views)))
+        (((flags & PSKV_HOST_FRAME) && frame_views(v, (size_t)s->vb, &views)) ||
+         pinned_views(v, (size_t)s->vb, &views)))
       return zero_copy_get_views(s, views);
   }
   std::vector<pskv_batch> dv = v;

@@ -4,9 +4,13 @@
                  b_j = seed-42 uniform multiple of 1M; vals U(-1, 1), seed 42+j
   cfg 3  zipf:   key space 1e8; 1M keys per batch, Zipf(s=0.99) over ranks
                  1..1e8, rank -> key by a seed-7 random permutation, unsorted
-  cfg 4  ranges: G range shards; every rank owns [r*K/G, (r+1)*K/G) and its
-                 producers push contiguous 1M windows inside it (weak scaling:
-                 per-GPU work fixed), routed through the range shard map
+  cfg 4  ranges: 1e9 keys over G range shards (rank r owns [r*K/G, (r+1)*K/G),
+                 base/range_partition_manager.hpp's map); 64 producer streams,
+                 stream s pushes a contiguous 1M window at a uniformly random
+                 base in [0, K - 1M] (seed 1000 + s), sliced by the range map —
+                 a window straddling a boundary splits in two (global_windows,
+                 route_windows).  The weak-scaled form (every rank's producers
+                 push 1M-aligned windows inside its own range) is rank_windows.
 
 Generation uses torch on the target device (outside any timed region).
 """
@@ -92,6 +96,26 @@ def rank_windows(rank: int, world: int, key_space: int, n_windows: int, batch: i
         rng = np.random.default_rng(seed + rank * n_windows + s)
         bases.append(lo + int(rng.integers(0, slots)) * batch)
     return np.asarray(bases, dtype=np.int64)
+
+
+def global_windows(n_producers: int, key_space: int, batch: int = MILLION, seed: int = 1000):
+    """cfg 4: producer stream s pushes the window [b_s, b_s + batch)
+    with b_s uniform over [0, key_space - batch], drawn with seed `seed` + s
+    (default 1000 + s).  Any alignment: windows straddle range boundaries."""
+    return np.asarray([int(np.random.default_rng(seed + s).integers(0, key_space - batch + 1))
+                       for s in range(n_producers)], dtype=np.int64)
+
+
+def interval_union(intervals) -> int:
+    """Number of distinct keys covered by half-open [a, a + n) intervals."""
+    tot, end = 0, -1
+    for a, n in sorted((int(a), int(n)) for a, n in intervals if n > 0):
+        b = a + n
+        if b <= end:
+            continue
+        tot += b - max(a, end)
+        end = b
+    return tot
 
 
 def set_seed(r: int, world: int) -> int:

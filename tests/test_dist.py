@@ -33,31 +33,44 @@ def _worker(rank, world, port, q):
         import bench
         import oracle
 
-        J, B = 16, 1_000_000
-        key_space, lo, hi, bases = bench.plan_rank(rank, world, J, B)
-        # gather every rank's range and windows
-        rr = [None] * world
-        dist.all_gather_object(rr, (lo, hi, [int(b) for b in bases]))
-        ranges = [(a, b) for a, b, _ in rr]
-        assert ranges[0][0] == 0 and ranges[-1][1] == key_space
-        assert all(ranges[i][1] == ranges[i + 1][0] for i in range(world - 1))
-        # the reference slicer routes a sample of every window's keys to its owner
-        for r, (_, _, bs) in enumerate(rr):
-            for b in bs:
-                sample = np.array([b, b + 1, b + B // 2, b + B - 1], dtype=np.uint32)
-                sl = oracle.range_slice_ref(ranges, sample)
-                assert [s for s, _ in sl] == [r], (r, b, sl)
-        # every window set the bench rotates over routes to its rank too, and
-        # the sets differ (distinct seeds)
-        for r in (1, 3):
-            _, lo_r, hi_r, bases_r = bench.plan_rank(rank, world, J, B, r)
-            assert (lo_r, hi_r) == (lo, hi)
-            assert all(lo <= int(b) and int(b) + B <= hi for b in bases_r)
-            assert list(bases_r) != list(bases)
+        J, B = 64, 1_000_000
+        for r in (0, 1, 3):
+            key_space, lo, hi, slices, bases = bench.plan_rank(rank, world, J, B, r)
+            assert key_space == 1_000_000_000
+            # gather every rank's range and slices of the 64 global producer windows
+            rr = [None] * world
+            dist.all_gather_object(rr, (lo, hi, slices, [int(b) for b in bases]))
+            ranges = [(a, b) for a, b, _, _ in rr]
+            assert ranges[0][0] == 0 and ranges[-1][1] == key_space
+            assert all(ranges[i][1] == ranges[i + 1][0] for i in range(world - 1))
+            assert all(x[3] == rr[0][3] for x in rr)  # every rank draws the same windows
+            pieces = {}
+            for q_, (a, b, sl, _) in enumerate(rr):
+                for w, first, n in sl:
+                    assert a <= first and first + n <= b  # a slice lies in its rank's range
+                    pieces.setdefault(w, []).append((first, n, q_))
+            # every window is covered exactly, in range order: whole, or split at a
+            # range boundary where it straddles one
+            assert sorted(pieces) == list(range(J))
+            for w, ps_ in pieces.items():
+                ps_.sort()
+                b0 = int(bases[w])
+                assert ps_[0][0] == b0 and sum(n for _, n, _ in ps_) == B
+                assert all(ps_[i][0] + ps_[i][1] == ps_[i + 1][0] for i in range(len(ps_) - 1))
+                # the reference slicer (range_partition_manager.hpp:19-46) routes
+                # the window's keys the same way: its slice boundaries and owners
+                keys = sorted({b0, b0 + B - 1} | {f for f, _, _ in ps_} | {f + n - 1 for f, n, _ in ps_})
+                ref = oracle.range_slice_ref(ranges, np.array(keys, dtype=np.uint32))
+                want = [(q_, [k for k in keys if f <= k < f + n]) for f, n, q_ in ps_]
+                assert ref == want, (w, ref, want)
+            # weak-scaled form: this rank's windows stay inside its range, whole
+            _, lo_w, hi_w, sl_w, _ = bench.plan_rank(rank, world, J, B, r, weak=True)
+            assert (lo_w, hi_w) == (lo, hi) and len(sl_w) == J
+            assert all(lo <= f and f + n <= hi and n == B for _, f, n in sl_w)
         # reductions as bench.py does them (device = cpu under gloo)
         t = bench.max_over_ranks(float(rank + 1), world, torch.device("cpu"))
         u = bench.sum_over_ranks(10.0, world, torch.device("cpu"))
-        q.put((rank, t, u, len(set(bases))))
+        q.put((rank, t, u, len(slices)))
     finally:
         dist.destroy_process_group()
 
@@ -75,4 +88,5 @@ def test_bench_multirank_plan_gloo(world):
         assert p.exitcode == 0
     res = sorted(q.get() for _ in range(world))
     for rank, mx, sm, nb in res:
-        assert mx == float(world) and sm == 10.0 * world and nb >= 1
+        assert mx == float(world) and sm == 10.0 * world and nb >= 0
+    assert sum(nb for *_, nb in res) >= 64  # the last set's windows, split ones counted per slice

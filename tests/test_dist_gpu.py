@@ -1,0 +1,123 @@
+"""cfg 4's multi-rank path on the GPU: two rank processes (gloo, both on cuda:0,
+bench.py's PSKV_BENCH_SHARE_GPU rehearsal setup) each own one 5e8-key range
+shard of the 1e9-key space (base/range_partition_manager.hpp's map) and run
+bench.py's own step — 64 producer windows at uniformly random bases, sliced by
+the range map (straddling windows split), pushed as one grouped Add per rank,
+then the next set's windows pulled — through the timed region (barrier,
+synchronize, max over ranks).  Every pull, and at the end every rank's WHOLE
+dense array, is compared bit for bit with the oracle's sequential
+last-write-wins restatement (map_storage.hpp:17-27) of the slices that rank
+received, in the order it applied them."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank(rank, world, port, q):
+    import sys
+
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), PSKV_BENCH_BACKEND="gloo", PSKV_BENCH_SHARE_GPU="1")
+    try:
+        import torch
+
+        import bench
+        import oracle
+        import parameter_server_amd as ps
+
+        oracle.build()
+        r_, w_, local = bench.dist_init(bench.parse([]))
+        assert (r_, w_, local) == (rank, world, 0)
+        dev = torch.device("cuda:0")
+        J, B, R = 64, 1_000_000, 3
+        sets = [bench.make_set(rank, world, J, B, dev, r) for r in range(2)]
+        # a third set whose windows surely straddle the 5e8 boundary (and
+        # overlap each other across it): the range map splits each in two
+        mid = 500_000_000
+        sets.append(bench.make_set(rank, world, 4, B, dev, 2,
+                                   bases=np.array([mid - 300_001, mid - 999_999, mid - 1, mid - 300_001])))
+        assert len(sets[2]["slices"]) == 4 and all(n < B for _, _, n in sets[2]["slices"])
+        _, lo, hi, _, _ = bench.plan_rank(rank, world, J, B)
+        assert hi - lo == 500_000_000
+        ref = np.zeros(hi - lo, np.float32)
+        host = [[(f, v.cpu().numpy()) for (_, f, _), (_, v) in zip(s["slices"], s["batches"])] for s in sets]
+        with ps.Shard(lo, hi, np.float32, device=0) as sh:
+            sh.set_stream(torch.cuda.current_stream().cuda_stream)
+            form = bench.Form(sh, sets, 1, dev)
+            steps = 2 * R
+            # stepwise: every pull against the oracle state after the step's Add
+            for i in range(steps):
+                for f, v in host[i % R]:
+                    oracle.dense_last_wins(ref, lo, np.arange(f, f + v.size, dtype=np.uint32), v)
+                form.step(i)
+                torch.cuda.synchronize()
+                t = form.pull_of(i)
+                for (_, f, n), o in zip(sets[t]["slices"], form.outs[t]):
+                    got = o.cpu().numpy()
+                    if not np.array_equal(got.view(np.uint32), ref[f - lo:f - lo + n].view(np.uint32)):
+                        raise AssertionError(f"rank {rank} step {i}: pull of key {f} differs from the oracle")
+            # the timed region as bench.py runs it, then the oracle catches up
+            elapsed, own = bench.timed(form, steps, world, dev)
+            assert elapsed >= own > 0
+            for i in range(steps):
+                for f, v in host[i % R]:
+                    oracle.dense_last_wins(ref, lo, np.arange(f, f + v.size, dtype=np.uint32), v)
+            dense = sh.dense_view().cpu().numpy()
+            sh.set_stream(None)
+            sh.sync()
+        if not np.array_equal(dense.view(np.uint32), ref.view(np.uint32)):
+            bad = np.nonzero(dense.view(np.uint32) != ref.view(np.uint32))[0]
+            raise AssertionError(f"rank {rank}: {bad.size} keys differ, first at {lo + bad[:4]}")
+        n_slices = sum(len(s["slices"]) for s in sets)
+        split = sum(1 for s in sets for _, _, n in s["slices"] if n < B)
+        total = bench.sum_over_ranks(float(sum(n for s in sets for _, _, n in s["slices"])), world, dev)
+        q.put((rank, "ok", n_slices, split, total, int(np.count_nonzero(ref))))
+        bench.barrier(world)
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+    except BaseException as e:  # report, never hang the parent
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc(), 0, 0, 0))
+        raise
+
+
+def test_cfg4_two_ranks_bit_exact():
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 2
+    ps = [ctx.Process(target=_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = []
+    for _ in range(world):
+        res.append(q.get(timeout=240))
+    for p in ps:
+        p.join(60)
+    errs = [r for r in res if r[1] != "ok"]
+    assert not errs, "\n".join(str(e[2]) for e in errs)
+    assert all(p.exitcode == 0 for p in ps)
+    res.sort()
+    # every set's windows arrived whole over the two ranks (split ones in two)
+    assert res[0][4] == (2 * 64 + 4) * 1_000_000
+    assert all(r[2] > 0 and r[3] >= 4 and r[5] > 0 for r in res)

@@ -414,6 +414,51 @@ def test_zipf_batches_parity(cuda, oracle_mod):
     assert_bits_equal(got, dense, "zipf")
 
 
+@pytest.mark.parametrize("mode", ["assign", "accumulate"])
+def test_cfg3_full_size_zipf_parity(cuda, oracle_mod, mode):
+    """cfg 3 at its stated size: a 1e8-key float shard, 8 x 1M unsorted
+    Zipf(0.99) pushes (workload.zipf_batches: seed-7 key permutation), as one
+    grouped unhinted Add (K5) — the bench's sparse step.  Assign: the WHOLE dense
+    array equals the oracle's sequential last-write-wins restatement
+    (map_storage.hpp:17-27) bit for bit, and a Get of every pushed key returns
+    it.  Accumulate: every key within the stated recursive-summation bound of
+    the float64 sum, untouched keys exactly 0."""
+    import torch
+
+    import parameter_server_amd as ps
+    from parameter_server_amd import workload
+
+    space = 100_000_000
+    zb = workload.zipf_batches(8, space, device=cuda)
+    keys = [k.cpu().numpy().view(np.uint32) for k, _ in zb]
+    vals = [v.cpu().numpy() for _, v in zb]
+    with ps.Shard(0, space, np.float32, mode=mode) as sh:
+        sh.add_grouped(zb)
+        allk = torch.cat([k for k, _ in zb])
+        pulled = sh.get(allk).cpu().numpy()
+        dense = sh.dense_view().cpu().numpy()
+        sh.sync()
+    allk_np = np.concatenate(keys).astype(np.int64)
+    if mode == "assign":
+        ref = np.zeros(space, np.float32)
+        for k, v in zip(keys, vals):
+            oracle_mod.dense_last_wins(ref, 0, k, v)
+        assert_bits_equal(dense, ref, "cfg 3 dense array")
+        assert_bits_equal(pulled, ref[allk_np], "cfg 3 pulls")
+        return
+    p64 = np.zeros(space, np.float64)
+    a64 = np.zeros(space, np.float64)
+    for k, v in zip(keys, vals):
+        oracle_mod.accumulate_ref(p64, a64, 0, k, v)
+    cnt = np.bincount(allk_np, minlength=space)
+    tol = 1.01 * (cnt + 1) * 2.0**-24 * a64
+    err = np.abs(dense.astype(np.float64) - p64)
+    assert np.all(err <= tol), f"{int(np.sum(err > tol))} keys outside the bound"
+    assert np.all(dense[cnt == 0] == 0)
+    assert cnt.max() > 40_000  # the hot key: ~48k hits per batch
+    assert_bits_equal(pulled, dense[allk_np], "cfg 3 pulls (accumulate)")
+
+
 def test_overflow_table_growth_and_edges(cuda, oracle_mod):
     import parameter_server_amd as ps
 

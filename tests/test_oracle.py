@@ -105,9 +105,12 @@ def test_oracle_rejects_mismatched_sizes(oracle_mod):
 
 
 def test_bench_step_bytes_and_single_gpu_sets():
-    """bench.py's algorithmic byte accounting (Add n*(4+V) + u*V,
-    Get q*(4+2V)) and the N = 1 window sets: 1M-aligned bases inside the 1e8-key
-    shard, set 0 on the config's seed 42, the other sets on distinct seeds."""
+    """bench.py's algorithmic byte accounting (counting what a step
+    must move: Add n*4 keys + u*V last values + u*V parameter writes, Get
+    q*(4+2V)) and the N = 1 window sets: 1M-aligned bases inside the 1e8-key
+    shard, set 0 on the config's seed 42, the other sets on distinct seeds, and
+    a push set plus the next pull set touching more than the 256 MB Infinity
+    Cache."""
     import sys
 
     sys.path.insert(0, ROOT)
@@ -115,12 +118,30 @@ def test_bench_step_bytes_and_single_gpu_sets():
     from parameter_server_amd import workload
 
     add, get = bench.step_bytes(64_000_000, 48_000_000, 64_000_000)
-    assert add == 64_000_000 * 8 + 48_000_000 * 4 and get == 64_000_000 * 12
+    assert add == 64_000_000 * 4 + 2 * 48_000_000 * 4 and get == 64_000_000 * 12
+    assert bench.step_bytes(10, 7, 3, vb=8) == (10 * 4 + 2 * 7 * 8, 3 * 20)
     seen = []
     for r in range(4):
-        ks, lo, hi, bases = bench.plan_rank(0, 1, 64, 1_000_000, r)
+        ks, lo, hi, slices, bases = bench.plan_rank(0, 1, 64, 1_000_000, r)
         assert (ks, lo, hi) == (100_000_000, 0, 100_000_000)
         assert all(b % 1_000_000 == 0 and 0 <= b <= 99_000_000 for b in bases)
+        assert [(w, f, n) for w, f, n in slices] == [(j, int(b), 1_000_000) for j, b in enumerate(bases)]
         seen.append(tuple(int(b) for b in bases))
     assert len(set(seen)) == 4
     assert seen[0] == tuple(int(b) for b in workload.dense_bases(64, 100_000_000, 1_000_000, seed=42))
+    for r in range(4):  # parameters touched by step r: push set r and pull set r+1
+        touched = workload.interval_union([(b, 1_000_000) for b in seen[r] + seen[(r + 1) % 4]]) * 4
+        assert touched > 256 << 20, (r, touched)
+
+
+def test_interval_union_and_global_windows():
+    from parameter_server_amd import workload
+
+    assert workload.interval_union([]) == 0
+    assert workload.interval_union([(5, 3), (0, 2), (6, 4), (20, 0)]) == 2 + 5
+    assert workload.interval_union([(0, 10), (2, 3)]) == 10
+    b = workload.global_windows(64, 1_000_000_000, 1_000_000, seed=1000)
+    assert b.shape == (64,) and int(b.min()) >= 0 and int(b.max()) <= 999_000_000
+    # producer s draws with seed 1000 + s: the same stream whatever the count
+    assert list(workload.global_windows(3, 1_000_000_000, 1_000_000, seed=1000)) == list(b[:3])
+    assert any(int(x) % 4 for x in b)  # any alignment
