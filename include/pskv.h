@@ -137,7 +137,8 @@ enum pskv_kernel {
   PSKV_K_ACC_DENSE = 7,     /* K7: accumulate dense windows, one RMW per key */
   PSKV_K_INLINE_ADD = 8,    /* K8: small host Add carried in the kernel arguments */
   PSKV_K_INLINE_GET = 9,    /* K8: small host Get, reply written to page-locked memory */
-  PSKV_K_COUNT = 10
+  PSKV_K_REPLAY = 10,       /* K4r: conditional replay behind a verifying sorted-path group */
+  PSKV_K_COUNT = 11
 };
 
 /* Create a shard owning keys [key_begin, key_end) on `device`.  The dense

@@ -34,7 +34,8 @@ PSKV_K_DENSE_CHECK = 6
 PSKV_K_ACC_DENSE = 7
 PSKV_K_INLINE_ADD = 8
 PSKV_K_INLINE_GET = 9
-PSKV_K_COUNT = 10
+PSKV_K_REPLAY = 10
+PSKV_K_COUNT = 11
 KERNEL_NAMES = {
     PSKV_K_GATHER: "k_gather",
     PSKV_K_ASSIGN_SORTED: "k_assign_sorted",
@@ -46,6 +47,7 @@ KERNEL_NAMES = {
     PSKV_K_ACC_DENSE: "k_acc_dense",
     PSKV_K_INLINE_ADD: "k_inline_add",
     PSKV_K_INLINE_GET: "k_inline_get",
+    PSKV_K_REPLAY: "k_replay",
 }
 
 # Every symbol include/pskv.h declares (checked by tests/test_abi.py).

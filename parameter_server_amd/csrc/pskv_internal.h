@@ -123,6 +123,10 @@ hipError_t launch_general_commit(int vb, const GroupArgs& ga, uint32_t nwg, cons
                                  const uint32_t* cond, uint32_t epoch, hipStream_t st);
 hipError_t launch_ovf_rehash(int vb, const Ovf& from, uint64_t from_cap, const Ovf& to,
                              hipStream_t st);
+// K4r: conditional replay of a group in call order by ONE workgroup (runs only
+// when *cond == epoch: a sorted-path hint was broken); assign or accumulate.
+hipError_t launch_replay(int dtype, int mode, const GroupArgs& ga, const DenseView& d, const Ovf& o,
+                         const uint32_t* cond, uint32_t epoch, hipStream_t st);
 // K5 key buckets: windows of 2^wbits keys of the owned range, window w in
 // bucket w % nbd (1 <= nbd < 2^12, windows < 2^21: wbits >= 11 or a range
 // below 2^32); magic = ceil(2^32 / nbd); span = keys per bucket at most

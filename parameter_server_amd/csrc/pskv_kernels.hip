@@ -61,6 +61,21 @@ __device__ __forceinline__ void st16(void* p, u32x4 v) {
     *reinterpret_cast<u32x4*>(p) = v;
 }
 
+// A 16-byte load from a DWORD-aligned address (global_load_dwordx4 needs only
+// dword alignment): a window that starts off a 16-byte slot still streams in
+// 16-byte pieces (K2g dense mode, phase != 0).
+typedef unsigned int u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+template <bool NT>
+__device__ __forceinline__ void ld16a4(const uint32_t* p, uint32_t (&v)[4]) {
+  const u32x4 t = NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4a4*>(p))
+                     : *reinterpret_cast<const u32x4a4*>(p);
+  v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+}
+template <bool NT>
+__device__ __forceinline__ void ld16a4(const unsigned long long* p, unsigned long long (&v)[4]) {
+  (void)p; v[0] = v[1] = v[2] = v[3] = 0ull;  // 8-byte values never take the phase path
+}
+
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 template <bool NT>
 __device__ __forceinline__ void ld8_keys(const uint32_t* p, uint32_t (&k)[2]) {
@@ -196,17 +211,32 @@ __device__ __forceinline__ VT load_one(const DenseView& d, const Ovf& o, uint32_
 
 // ------------------------------------------------------------- K1 gather
 
-// Four keys of one lane: when they are four consecutive in-range keys starting
-// on a 4-aligned offset (dense pulls), one 16-byte (or 2x16-byte) load serves
-// them; otherwise four scalar gathers.
+// Four keys of one lane: when they are four consecutive in-range keys (dense
+// pulls), 16-byte parameter loads serve them — one when the run starts on a
+// 16-byte parameter slot, else the two slots it straddles (the second one is
+// the neighbouring lane's first, so the lines are fetched once) and a select;
+// otherwise four scalar gathers.  A pulled window may start at any key (cfg 4's
+// producer windows do); per-element loads there cost K1 ~6 % (align_probe).
 template <typename VT>
 __device__ __forceinline__ void gather4(const DenseView& d, const Ovf& o, const uint32_t (&k)[4],
                                         VT (&v)[4]) {
   const uint32_t off0 = k[0] - d.key_begin;
   const bool run = (k[1] == k[0] + 1u) & (k[2] == k[0] + 2u) & (k[3] == k[0] + 3u) &
-                   ((off0 & 3u) == 0u) & ((uint64_t)off0 + 3u < d.range);
-  if (run) {
+                   ((uint64_t)off0 + 3u < d.range);
+  const uint32_t ph = off0 & 3u;
+  if (run && ph == 0u) {
     Vec4<VT>::load(reinterpret_cast<const VT*>(d.param) + off0, v);
+  } else if (sizeof(VT) == 4 && run) {
+    // both slots start inside the array (off0 - ph >= 0; off0 - ph + 4 <= off0 + 3),
+    // and a 16-byte slot that starts inside the allocation lies inside it
+    const VT* pa = reinterpret_cast<const VT*>(d.param) + (off0 - ph);
+    VT a[4], b[4];
+    Vec4<VT>::load(pa, a);
+    Vec4<VT>::load(pa + 4, b);
+    v[0] = ph == 1u ? a[1] : ph == 2u ? a[2] : a[3];
+    v[1] = ph == 1u ? a[2] : ph == 2u ? a[3] : b[0];
+    v[2] = ph == 1u ? a[3] : ph == 2u ? b[0] : b[1];
+    v[3] = ph == 1u ? b[0] : ph == 2u ? b[1] : b[2];
   } else {
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = load_one<VT>(d, o, k[e]);
@@ -214,14 +244,21 @@ __device__ __forceinline__ void gather4(const DenseView& d, const Ovf& o, const 
 }
 
 // Two keys of one lane, 8-byte values: one 16-byte load when they are two
-// consecutive in-range keys on an even offset.
+// consecutive in-range keys on an even offset; on an odd offset the two
+// 16-byte slots they straddle.
 __device__ __forceinline__ void gather2(const DenseView& d, const Ovf& o, const uint32_t (&k)[2],
                                         unsigned long long (&v)[2]) {
   using T = unsigned long long;
   const uint32_t off0 = k[0] - d.key_begin;
-  const bool run = (k[1] == k[0] + 1u) & ((off0 & 1u) == 0u) & ((uint64_t)off0 + 1u < d.range);
-  if (run) {
+  const bool run = (k[1] == k[0] + 1u) & ((uint64_t)off0 + 1u < d.range);
+  if (run && (off0 & 1u) == 0u) {
     Vec2x8::load(reinterpret_cast<const T*>(d.param) + off0, v);
+  } else if (run) {
+    T a[2], b[2];
+    Vec2x8::load(reinterpret_cast<const T*>(d.param) + (off0 - 1u), a);
+    Vec2x8::load(reinterpret_cast<const T*>(d.param) + (off0 + 1u), b);
+    v[0] = a[1];
+    v[1] = b[0];
   } else {
     v[0] = load_one<T>(d, o, k[0]);
     v[1] = load_one<T>(d, o, k[1]);
@@ -471,7 +508,16 @@ __device__ __forceinline__ bool dense_chunk(const GroupArgs& ga, const DenseView
   const uint64_t base = (uint64_t)(c - ga.wg_prefix[j]) * CH;
   const uint64_t end = n < base + CH ? n : base + CH;
   const uint32_t first = s_first[j];
-  const uint32_t c_lo = first + (uint32_t)base, c_hi = first + (uint32_t)(end - 1);
+  // Phase of the window against the 16-byte parameter slots (4-byte values):
+  // when the window starts off a slot (p != 0; cfg 4's producer windows start
+  // at any key), the chunk STORES the elements [s_lo, s_hi) — its own range
+  // shifted down by p (the first chunk from 0, the last to n) — so its 16-byte
+  // parameter stores are aligned, and VERIFIES its own range [base, end).
+  const uint32_t p0 = first - d.key_begin;
+  const uint32_t ph = (sizeof(VT) == 4 && VEC) ? (p0 & 3u) : 0u;
+  const uint64_t s_lo = (ph == 0u || base == 0) ? base : base - ph;
+  const uint64_t s_hi = (ph == 0u || end == n) ? end : end - ph;
+  const uint32_t c_lo = first + (uint32_t)s_lo, c_hi = first + (uint32_t)(end - 1);
   // later batches whose interval meets this chunk's interval (every wave computes it)
   const bool ov = lane > j && lane < ga.nb && s_first[lane] <= c_hi && s_last[lane] >= c_lo;
   const unsigned long long later = __ballot(ov);
@@ -535,49 +581,86 @@ __device__ __forceinline__ bool dense_chunk(const GroupArgs& ga, const DenseView
       }
     }
   } else if (VEC && end - base == CH) {
+    // 4-byte values, a whole chunk.  Each lane verifies its 16-byte key piece
+    // i .. i+3 and stores the 16-byte parameter slot of the elements
+    // g = i - ph .. +3 (slot-aligned: p0 + g == 0 mod 4), their values read by
+    // one dword-aligned 16-byte load (phase 0: the aligned piece i itself).
+    // So a window at any key streams like an aligned one.  (The two aligned
+    // pieces the group straddles, selected in registers, took the kernel from
+    // 95 to 127 VGPRs; shuffling the previous lane's piece, to 134.)
+    using BT = typename std::conditional<sizeof(VT) == 4, uint32_t, VT>::type;
+    const BT* __restrict__ vb = reinterpret_cast<const BT*>(vals);
+    BT* __restrict__ pb = reinterpret_cast<BT*>(param);
+    // chunk-uniform bases (scalar registers) and 32-bit lane offsets: one
+    // address register per access instead of a 64-bit pair
+    const uint32_t* __restrict__ kc = keys + base;
+    const bool head = base == 0 && ph != 0u;  // the batch's first piece starts its group before element 0
+    const BT* __restrict__ vc = vb + (base - (head ? 0u : ph));
+    BT* __restrict__ pc = pb + p0 + (base - (head ? 0u : ph));
     uint32_t k[U][4];
-    VT v[U][4];
+    BT v[U][4];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint64_t i = base + (uint64_t)(u * kBlock + tid) * 4;
-      Vec4<uint32_t>::load<NT>(keys + i, k[u]);
-      Vec4<VT>::template load<NT>(vals + i, v[u]);
+      const uint32_t o = (uint32_t)(u * kBlock + tid) * 4u;
+      Vec4<uint32_t>::load<NT>(kc + o, k[u]);
+      if (!head || o != 0u) {
+        ld16a4<NT>(vc + (o - (head ? ph : 0u)), v[u]);
+      } else {  // group starts before element 0: its valid part one by one
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[u][e] = (uint32_t)e >= ph ? vb[e - ph] : BT(0);
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint64_t i = base + (uint64_t)(u * kBlock + tid) * 4;
-      const uint32_t k0 = first + (uint32_t)i;
+      const uint32_t o = (uint32_t)(u * kBlock + tid) * 4u;
+      const uint32_t k0 = first + (uint32_t)base + o;
       bad |= (k[u][0] != k0) | (k[u][1] != k0 + 1u) | (k[u][2] != k0 + 2u) | (k[u][3] != k0 + 3u);
-      const uint32_t off0 = k0 - d.key_begin;
-      if (later == 0 && (off0 & 3u) == 0u) {
-        Vec4<VT>::template store<NTP>(param + off0, v[u]);
+      if (later == 0 && (!head || o != 0u)) {
+        Vec4<BT>::template store<NTP>(pc + (o - (head ? ph : 0u)), v[u]);
       } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (!shadowed(k0 + e)) param[off0 + e] = v[u][e];
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t g = (uint32_t)base + o + (uint32_t)e;  // element g - ph of the batch
+          if (g >= ph && !shadowed(first + (g - ph))) pb[p0 + (g - ph)] = v[u][e];
+        }
       }
+    }
+    // the last ph elements of the batch, when this chunk ends it: no group
+    // holds them
+    if (ph != 0u && end == n && (uint32_t)tid < ph) {
+      const uint64_t ie = n - ph + tid;
+      if (!shadowed(first + (uint32_t)ie)) pb[p0 + ie] = vb[ie];
     }
   } else {
     // a partial (or unaligned) chunk — the last one of every window: eight
     // elements per lane loaded together, then checked and stored, so the
     // chunk costs one dependent round trip per eight elements per lane rather
-    // than one per element (a window's 576-key tail took three in a row)
+    // than one per element (a window's 576-key tail took three in a row).
+    // It verifies its own elements [base, end) and stores [s_lo, s_hi) (the
+    // same range unless the phase shifted it, above)
     for (uint64_t i0 = base + tid; i0 < end; i0 += 8ull * kBlock) {
       uint32_t kk[8];
-      VT vv[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const uint64_t i = i0 + (uint64_t)q * kBlock;
-        kk[q] = i < end ? keys[i] : 0u;
-        vv[q] = i < end ? vals[i] : VT(0);
+        kk[q] = i < end ? keys[i] : first + (uint32_t)i;
       }
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const uint64_t i = i0 + (uint64_t)q * kBlock;
-        if (i >= end) continue;
-        const uint32_t k = first + (uint32_t)i;
-        bad |= kk[q] != k;
-        if (!shadowed(k)) param[k - d.key_begin] = vv[q];
+      for (int q = 0; q < 8; ++q) bad |= kk[q] != first + (uint32_t)(i0 + (uint64_t)q * kBlock);
+    }
+    if (!covered) {
+      for (uint64_t i0 = s_lo + tid; i0 < s_hi; i0 += 8ull * kBlock) {
+        VT vv[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const uint64_t i = i0 + (uint64_t)q * kBlock;
+          vv[q] = i < s_hi ? vals[i] : VT(0);
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const uint64_t i = i0 + (uint64_t)q * kBlock;
+          if (i < s_hi && !shadowed(first + (uint32_t)i)) param[p0 + i] = vv[q];
+        }
       }
     }
   }
@@ -1554,6 +1637,105 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
   }
 }
 
+// ------------------------------------------ K4r conditional group replay
+// The safety net behind the sorted paths (K2 / K2g verify their hint on every
+// element and tag `cond` with the call's epoch on any violation; K7 behind
+// K6's density proof).  ONE workgroup replays the whole group in call order:
+// batch by batch, 4 Ki elements per pass, each pass resolved in an LDS hash
+// (assign: the largest element index of a key wins, map_storage.hpp:22-23;
+// accumulate: the pass's sum of a key, added by the key's first occurrence),
+// the passes separated by workgroup barriers, so later passes' stores land
+// last (one CU: its vector memory operations reach L2 in order).  That
+// overwrites every key the group touched with its sequential value, whatever
+// the sorted pass wrote — a wrong hint costs time, never correctness.
+// Why one workgroup: the launch sits behind EVERY hinted group and almost
+// always exits at once, so what matters is its idle cost — one launch of one
+// workgroup (the two-launch, grid-wide K4a/K4b repair it replaces cost two
+// kernel boundaries per step) — not the speed of a repair that only a broken
+// hint triggers (~1 GB/s: 64 M keys take ~0.3 s).
+constexpr int kReplayBlock = 1024;
+constexpr int kReplayChunk = 4 * kReplayBlock;
+constexpr int kReplaySlots = 2 * kReplayChunk;
+
+template <typename VT, int MODE>
+__global__ __launch_bounds__(kReplayBlock) void k_replay(GroupArgs ga, DenseView d, Ovf o,
+                                                         const uint32_t* cond, uint32_t epoch) {
+  if (*cond != epoch) return;  // the hint held (the usual case)
+  constexpr int PER = kReplayChunk / kReplayBlock;
+  __shared__ uint32_t hk[kReplaySlots];
+  __shared__ uint32_t hidx[MODE == 0 ? kReplaySlots + 1 : 1];  // assign: 1 + largest local index
+  __shared__ VT hsum[MODE == 1 ? kReplaySlots + 1 : 1];        // accumulate: the pass's sums
+  __shared__ uint32_t sent;
+  const int tid = threadIdx.x;
+  for (int j = 0; j < ga.nb; ++j) {
+    const uint32_t* __restrict__ keys = ga.b[j].keys;
+    const VT* __restrict__ vals = reinterpret_cast<const VT*>(ga.b[j].vals);
+    const uint64_t n = ga.b[j].n;
+    for (uint64_t base = 0; base < n; base += kReplayChunk) {
+      for (int s = tid; s < kReplaySlots; s += kReplayBlock) {
+        hk[s] = kEmpty32;
+        if (MODE == 0)
+          hidx[s] = 0u;
+        else
+          hsum[s] = VT(0);
+      }
+      if (tid == 0) {
+        sent = 0u;
+        if (MODE == 0)
+          hidx[kReplaySlots] = 0u;
+        else
+          hsum[kReplaySlots] = VT(0);
+      }
+      __syncthreads();  // also orders the previous pass's stores before this pass's
+      uint32_t key[PER], slot[PER], valid = 0;
+      VT v[PER];
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const uint64_t i = base + (uint64_t)(q * kReplayBlock + tid);
+        const bool in = i < n;
+        valid |= in ? (1u << q) : 0u;
+        key[q] = in ? keys[i] : 0u;
+        v[q] = in ? vals[i] : VT(0);
+      }
+      const uint32_t own = lds_insert<PER, kReplaySlots>(hk, &sent, key, valid, slot);
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        if (!(valid >> q & 1u)) continue;
+        if (MODE == 0)
+          atomicMax(&hidx[slot[q]], (uint32_t)(q * kReplayBlock + tid) + 1u);
+        else
+          lds_add(&hsum[slot[q]], v[q]);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        if (!(valid >> q & 1u)) continue;
+        const uint32_t off = key[q] - d.key_begin;
+        if (MODE == 0) {
+          if (hidx[slot[q]] != (uint32_t)(q * kReplayBlock + tid) + 1u) continue;  // a later occurrence wins
+          if ((uint64_t)off < d.range) {
+            reinterpret_cast<VT*>(d.param)[off] = v[q];
+          } else {
+            const long long sl = ovf_insert(o, key[q]);
+            if (sl >= 0) reinterpret_cast<VT*>(o.vals)[sl] = v[q];
+          }
+        } else {
+          if (!(own >> q & 1u)) continue;  // the key's inserting lane adds the pass's sum
+          VT* p = nullptr;
+          if ((uint64_t)off < d.range) {
+            p = reinterpret_cast<VT*>(d.param) + off;
+          } else {
+            const long long sl = ovf_insert(o, key[q]);
+            if (sl >= 0) p = reinterpret_cast<VT*>(o.vals) + sl;
+          }
+          if (p) *p = add_wrap<VT>(*p, hsum[slot[q]]);
+        }
+      }
+      __syncthreads();  // the table is read before the next pass clears it
+    }
+  }
+}
+
 // ------------------------------------------- K6/K7 dense accumulate
 // Accumulate for grouped batches that are each one contiguous key window
 // (first_j .. first_j + n_j - 1): no atomics and no duplicates to resolve.
@@ -2176,6 +2358,25 @@ hipError_t launch_general_commit(int vb, const GroupArgs& ga, uint32_t nwg, cons
     k_general_commit<uint32_t><<<nwg, kBlock, 0, st>>>(ga, d, o, owner, cond, epoch);
   else
     k_general_commit<unsigned long long><<<nwg, kBlock, 0, st>>>(ga, d, o, owner, cond, epoch);
+  return hipGetLastError();
+}
+
+hipError_t launch_replay(int dtype, int mode, const GroupArgs& ga, const DenseView& d, const Ovf& o,
+                         const uint32_t* cond, uint32_t epoch, hipStream_t st) {
+  if (ga.nb == 0) return hipSuccess;
+  if (mode == 0) {
+    // assign moves value bits only: int32 and float share the 4-byte form
+    if (dtype == 2)
+      k_replay<unsigned long long, 0><<<1, kReplayBlock, 0, st>>>(ga, d, o, cond, epoch);
+    else
+      k_replay<uint32_t, 0><<<1, kReplayBlock, 0, st>>>(ga, d, o, cond, epoch);
+  } else if (dtype == 0) {
+    k_replay<int, 1><<<1, kReplayBlock, 0, st>>>(ga, d, o, cond, epoch);
+  } else if (dtype == 1) {
+    k_replay<float, 1><<<1, kReplayBlock, 0, st>>>(ga, d, o, cond, epoch);
+  } else {
+    k_replay<double, 1><<<1, kReplayBlock, 0, st>>>(ga, d, o, cond, epoch);
+  }
   return hipGetLastError();
 }
 

@@ -805,8 +805,23 @@ int general_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_
   return PSKV_OK;
 }
 
+// The safety net behind a verifying sorted-path launch group: K4r replays the
+// group in call order iff the verification tagged s->flag with `epoch` (one
+// single-workgroup launch that exits at once otherwise).
+int replay(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t e, uint32_t epoch) {
+  GroupArgs ga;
+  (void)build_group(v, b, e, kGeneralChunk, &ga);
+  uint64_t elems = 0;
+  for (size_t i = b; i < e; ++i) elems += v[i].n;
+  LaunchTimer t(s, PSKV_K_REPLAY, elems);
+  PSKV_HIP(launch_replay(s->dtype, s->mode, ga, s->dview(), s->ovf, s->flag, epoch, s->stream));
+  t.done();
+  s->n_general++;
+  return PSKV_OK;
+}
+
 // Sorted path over one launch group of device-resident batches (verifying);
-// `repair` adds the conditional general launches behind it.
+// `repair` adds the conditional replay launch behind it.
 int sorted_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t e, bool vec,
                uint32_t epoch, bool repair) {
   uint64_t elems = 0;
@@ -824,15 +839,19 @@ int sorted_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t
     while (shift > 12 && (elems >> shift) < 2048) --shift;
     if (s->tune_tile_shift) shift = s->tune_tile_shift;
     const uint64_t ntiles = (s->range + (1ull << shift) - 1) >> shift;
-    const uint32_t grid =
-        (uint32_t)std::min<uint64_t>(std::max<uint64_t>(ntiles, nchunks), s->tune_tile_grid);
+    // grid: one workgroup per dense-mode chunk (the common case: every batch a
+    // window), at least 1024 for the tile mode's grid-stride over the tiles;
+    // a workgroup beyond the chunks only runs the prologue (two dependent key
+    // loads per batch) and leaves
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(
+        std::max<uint64_t>(std::min<uint64_t>(ntiles, 1024), nchunks), s->tune_tile_grid);
     LaunchTimer t(s, PSKV_K_ASSIGN_TILES, elems);
     PSKV_HIP(launch_assign_group(s->vb, vec, s->tune_unroll, s->tune_nt, s->tune_ntp, ga, s->dview(), shift,
                                  ntiles, grid, s->flag, epoch, s->stream));
     t.done();
   }
   s->n_sorted++;
-  if (repair) return general_add(s, v, b, e, epoch, s->flag);
+  if (repair) return replay(s, v, b, e, epoch);
   return PSKV_OK;
 }
 
@@ -858,7 +877,7 @@ int dense_accumulate(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, 
     t.done();
   }
   s->n_sorted++;
-  if (verify) return general_add(s, v, b, e, epoch, s->flag, /*radix=*/false);
+  if (verify) return replay(s, v, b, e, epoch);
   return PSKV_OK;
 }
 

@@ -512,15 +512,23 @@ bool same(const Run& a, const Run& b, std::string* why) {
   return true;
 }
 
-// The reference model tests (server/consistency/*_model_test.cpp) over a storage.
+// The reference model tests (server/consistency/*_model_test.cpp) over a storage,
+// and its server/util tests (ProgressTracker, PendingBuffer).  Each case prints
+// "case <name>: ok" — the names of tests/golden/reference_known_answers.json's
+// model_cases / util_cases, which tests/test_replay.py checks are all present.
 template <typename MakeStorage>
 int known_answers(MakeStorage make, const char* label) {
-  int fails = 0;
+  int fails = 0, case_fails = 0;
   auto expect = [&](bool c, const char* what) {
     if (!c) {
       ++fails;
+      ++case_fails;
       std::printf("  FAIL [%s] %s\n", label, what);
     }
+  };
+  auto done = [&](const char* name) {
+    std::printf("[%s] case %s: %s\n", label, name, case_fails ? "FAIL" : "ok");
+    case_fails = 0;
   };
   auto msg = [](Flag f, int sender, std::vector<int> keys, std::vector<int> vals) {
     Message m;
@@ -556,6 +564,7 @@ int known_answers(MakeStorage make, const char* label) {
            "ssp: key 0 -> 1 to worker 2");
     q.Pop(&r);
     expect(third_party::SArray<int>(r.data[1])[0] == 2 && r.meta.recver == 3, "ssp: key 1 -> 2 to worker 3");
+    done("SSP CheckGetAndAdd");
   }
   {  // ssp_model_test.cpp:161-251 CheckStaleness
     ReplyQueue q;
@@ -579,6 +588,7 @@ int known_answers(MakeStorage make, const char* label) {
     Message g2 = msg(Flag::kGet, 2, {0}, {});
     md.Get(g2);
     expect(md.GetPendingSize(1) == 0, "ssp staleness: released");
+    done("SSP CheckStaleness");
   }
   {  // bsp_model_test.cpp:29-130 CheckGetAndAdd
     ReplyQueue q;
@@ -601,6 +611,90 @@ int known_answers(MakeStorage make, const char* label) {
     Message cm2 = msg(Flag::kGet, 3, {1}, {});
     md.Get(cm2);
     expect(q.Pop(&r) && third_party::SArray<int>(r.data[1])[0] == 100, "bsp: 100 after the clock");
+    done("BSP CheckGetAndAdd");
+  }
+  {  // asp_model_test.cpp:33-179 CheckGetAndAdd: Gets served at once, in order
+     // with the Adds; Clock a no-op
+    ReplyQueue q;
+    ASPModel md(0, make(), &q);
+    reset(&md, q);
+    auto reply = [&](int recver, int key, int val, const char* what) {
+      Message r;
+      const bool got = q.Pop(&r);
+      expect(got && r.meta.flag == Flag::kGet && r.meta.sender == 0 && r.meta.recver == recver &&
+                 r.data.size() == 2 && third_party::SArray<int>(r.data[0]).size() == 1 &&
+                 third_party::SArray<int>(r.data[0])[0] == key && third_party::SArray<int>(r.data[1])[0] == val,
+             what);
+    };
+    Message g0 = msg(Flag::kGet, 2, {0}, {}), g1 = msg(Flag::kGet, 3, {1}, {});
+    md.Get(g0);
+    md.Get(g1);
+    reply(2, 0, 0, "asp: key 0 -> 0 to worker 2");
+    reply(3, 1, 0, "asp: key 1 -> 0 to worker 3");
+    Message g2 = msg(Flag::kGet, 3, {1}, {}), a2 = msg(Flag::kAdd, 2, {1}, {1});
+    md.Get(g2);
+    md.Add(a2);
+    expect(q.Size() == 1, "asp: the Get is not blocked");
+    reply(3, 1, 0, "asp: the Get before the Add reads 0");
+    Message g3 = msg(Flag::kGet, 2, {1}, {});
+    md.Clock(g3);
+    md.Get(g3);
+    expect(q.Size() == 1, "asp: clock then get");
+    reply(2, 1, 1, "asp: key 1 -> 1 after the Add");
+    Message a3 = msg(Flag::kAdd, 3, {0}, {1});
+    md.Add(a3);
+    md.Clock(a3);
+    Message g4 = msg(Flag::kGet, 3, {0}, {});
+    md.Get(g4);
+    expect(q.Size() == 1, "asp: add, clock, get");
+    reply(3, 0, 1, "asp: key 0 -> 1");
+    done("ASP CheckGetAndAdd");
+  }
+  {  // progress_tracker_test.cpp:19-25 Basic
+    ProgressTracker t;
+    t.Init({2, 7});
+    expect(t.GetNumThreads() == 2 && t.GetProgress(2) == 0 && t.GetProgress(7) == 0, "tracker basic");
+    done("ProgressTracker Basic");
+  }
+  {  // progress_tracker_test.cpp:27-34 CheckThreadValid
+    ProgressTracker t;
+    t.Init({2, 7});
+    expect(t.CheckThreadValid(2) && !t.CheckThreadValid(3) && !t.CheckThreadValid(6) && t.CheckThreadValid(7),
+           "tracker valid threads");
+    done("ProgressTracker CheckThreadValid");
+  }
+  {  // progress_tracker_test.cpp:36-47 Advance
+    ProgressTracker t;
+    t.Init({2, 7});
+    expect(t.GetMinClock() == 0, "tracker min 0");
+    expect(t.AdvanceAndGetChangedMinClock(2) == -1, "advance 2 -> [1,0]");
+    expect(t.AdvanceAndGetChangedMinClock(7) == 1, "advance 7 -> [1,1]");
+    expect(t.AdvanceAndGetChangedMinClock(7) == -1, "advance 7 -> [1,2]");
+    expect(t.AdvanceAndGetChangedMinClock(7) == -1, "advance 7 -> [1,3]");
+    expect(t.AdvanceAndGetChangedMinClock(2) == 2, "advance 2 -> [2,3]");
+    expect(t.GetProgress(2) == 2 && t.GetProgress(7) == 3, "tracker progress");
+    done("ProgressTracker Advance");
+  }
+  {  // progress_tracker_test.cpp:49-55 UniqueMin
+    ProgressTracker t;
+    t.Init({2, 7});
+    expect(!t.IsUniqueMin(2), "not unique min at [0,0]");
+    t.AdvanceAndGetChangedMinClock(2);
+    expect(t.IsUniqueMin(7), "unique min at [1,0]");
+    done("ProgressTracker UniqueMin");
+  }
+  {  // pending_buffer_test.cpp:21-61 PushAndPop
+    PendingBuffer b;
+    Message m1 = msg(Flag::kAdd, 2, {0}, {1}), m2 = msg(Flag::kAdd, 2, {0}, {1});
+    b.Push(0, m1);
+    b.Push(0, m1);
+    b.Push(1, m2);
+    expect(b.Size(0) == 2 && b.Size(1) == 1, "buffer sizes");
+    const auto p0 = b.Pop(0);
+    const auto p1 = b.Pop(1);
+    expect(p0.size() == 2 && p1.size() == 1, "buffer pops");
+    expect(b.Size(0) == 0 && b.Size(1) == 0, "buffer empty after the pops");
+    done("PendingBuffer PushAndPop");
   }
   std::printf("[%s] model known answers: %s\n", label, fails ? "FAIL" : "ok");
   return fails;

@@ -74,6 +74,44 @@ KNOWN = {
                         {"recver": 3, "keys": [1], "vals": [0]},
                         {"recver": 3, "keys": [1], "vals": [100]}],
         },
+        {
+            "name": "SSP CheckStaleness",
+            "cite": "server/consistency/ssp_model_test.cpp:161-251",
+            "staleness": 2, "tids": [2, 3],
+            # worker 2 runs ahead: its Get at clock 3 > min 0 + 2 is buffered at
+            # 3 - 2 = 1 and released (as the request) when worker 3 clocks
+            "ops": [["get", 2, [0]], ["clock", 2], ["add", 2, [0], [1]], ["clock", 2], ["clock", 2],
+                    ["get", 2, [0]], ["pending", 1, 1], ["clock", 3], ["get", 2, [0]], ["pending", 1, 0]],
+        },
+        {
+            "name": "ASP CheckGetAndAdd",
+            "cite": "server/consistency/asp_model_test.cpp:33-179",
+            "tids": [2, 3],
+            # Gets are served at once, in order with the Adds; Clock is a no-op
+            "ops": [["get", 2, [0]], ["get", 3, [1]], ["get", 3, [1]], ["add", 2, [1], [1]],
+                    ["clock", 2], ["get", 2, [1]], ["add", 3, [0], [1]], ["clock", 3], ["get", 3, [0]]],
+            "replies": [{"recver": 2, "sender": 0, "keys": [0], "vals": [0]},
+                        {"recver": 3, "sender": 0, "keys": [1], "vals": [0]},
+                        {"recver": 3, "sender": 0, "keys": [1], "vals": [0]},
+                        {"recver": 2, "sender": 0, "keys": [1], "vals": [1]},
+                        {"recver": 3, "sender": 0, "keys": [0], "vals": [1]}],
+        },
+    ],
+    # server/util: the progress tracker and pending buffer the SSP/BSP models
+    # are built on.  ops: [query, argument(s), expected]
+    "util_cases": [
+        {"name": "ProgressTracker Basic", "cite": "server/util/progress_tracker_test.cpp:19-25", "tids": [2, 7],
+         "ops": [["num_threads", 2], ["progress", 2, 0], ["progress", 7, 0]]},
+        {"name": "ProgressTracker CheckThreadValid", "cite": "server/util/progress_tracker_test.cpp:27-34",
+         "tids": [2, 7], "ops": [["valid", 2, True], ["valid", 3, False], ["valid", 6, False], ["valid", 7, True]]},
+        {"name": "ProgressTracker Advance", "cite": "server/util/progress_tracker_test.cpp:36-47", "tids": [2, 7],
+         "ops": [["min_clock", 0], ["advance", 2, -1], ["advance", 7, 1], ["advance", 7, -1], ["advance", 7, -1],
+                 ["advance", 2, 2], ["progress", 2, 2], ["progress", 7, 3]]},
+        {"name": "ProgressTracker UniqueMin", "cite": "server/util/progress_tracker_test.cpp:49-55", "tids": [2, 7],
+         "ops": [["unique_min", 2, False], ["advance", 2, -1], ["unique_min", 7, True]]},
+        {"name": "PendingBuffer PushAndPop", "cite": "server/util/pending_buffer_test.cpp:21-61",
+         "ops": [["push", 0], ["push", 0], ["push", 1], ["size", 0, 2], ["size", 1, 1], ["pop", 0, 2],
+                 ["pop", 1, 1]]},
     ],
     "slice_cases": [
         {"cite": "base/range_partition_manager_test.cpp:19-33", "ranges": [[2, 4], [4, 7], [7, 10]],

@@ -567,6 +567,56 @@ def test_grouped_dense_windows_mode(cuda, oracle_mod, nb, dtype):
     assert_bits_equal(got, dense, f"dense windows nb={nb}")
 
 
+@pytest.mark.parametrize("key_begin", [0, 1, 2, 3])
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_dense_windows_every_phase(cuda, oracle_mod, key_begin, dtype):
+    """cfg 4's producer windows start at any key: windows at every phase against
+    the 16-byte parameter slots (the shard's key_begin shifts it once more),
+    lengths around the dense chunk (8192 keys) and its multiples, whole windows
+    repeated (a later one covers an earlier one), partial overlaps, tiny
+    windows; grouped sorted Add (K2g dense mode: phase-shifted slot stores),
+    then Gets of every window, of windows at other phases and of the whole
+    array (K1: the two-slot loads) — bit-exact against the oracle."""
+    import torch
+
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(700 + key_begin)
+    size = 600_000
+    kb = key_begin
+    dense = np.zeros(size, dtype)
+    wins = []
+    for n in (8192 * 3, 8192 * 3 + 1, 8192 * 3 - 1, 8192 * 5 + 2, 8192 + 3, 8191, 8193, 4, 3, 1, 2, 5, 70_001):
+        for ph in range(4):
+            b = int(rng.integers(0, (size - n) // 4)) * 4 + ph
+            wins.append((b, n))
+    wins.append(wins[0])                               # repeated whole: the later one wins
+    b0, n0 = wins[5]
+    wins.append((b0 + 1000, 30_000))                   # partial overlap of a phase-1 window
+    rng.shuffle(wins)
+    batches = []
+    for b, n in wins:
+        k = np.arange(kb + b, kb + b + n, dtype=np.uint32)
+        v = rng.standard_normal(n).astype(dtype)
+        batches.append((k, v))
+    with ps.Shard(kb, kb + size, dtype) as sh:
+        for g in (batches[:27], batches[27:]):         # two grouped calls
+            sh.add_grouped([(tdev(k, cuda), tdev(v, cuda)) for k, v in g], sorted_hint=True)
+            for k, v in g:
+                oracle_mod.dense_last_wins(dense, kb, k, v)
+        outs = [torch.empty(k.size, dtype=torch.float32 if dtype == np.float32 else torch.float64,
+                            device=cuda) for k, _ in batches]
+        sh.get_grouped([(tdev(k, cuda), o) for (k, _), o in zip(batches, outs)])
+        for (k, _), o in zip(batches, outs):
+            assert_bits_equal(o.cpu().numpy(), dense[k.astype(np.int64) - kb], f"pull of window at {k[0]}")
+        for ph in range(4):                            # pulls at other phases than the pushes
+            b = int(rng.integers(0, (size - 40_000) // 4)) * 4 + ph
+            k = np.arange(kb + b, kb + b + 40_000, dtype=np.uint32)
+            assert_bits_equal(sh.get(tdev(k, cuda)).cpu().numpy(), dense[b:b + 40_000], f"pull phase {ph}")
+        got = sh.get(np.arange(kb, kb + size, dtype=np.uint32))
+    assert_bits_equal(got, dense, f"dense windows at every phase, key_begin {kb}")
+
+
 def test_grouped_dense_lookalike_is_repaired(cuda, oracle_mod):
     """Endpoints say 'dense window' but the keys are not contiguous (two swapped,
     one duplicated): the per-element check must tag the group for repair."""

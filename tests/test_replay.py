@@ -20,11 +20,24 @@ def run(*args):
     return r.returncode, r.stdout + r.stderr
 
 
+def known_case_names():
+    import json
+
+    with open(os.path.join(ROOT, "tests", "golden", "reference_known_answers.json")) as f:
+        k = json.load(f)
+    return [c["name"] for c in k["model_cases"] + k["util_cases"]]
+
+
 @pytest.mark.parametrize("model", ["ssp", "bsp", "asp"])
 def test_replay_cpu_deterministic_and_model_known_answers(model):
     rc, out = run("--cpu-only", "--known-answers", "--model", model, "--iters", "6")
     assert rc == 0, out
     assert "REPLAY OK" in out and "[oracle] model known answers: ok" in out
+    # every reference model / util test of the fixture ran and passed
+    # (consistency/*_model_test.cpp, util/progress_tracker_test.cpp,
+    # util/pending_buffer_test.cpp)
+    for name in known_case_names():
+        assert f"[oracle] case {name}: ok" in out, name
     if model == "ssp":
         assert "ssp_releases=0 " not in out  # the straggler pattern really exercises staleness
 
@@ -36,6 +49,8 @@ def test_replay_hip_vs_cpu(model, staleness):
                   "--shards", "8", "--workers", "4")
     assert rc == 0, out
     assert "REPLAY OK (bit-exact)" in out and "[hip] model known answers: ok" in out
+    for name in known_case_names():
+        assert f"[hip] case {name}: ok" in out, name
 
 
 @pytest.mark.parametrize("model", ["ssp", "bsp", "asp"])
