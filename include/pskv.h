@@ -187,6 +187,18 @@ void* pskv_get_stream(pskv_shard* s);
 void* pskv_dense_ptr(pskv_shard* s);
 int pskv_shard_info(pskv_shard* s, pskv_info* info);
 
+/* Tuning and path options of one shard, by name (DESIGN.md §5 lists them and
+ * what each selects): GENERAL (0 = K4 stamps, 1 = auto, 2 = K5 always),
+ * UNROLL, NT, NTP, PAGEABLE_DMA, DMA_MIN_BYTES, DMA_MIN_BYTES_GET,
+ * DMA_MIN_BYTES_PINNED, ZC_MAX_BYTES, FRAME_ZC_MAX_BYTES, INLINE,
+ * INLINE_ADD_CHUNKS, INLINE_GET_CHUNKS, ISPIN, SERVE, SERVE_IDLE_US,
+ * TILE_SHIFT, TILE_GRID, RB_WBITS, RB_NBD, RB_TB, RB_APPLY_LOG2.  The
+ * environment variable PSKV_<NAME> sets a creation default.  Every option
+ * changes speed only, never results.  PSKV_EINVAL for an unknown name or a
+ * value out of range (the shard is unchanged). */
+int pskv_set_option(pskv_shard* s, const char* name, int64_t value);
+int pskv_get_option(pskv_shard* s, const char* name, int64_t* value);
+
 /* Per-kernel timing with HIP events on the launch stream (off by default).
  * pskv_set_timing brackets every kernel; pskv_set_timing_mask only the kernels
  * whose bit (1 << pskv_kernel) is set. */

@@ -57,7 +57,7 @@ EXPORTED = [
     "pskv_get_stream", "pskv_dense_ptr", "pskv_shard_info", "pskv_set_timing", "pskv_set_timing_mask",
     "pskv_kernel_time", "pskv_reset_timing", "pskv_range_slice", "pskv_jump_hash", "pskv_last_error",
     "pskv_abi_version", "pskv_device_count", "pskv_host_alloc", "pskv_host_free",
-    "pskv_host_pool_stats", "pskv_host_pool_trim",
+    "pskv_host_pool_stats", "pskv_host_pool_trim", "pskv_set_option", "pskv_get_option",
 ]
 
 
@@ -117,6 +117,8 @@ def _load():
         "pskv_host_free": ([vp], i32),
         "pskv_host_pool_stats": ([ctypes.POINTER(u64)] * 3, i32),
         "pskv_host_pool_trim": ([], i32),
+        "pskv_set_option": ([vp, ctypes.c_char_p, ctypes.c_int64], i32),
+        "pskv_get_option": ([vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cctype>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -307,6 +308,8 @@ struct pskv_shard {
   uint32_t srv_posted = 0;
   unsigned long long srv_idle_ticks = 0;
   bool counted = false;  // in g_device_shards
+  bool add_chunks_set = false;  // INLINE_ADD_CHUNKS chosen explicitly
+  int wall_khz = 0;             // device wall-clock rate (the server's idle timer)
 
   DenseView dview() const { return DenseView{dense, key_begin, range}; }
 };
@@ -427,6 +430,9 @@ int srv_launch(pskv_shard* s) {
   __atomic_store_n(&r->stop, 0u, __ATOMIC_RELAXED);
   __atomic_store_n(&r->alive, 1u, __ATOMIC_RELEASE);
   ++s->srv_gen;
+  // SERVE_IDLE_US may change between launches (pskv_set_option)
+  s->srv_idle_ticks =
+      (unsigned long long)s->tune_serve_idle_us * (unsigned long long)std::max(s->wall_khz, 1) / 1000ull;
   PSKV_HIP(hipEventRecord(s->srv_dep, s->stream));
   PSKV_HIP(hipStreamWaitEvent(s->srv_stream, s->srv_dep, 0));
   PSKV_HIP(launch_serve(s->dtype, s->mode, r, s->dview(), s->ovf, s->ireply, start, s->srv_idle_ticks,
@@ -488,9 +494,7 @@ int srv_ensure(pskv_shard* s) {
     s->srv = static_cast<SrvRing*>(p);
     PSKV_HIP(hipStreamCreateWithFlags(&s->srv_stream, hipStreamNonBlocking));
     PSKV_HIP(hipEventCreateWithFlags(&s->srv_dep, hipEventDisableTiming | hipEventDisableSystemFence));
-    int khz = 0;
-    PSKV_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, s->device));
-    s->srv_idle_ticks = (unsigned long long)s->tune_serve_idle_us * (unsigned long long)std::max(khz, 1) / 1000ull;
+    PSKV_HIP(hipDeviceGetAttribute(&s->wall_khz, hipDeviceAttributeWallClockRate, s->device));
   }
   if (s->srv_running && __atomic_load_n(&s->srv->alive, __ATOMIC_ACQUIRE) == 0u)
     if (int rc = srv_reap(s)) return rc;
@@ -1639,6 +1643,91 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
   return PSKV_OK;
 }
 
+// ------------------------------------------------------------- options
+// Every tuning knob and path selector of a shard, by name: pskv_set_option /
+// pskv_get_option, and the environment variable PSKV_<NAME> as the creation
+// default (the earlier interface; tests and tools now set options per shard).
+// Each entry validates its value; DESIGN.md §5 says what each path is for.
+struct Option {
+  const char* name;
+  int64_t lo, hi;  // accepted range
+  int64_t (*get)(const pskv_shard*);
+  void (*set)(pskv_shard*, int64_t);
+};
+
+#define PSKV_OPT(NAME, LO, HI, FIELD, T)                                           \
+  Option {                                                                         \
+    NAME, LO, HI, [](const pskv_shard* s) -> int64_t { return (int64_t)s->FIELD; }, \
+        [](pskv_shard* s, int64_t v) { s->FIELD = (T)v; }                          \
+  }
+
+const Option kOptions[] = {
+    // general (any order) Add: 0 = K4 stamps, 1 = auto (K5), 2 = K5 always;
+    // the environment form also takes "stamps" / "auto" / "radix"
+    PSKV_OPT("GENERAL", 0, 2, general_path, int),
+    PSKV_OPT("UNROLL", 4, 8, tune_unroll, int),              // 4 or 8 (others: 8)
+    PSKV_OPT("NT", 0, 1, tune_nt, bool),
+    PSKV_OPT("NTP", 0, 1, tune_ntp, bool),
+    PSKV_OPT("PAGEABLE_DMA", 0, 1, tune_pageable_dma, bool),
+    PSKV_OPT("DMA_MIN_BYTES", 0, INT64_MAX, tune_dma_min_bytes, size_t),
+    PSKV_OPT("DMA_MIN_BYTES_GET", 0, INT64_MAX, tune_dma_min_bytes_get, size_t),
+    PSKV_OPT("DMA_MIN_BYTES_PINNED", 0, INT64_MAX, tune_dma_min_bytes_pinned, size_t),
+    PSKV_OPT("ZC_MAX_BYTES", 0, INT64_MAX, tune_zc_max_bytes, size_t),
+    PSKV_OPT("FRAME_ZC_MAX_BYTES", 0, INT64_MAX, tune_frame_zc_max_bytes, size_t),
+    PSKV_OPT("INLINE", 0, 1, tune_inline, bool),
+    PSKV_OPT("INLINE_ADD_CHUNKS", 1, kInlineMaxChunks, tune_inline_add_chunks, int),
+    PSKV_OPT("INLINE_GET_CHUNKS", 1, kInlineMaxChunks, tune_inline_get_chunks, int),
+    PSKV_OPT("ISPIN", 0, 1, tune_ispin, bool),
+    PSKV_OPT("SERVE", 0, 1, tune_serve, bool),
+    PSKV_OPT("SERVE_IDLE_US", 1, 10000000, tune_serve_idle_us, uint32_t),
+    PSKV_OPT("TILE_SHIFT", 0, 20, tune_tile_shift, uint32_t),  // 0 = by size, else 10..20
+    PSKV_OPT("TILE_GRID", 1, 65536, tune_tile_grid, uint32_t),
+    PSKV_OPT("RB_WBITS", 0, 31, tune_rb_wbits, uint32_t),
+    PSKV_OPT("RB_NBD", 0, kRbMaxBuckets - 1, tune_rb_nbd, uint32_t),
+    PSKV_OPT("RB_TB", 0, 11, tune_rb_tb, uint32_t),
+    PSKV_OPT("RB_APPLY_LOG2", 0, 14, tune_rb_apply_log2, int),  // 0 = by size, 13 or 14
+};
+#undef PSKV_OPT
+
+const Option* find_option(const char* name) {
+  for (const auto& o : kOptions)
+    if (std::strcmp(o.name, name) == 0) return &o;
+  return nullptr;
+}
+
+int set_option(pskv_shard* s, const Option& o, int64_t v) {
+  if (v < o.lo || v > o.hi) return fail(PSKV_EINVAL, std::string("option ") + o.name + ": value out of range");
+  if (std::strcmp(o.name, "UNROLL") == 0 && v != 4 && v != 8) return fail(PSKV_EINVAL, "option UNROLL: 4 or 8");
+  if (std::strcmp(o.name, "TILE_SHIFT") == 0 && v != 0 && v < 10) return fail(PSKV_EINVAL, "option TILE_SHIFT: 0 or 10..20");
+  if (std::strcmp(o.name, "RB_APPLY_LOG2") == 0 && v != 0 && v != 13 && v != 14)
+    return fail(PSKV_EINVAL, "option RB_APPLY_LOG2: 0, 13 or 14");
+  o.set(s, v);
+  if (std::strcmp(o.name, "INLINE_ADD_CHUNKS") == 0) s->add_chunks_set = true;
+  // a ring slot costs the host ~0.2 us where a K8 launch costs 3-7: with the
+  // server, Adds of up to 2 slots (512 keys) take it unless the chunk count
+  // was chosen.  Measured (tools/micro/small_latency.cpp, Add then Get): 512
+  // keys 17-18 us against 23-27 through the copy; from 1 Ki keys the server's
+  // per-slot work (~6 us per 256-key slot) is behind the copy (1 Ki: 31-34
+  // against 28)
+  if (std::strcmp(o.name, "SERVE") == 0 && !s->add_chunks_set) s->tune_inline_add_chunks = v ? 2 : 1;
+  return PSKV_OK;
+}
+
+int apply_env_options(pskv_shard* s) {
+  for (const auto& o : kOptions) {
+    const std::string var = std::string("PSKV_") + o.name;
+    const char* e = std::getenv(var.c_str());
+    if (!e || !*e) continue;
+    int64_t v;
+    if (std::strcmp(o.name, "GENERAL") == 0 && (std::isalpha((unsigned char)e[0]) != 0))
+      v = std::strcmp(e, "stamps") == 0 ? 0 : std::strcmp(e, "radix") == 0 ? 2 : 1;
+    else
+      v = std::atoll(e);
+    if (int rc = set_option(s, o, v)) return fail(rc, "environment " + var + ": " + g_last_error);
+  }
+  return PSKV_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1673,50 +1762,11 @@ int pskv_shard_create_ex(int device, uint32_t key_begin, uint64_t key_end, int d
   s->vb = vb;
   s->key_begin = key_begin;
   s->range = key_end - key_begin;
-  if (const char* e = std::getenv("PSKV_TILE_SHIFT")) {
-    const int v = std::atoi(e);
-    if (v >= 10 && v <= 20) s->tune_tile_shift = (uint32_t)v;
-  }
-  if (const char* e = std::getenv("PSKV_GENERAL"))
-    s->general_path = std::strcmp(e, "stamps") == 0 ? 0 : std::strcmp(e, "radix") == 0 ? 2 : 1;
-  if (const char* e = std::getenv("PSKV_UNROLL")) s->tune_unroll = std::atoi(e) == 4 ? 4 : 8;
-  if (const char* e = std::getenv("PSKV_NT")) s->tune_nt = std::atoi(e) != 0;
-  if (const char* e = std::getenv("PSKV_NTP")) s->tune_ntp = std::atoi(e) != 0;
-  if (const char* e = std::getenv("PSKV_PAGEABLE_DMA")) s->tune_pageable_dma = std::atoi(e) != 0;
-  if (const char* e = std::getenv("PSKV_DMA_MIN_BYTES")) s->tune_dma_min_bytes = (size_t)std::atoll(e);
-  if (const char* e = std::getenv("PSKV_DMA_MIN_BYTES_GET")) s->tune_dma_min_bytes_get = (size_t)std::atoll(e);
-  if (const char* e = std::getenv("PSKV_DMA_MIN_BYTES_PINNED")) s->tune_dma_min_bytes_pinned = (size_t)std::atoll(e);
-  if (const char* e = std::getenv("PSKV_ZC_MAX_BYTES")) s->tune_zc_max_bytes = (size_t)std::atoll(e);
-  if (const char* e = std::getenv("PSKV_FRAME_ZC_MAX_BYTES")) s->tune_frame_zc_max_bytes = (size_t)std::atoll(e);
-  if (const char* e = std::getenv("PSKV_INLINE")) s->tune_inline = std::atoi(e) != 0;
-  if (const char* e = std::getenv("PSKV_INLINE_ADD_CHUNKS"))
-    s->tune_inline_add_chunks = std::max(1, std::min(kInlineMaxChunks, std::atoi(e)));
-  if (const char* e = std::getenv("PSKV_INLINE_GET_CHUNKS"))
-    s->tune_inline_get_chunks = std::max(1, std::min(kInlineMaxChunks, std::atoi(e)));
-  if (const char* e = std::getenv("PSKV_ISPIN")) s->tune_ispin = std::atoi(e) != 0;
-  if (const char* e = std::getenv("PSKV_SERVE")) s->tune_serve = std::atoi(e) != 0;
-  // a ring slot costs the host ~0.2 us where a K8 launch costs 3-7: with the
-  // server, Adds of up to 2 slots (512 keys) take it.  Measured
-  // (tools/micro/small_latency.cpp, Add then Get): 512 keys 17-18 us against
-  // 23-27 through the copy; from 1 Ki keys the server's per-slot work (~6 us
-  // per 256-key slot) is behind the copy (1 Ki: 31-34 against 28)
-  if (s->tune_serve && !std::getenv("PSKV_INLINE_ADD_CHUNKS")) s->tune_inline_add_chunks = 2;
-  if (const char* e = std::getenv("PSKV_SERVE_IDLE_US"))
-    s->tune_serve_idle_us = (uint32_t)std::max(1, std::min(10000000, std::atoi(e)));
-  if (const char* e = std::getenv("PSKV_TILE_GRID")) {
-    const int v = std::atoi(e);
-    if (v >= 1 && v <= 65536) s->tune_tile_grid = (uint32_t)v;
-  }
-  if (const char* e = std::getenv("PSKV_RB_WBITS")) s->tune_rb_wbits = (uint32_t)std::max(0, std::min(31, std::atoi(e)));
-  if (const char* e = std::getenv("PSKV_RB_NBD"))
-    if (std::atoi(e) > 0) s->tune_rb_nbd = (uint32_t)std::min(kRbMaxBuckets - 1, std::atoi(e));
-  if (const char* e = std::getenv("PSKV_RB_TB")) {
-    const int v = std::atoi(e);
-    if (v >= 1 && v <= 11) s->tune_rb_tb = (uint32_t)v;
-  }
-  if (const char* e = std::getenv("PSKV_RB_APPLY_LOG2")) {
-    const int v = std::atoi(e);
-    if (v == 13 || v == 14) s->tune_rb_apply_log2 = v;
+  // tuning / path options: creation defaults from the environment (PSKV_<NAME>),
+  // changeable later through pskv_set_option (kOptions below)
+  if (int rc = apply_env_options(s)) {
+    delete s;
+    return rc;
   }
   auto bail = [&](int rc) {
     pskv_shard_destroy(s);
@@ -1932,6 +1982,27 @@ int pskv_reset_timing(pskv_shard* s) {
     s->t_ms[k] = 0;
     s->t_elems[k] = 0;
   }
+  return PSKV_OK;
+}
+
+int pskv_set_option(pskv_shard* s, const char* name, int64_t value) {
+  if (!s || !name) return fail(PSKV_EINVAL, "pskv_set_option: null argument");
+  const Option* o = find_option(name);
+  if (!o) return fail(PSKV_EINVAL, std::string("pskv_set_option: unknown option ") + name);
+  int rc = use_device(s);
+  if (rc) return rc;
+  // the request server runs with the options it was launched with: drain and
+  // stop it first (it restarts on the next small message if still enabled)
+  rc = srv_stop(s);
+  if (rc) return rc;
+  return set_option(s, *o, value);
+}
+
+int pskv_get_option(pskv_shard* s, const char* name, int64_t* value) {
+  if (!s || !name || !value) return fail(PSKV_EINVAL, "pskv_get_option: null argument");
+  const Option* o = find_option(name);
+  if (!o) return fail(PSKV_EINVAL, std::string("pskv_get_option: unknown option ") + name);
+  *value = o->get(s);
   return PSKV_OK;
 }
 

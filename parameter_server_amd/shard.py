@@ -45,7 +45,7 @@ class Shard:
     "accumulate" is the gradient-reduction mode (param[k] += v)."""
 
     def __init__(self, key_begin: int = 0, key_end: int = 1 << 32, dtype=np.float32,
-                 mode: str = "assign", device: int = 0, overflow_slots: int = 0):
+                 mode: str = "assign", device: int = 0, overflow_slots: int = 0, options=None):
         self.dtype = np.dtype(dtype) if not _is_torch(dtype) else _NP_DTYPE[dtype_code(dtype)]
         self.code = dtype_code(self.dtype)
         self.mode = {"assign": _lib.PSKV_ASSIGN, "accumulate": _lib.PSKV_ACCUMULATE}[mode]
@@ -54,6 +54,8 @@ class Shard:
         check(lib.pskv_shard_create_ex(self.device, self.key_begin, self.key_end, self.code,
                                        self.mode, int(overflow_slots), ctypes.byref(h)))
         self._h = h
+        for name, value in (options or {}).items():
+            self.set_option(name, value)
 
     # ------------------------------------------------------------ lifetime
     def close(self):
@@ -179,6 +181,20 @@ class Shard:
                 raise ValueError("device tensors must be contiguous and on the shard's GPU")
 
     # ------------------------------------------------------------ control
+    _GENERAL = {"stamps": 0, "auto": 1, "radix": 2}
+
+    def set_option(self, name: str, value):
+        """pskv_set_option: a tuning / path option of this shard (include/pskv.h).
+        GENERAL also takes "stamps" / "auto" / "radix"; booleans as 0 / 1."""
+        if name == "GENERAL" and isinstance(value, str):
+            value = self._GENERAL[value]
+        check(lib.pskv_set_option(self._h, name.encode(), int(value)))
+
+    def get_option(self, name: str) -> int:
+        v = ctypes.c_int64()
+        check(lib.pskv_get_option(self._h, name.encode(), ctypes.byref(v)))
+        return v.value
+
     def sync(self):
         check(lib.pskv_sync(self._h))
 

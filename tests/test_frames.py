@@ -57,11 +57,11 @@ def _messages(rng, kb, ke, n, count):
 @pytest.mark.parametrize("n", [300, 5000, 70_000, 400_000])
 @pytest.mark.parametrize("mode,dt", [("assign", np.float64), ("assign", np.int32),
                                      ("accumulate", np.float32), ("accumulate", np.int32)])
-def test_frame_add_get_parity(cuda, oracle_mod, mode, dt, n, zc, monkeypatch):
+def test_frame_add_get_parity(cuda, oracle_mod, mode, dt, n, zc):
     import parameter_server_amd as ps
 
-    if zc == "dma":  # every frame call above the inline size DMAs instead of reading in place
-        monkeypatch.setenv("PSKV_FRAME_ZC_MAX_BYTES", "0")
+    # zc "dma": every frame call above the inline size DMAs instead of reading in place
+    opts = {"FRAME_ZC_MAX_BYTES": 0} if zc == "dma" else None
     rng = np.random.default_rng(n + 7)
     kb, ke = 1000, 1000 + 600_000
     keys = _messages(rng, kb, ke, n, 6)
@@ -70,7 +70,7 @@ def test_frame_add_get_parity(cuda, oracle_mod, mode, dt, n, zc, monkeypatch):
     q[:2] = [0xFFFFFFFF, kb]
     res = {}
     for path in ("staged", "frames"):
-        with ps.Shard(kb, ke, dt, mode=mode, overflow_slots=1 << 12) as sh:
+        with ps.Shard(kb, ke, dt, mode=mode, overflow_slots=1 << 12, options=opts) as sh:
             keep = []
             for j, (k, v) in enumerate(zip(keys, vals)):
                 if path == "staged":

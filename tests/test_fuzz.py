@@ -30,9 +30,11 @@ N_SCENARIOS = int(os.environ.get("FUZZ_SCENARIOS", "160"))
 SEED0 = int(os.environ.get("FUZZ_SEED0", "0"))  # first scenario seed (longer runs: new seeds)
 N_STEPS = 18
 N_GROUPS = int(os.environ.get("FUZZ_GROUPS", "4"))  # concurrent groups of 6 shards
-KNOBS = [{}, {}, {}, {"PSKV_SERVE": "1"}, {"PSKV_GENERAL": "stamps"}, {"PSKV_INLINE": "0"},
-         {"PSKV_UNROLL": "4"}, {"PSKV_PAGEABLE_DMA": "1"}, {"PSKV_ZC_MAX_BYTES": "0"},
-         {"PSKV_RB_APPLY_LOG2": "13"}]
+# shard options (pskv_set_option) that route calls through other host or
+# kernel paths; each scenario takes one
+KNOBS = [{}, {}, {}, {"SERVE": 1}, {"GENERAL": "stamps"}, {"INLINE": 0},
+         {"UNROLL": 4}, {"PAGEABLE_DMA": 1}, {"ZC_MAX_BYTES": 0},
+         {"RB_APPLY_LOG2": 13}]
 SIZES = [0, 1, 5, 100, 256, 257, 1024, 2049, 5000, 40_000, 300_000]
 U32 = 1 << 32
 
@@ -123,10 +125,8 @@ def _scenario(seed):
 
 
 @pytest.mark.parametrize("seed", range(SEED0, SEED0 + N_SCENARIOS))
-def test_fuzz_against_oracle(cuda, oracle_mod, seed, monkeypatch):
+def test_fuzz_against_oracle(cuda, oracle_mod, seed):
     rng, dt, mode, kb, ke, knobs = _scenario(seed)
-    for k, v in knobs.items():
-        monkeypatch.setenv(k, v)
     _run(cuda, oracle_mod, seed, rng, dt, mode, kb, ke, knobs)
 
 
@@ -143,8 +143,8 @@ def test_fuzz_concurrent_shards(cuda, oracle_mod, group):
 
     def worker(seed):
         try:
-            rng, dt, mode, kb, ke, _ = _scenario(seed)
-            _run(cuda, oracle_mod, seed, rng, dt, mode, kb, ke, {})
+            rng, dt, mode, kb, ke, knobs = _scenario(seed)  # options are per shard: no races
+            _run(cuda, oracle_mod, seed, rng, dt, mode, kb, ke, knobs)
         except BaseException as e:  # noqa: B902 - re-raised in the main thread
             errs.append(e)
 
@@ -175,7 +175,7 @@ def _run(cuda, oracle_mod, seed, rng, dt, mode, kb, ke, knobs):
         else:
             ref.check(q, got, what)
 
-    with ps.Shard(kb, ke, dt, mode=mode, overflow_slots=1 << 14) as sh:
+    with ps.Shard(kb, ke, dt, mode=mode, overflow_slots=1 << 14, options=knobs) as sh:
         for step in range(N_STEPS):
             op = rng.choice(["add", "add", "add_dev", "add_grouped", "add_grouped_dev",
                              "get", "get_dev", "get_grouped", "clear"],

@@ -644,12 +644,12 @@ def test_grouped_dense_lookalike_is_repaired(cuda, oracle_mod):
 
 @pytest.mark.parametrize("mode,dtype", [("assign", np.float32), ("assign", np.float64),
                                         ("accumulate", np.float64), ("accumulate", np.int32)])
-def test_radix_path_hot_bucket_many_rounds(cuda, oracle_mod, mode, dtype, monkeypatch):
+def test_radix_path_hot_bucket_many_rounds(cuda, oracle_mod, mode, dtype):
     """K5: every key in ONE key bucket (and the out-of-range bucket), far more
     entries than the apply workgroup's LDS table holds -> multi-round apply."""
     import parameter_server_amd as ps
 
-    monkeypatch.setenv("PSKV_GENERAL", "radix")  # K5 for accumulate too
+    opts = {"GENERAL": "radix"}  # K5 for accumulate too
 
     rng = np.random.default_rng(55)
     size = 1 << 25                      # bucket width 64 Ki keys
@@ -666,7 +666,7 @@ def test_radix_path_hot_bucket_many_rounds(cuda, oracle_mod, mode, dtype, monkey
             v = rng.standard_normal(n).astype(dtype)
         batches.append((k, v))
     q = np.unique(np.concatenate([k for k, _ in batches]))
-    with ps.Shard(kb, kb + size, dtype, mode=mode, overflow_slots=1 << 15) as sh:
+    with ps.Shard(kb, kb + size, dtype, mode=mode, overflow_slots=1 << 15, options=opts) as sh:
         sh.add_grouped([(tdev(k, cuda), tdev(v, cuda)) for k, v in batches])
         got = sh.get(q)
         sh.sync()
@@ -903,14 +903,15 @@ def test_radix_path_split_launches(cuda, oracle_mod, dtype):
     assert_bits_equal(got, dense, "split")
 
 
-def test_general_path_stamps_variant_matches(cuda, oracle_mod, monkeypatch):
-    """The K4 stamp path (kept for repairs) as the unhinted general path."""
+def test_general_path_stamps_variant_matches(cuda, oracle_mod):
+    """The K4 stamp path (shard option GENERAL = stamps) as the unhinted
+    general path."""
     import parameter_server_amd as ps
 
-    monkeypatch.setenv("PSKV_GENERAL", "stamps")
     rng = np.random.default_rng(66)
     ref = oracle_mod.MapStorageRef(np.float32)
-    with ps.Shard(0, 500_000, np.float32, overflow_slots=1 << 14) as sh:
+    with ps.Shard(0, 500_000, np.float32, overflow_slots=1 << 14, options={"GENERAL": "stamps"}) as sh:
+        assert sh.get_option("GENERAL") == 0
         for _ in range(4):
             k = rng.integers(0, 520_000, size=90_000).astype(np.uint32)
             v = rng.standard_normal(k.size).astype(np.float32)
@@ -922,16 +923,16 @@ def test_general_path_stamps_variant_matches(cuda, oracle_mod, monkeypatch):
 
 
 @pytest.mark.parametrize("dtype", [np.int32, np.float32])
-def test_accumulate_stamps_variant_k4a(cuda, monkeypatch, dtype):
+def test_accumulate_stamps_variant_k4a(cuda, dtype):
     """K4a accumulate (LDS chunk sums + one atomic add per distinct key per
-    chunk), selected by PSKV_GENERAL=stamps: int32 exact, float within bound."""
+    chunk), selected by the shard option GENERAL = stamps: int32 exact, float
+    within bound."""
     import parameter_server_amd as ps
 
-    monkeypatch.setenv("PSKV_GENERAL", "stamps")
     rng = np.random.default_rng(67)
     size = 300_000
     p64, a64, cnt = np.zeros(size), np.zeros(size), np.zeros(size, np.int64)
-    with ps.Shard(0, size, dtype, mode="accumulate") as sh:
+    with ps.Shard(0, size, dtype, mode="accumulate", options={"GENERAL": "stamps"}) as sh:
         for _ in range(3):
             k = (rng.zipf(1.3, size=120_000) % size).astype(np.uint32)
             v = (rng.integers(-1000, 1000, size=k.size).astype(np.int32) if dtype is np.int32
@@ -961,7 +962,7 @@ def _pinned(a):
 @pytest.mark.parametrize("pinned_path", ["dma", "default"])
 @pytest.mark.parametrize("pageable_path", ["dma", "staged"])
 @pytest.mark.parametrize("mode", ["assign", "accumulate"])
-def test_pinned_host_buffers_direct_dma(cuda, oracle_mod, mode, pageable_path, pinned_path, monkeypatch):
+def test_pinned_host_buffers_direct_dma(cuda, oracle_mod, mode, pageable_path, pinned_path):
     """Page-locked caller buffers (the zmq frames after the SURVEY §8f-3 mailbox
     change): same results as pageable buffers, for sorted, dense and unsorted
     batches, Add and Get.  pinned_path "dma": Adds and Gets DMA'd directly
@@ -969,15 +970,12 @@ def test_pinned_host_buffers_direct_dma(cuda, oracle_mod, mode, pageable_path, p
     copy and Gets up to 8 MiB run K1 on them in place (zero copy)."""
     import parameter_server_amd as ps
 
+    opts = {}
     if pinned_path == "dma":
-        monkeypatch.setenv("PSKV_DMA_MIN_BYTES_PINNED", "0")
-        monkeypatch.setenv("PSKV_FRAME_ZC_MAX_BYTES", "0")
-
+        opts.update(DMA_MIN_BYTES_PINNED=0, FRAME_ZC_MAX_BYTES=0)
     # pageable buffers go by direct DMA (forced at every size: by default only
     # calls of >= 32 MiB (Add) / 32 KiB (Get) do) or through pinned staging
-    monkeypatch.setenv("PSKV_PAGEABLE_DMA", "1" if pageable_path == "dma" else "0")
-    monkeypatch.setenv("PSKV_DMA_MIN_BYTES", "0")
-    monkeypatch.setenv("PSKV_DMA_MIN_BYTES_GET", "0")
+    opts.update(PAGEABLE_DMA=1 if pageable_path == "dma" else 0, DMA_MIN_BYTES=0, DMA_MIN_BYTES_GET=0)
     rng = np.random.default_rng(71)
     kb, size = 10, 400_000
     batches = []
@@ -994,7 +992,7 @@ def test_pinned_host_buffers_direct_dma(cuda, oracle_mod, mode, pageable_path, p
     q = np.arange(0, kb + size + 1000, dtype=np.uint32)
     outs = {}
     for kind in ("pageable", "pinned"):
-        with ps.Shard(kb, kb + size, np.float64, mode=mode, overflow_slots=1 << 14) as sh:
+        with ps.Shard(kb, kb + size, np.float64, mode=mode, overflow_slots=1 << 14, options=opts) as sh:
             bb = batches if kind == "pageable" else [(_pinned(k), _pinned(v)) for k, v in batches]
             sh.add_grouped(bb[:3])
             for k, v in bb[3:]:
@@ -1035,7 +1033,7 @@ def _small_messages(rng, kb, ke, count, max_n=256):
 
 
 @pytest.mark.parametrize("dt", [np.int32, np.float32, np.float64])
-def test_inline_small_messages_assign(cuda, oracle_mod, dt, monkeypatch):
+def test_inline_small_messages_assign(cuda, oracle_mod, dt):
     """K8 assign: last write wins within and across messages, missing keys 0,
     overflow keys kept; the same message stream through the staged path
     (PSKV_INLINE=0) gives the same bits."""
@@ -1047,10 +1045,8 @@ def test_inline_small_messages_assign(cuda, oracle_mod, dt, monkeypatch):
     msgs = _small_messages(rng, kb, ke, 120)
     vals = [(rng.standard_normal(k.size) * 100).astype(dt) for k in msgs]
     ref = oracle_mod.MapStorageRef(dt)
-    monkeypatch.setenv("PSKV_INLINE", "0")
-    staged = ps.Shard(kb, ke, dt, overflow_slots=64)
+    staged = ps.Shard(kb, ke, dt, overflow_slots=64, options={"INLINE": 0})
     staged.set_timing(True)
-    monkeypatch.delenv("PSKV_INLINE")
     try:
         with ps.Shard(kb, ke, dt, overflow_slots=64) as sh:
             sh.set_timing(True)
@@ -1080,19 +1076,19 @@ def test_inline_small_messages_assign(cuda, oracle_mod, dt, monkeypatch):
 
 @pytest.mark.parametrize("max_n,chunks", [(256, "1"), (2048, "8")])
 @pytest.mark.parametrize("dt", [np.int32, np.float32, np.float64])
-def test_inline_accumulate_sequential_bits(cuda, dt, max_n, chunks, monkeypatch):
+def test_inline_accumulate_sequential_bits(cuda, dt, max_n, chunks):
     """K8 accumulate: the first occurrence of a key adds every occurrence in
     index order, so the result equals sequential accumulation in the value
     dtype BIT FOR BIT (np.add.at), overflow keys included."""
     import parameter_server_amd as ps
 
-    monkeypatch.setenv("PSKV_INLINE_ADD_CHUNKS", chunks)  # 8: messages of up to 8 launches
     rng = np.random.default_rng(909)
     kb, ke = 0, 2048
     msgs = _small_messages(rng, kb, ke, 80, max_n=max_n)
     want = np.zeros(ke - kb, dt)
     want_ovf = {}
-    with ps.Shard(kb, ke, dt, mode="accumulate", overflow_slots=64) as sh:
+    # INLINE_ADD_CHUNKS 8: messages of up to 8 launches
+    with ps.Shard(kb, ke, dt, mode="accumulate", overflow_slots=64, options={"INLINE_ADD_CHUNKS": int(chunks)}) as sh:
         for k in msgs:
             v = (rng.integers(-2**31, 2**31 - 1, size=k.size, dtype=np.int64).astype(np.int32)
                  if dt is np.int32 else rng.standard_normal(k.size).astype(dt))
@@ -1146,16 +1142,15 @@ def test_inline_size_boundaries(cuda, oracle_mod, n):
 
 
 @pytest.mark.parametrize("spin", ["1", "0"])
-def test_inline_get_reply_paths(cuda, oracle_mod, spin, monkeypatch):
+def test_inline_get_reply_paths(cuda, oracle_mod, spin):
     """The inline Get's two completion forms: the polled sequence word the
     kernel publishes after its reply (default) and a plain stream wait
     (PSKV_ISPIN=0); with timing on, the polled form is bypassed too."""
     import parameter_server_amd as ps
 
-    monkeypatch.setenv("PSKV_ISPIN", spin)
     rng = np.random.default_rng(11)
     ref = oracle_mod.MapStorageRef(np.float32)
-    with ps.Shard(0, 1 << 16, np.float32) as sh:
+    with ps.Shard(0, 1 << 16, np.float32, options={"ISPIN": int(spin)}) as sh:
         for i in range(300):
             k = rng.integers(0, 1 << 17, size=int(rng.integers(1, 300))).astype(np.uint32)
             v = rng.standard_normal(k.size).astype(np.float32)
@@ -1207,7 +1202,7 @@ def test_batch_beyond_2_to_32_elements(cuda):
 
 
 @pytest.mark.parametrize("n", [1025, 1500, 4096, 8193, 70_000, 120_000])
-def test_zero_copy_get_sizes(cuda, oracle_mod, n, monkeypatch):
+def test_zero_copy_get_sizes(cuda, oracle_mod, n):
     """Medium pageable host Gets (past the inline size, <= 1 MiB of keys and
     values) run K1 over pinned staging: the keys read and the values written
     across PCIe by the kernel.  Partial chunks, unaligned sizes, missing and
@@ -1225,9 +1220,8 @@ def test_zero_copy_get_sizes(cuda, oracle_mod, n, monkeypatch):
     q[:3] = [0xFFFFFFFF, ke + 2999, kb]
     res = {}
     for zc in ("default", "0"):
-        if zc == "0":
-            monkeypatch.setenv("PSKV_ZC_MAX_BYTES", "0")
-        with ps.Shard(kb, ke, np.float64, overflow_slots=1 << 16) as sh:
+        with ps.Shard(kb, ke, np.float64, overflow_slots=1 << 16,
+                      options={"ZC_MAX_BYTES": 0} if zc == "0" else None) as sh:
             sh.add(k, v)
             parts = np.array_split(q, 3)
             outs = [np.empty(p.size) for p in parts]
@@ -1296,3 +1290,35 @@ def test_c_abi_error_paths_leave_the_shard_usable(cuda, oracle_mod):
         assert L.pskv_shard_create(*args, ctypes.byref(hh)) == _lib.PSKV_EINVAL, args
         assert msg in L.pskv_last_error(), (args, L.pskv_last_error())
     ref.close()
+
+
+def test_shard_options_api(cuda):
+    """pskv_set_option / pskv_get_option: every option by name, round trip,
+    unknown names and out-of-range values rejected with PSKV_EINVAL (the shard
+    unchanged), the environment as the creation default."""
+    import parameter_server_amd as ps
+    from parameter_server_amd import PskvError, _lib
+
+    names = ["GENERAL", "UNROLL", "NT", "NTP", "PAGEABLE_DMA", "DMA_MIN_BYTES", "DMA_MIN_BYTES_GET",
+             "DMA_MIN_BYTES_PINNED", "ZC_MAX_BYTES", "FRAME_ZC_MAX_BYTES", "INLINE", "INLINE_ADD_CHUNKS",
+             "INLINE_GET_CHUNKS", "ISPIN", "SERVE", "SERVE_IDLE_US", "TILE_SHIFT", "TILE_GRID", "RB_WBITS",
+             "RB_NBD", "RB_TB", "RB_APPLY_LOG2"]
+    with ps.Shard(0, 1000, np.float32) as sh:
+        for n in names:
+            sh.set_option(n, sh.get_option(n))  # every default is a valid value
+        sh.set_option("GENERAL", "stamps")
+        assert sh.get_option("GENERAL") == 0
+        sh.set_option("SERVE", 1)
+        assert sh.get_option("INLINE_ADD_CHUNKS") == 2  # the server's small-Add default
+        sh.set_option("ZC_MAX_BYTES", 12345)
+        assert sh.get_option("ZC_MAX_BYTES") == 12345
+        for n, bad in (("UNROLL", 5), ("RB_APPLY_LOG2", 12), ("TILE_SHIFT", 3), ("INLINE", 2), ("NOPE", 1)):
+            before = sh.get_option(n) if n != "NOPE" else None
+            with pytest.raises(PskvError) as ei:
+                sh.set_option(n, bad)
+            assert ei.value.code == _lib.PSKV_EINVAL
+            if before is not None:
+                assert sh.get_option(n) == before
+        k = np.arange(100, dtype=np.uint32)
+        sh.add(k, k.astype(np.float32))
+        assert np.array_equal(sh.get(k), k.astype(np.float32))

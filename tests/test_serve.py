@@ -18,9 +18,9 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture
-def serve(monkeypatch):
-    monkeypatch.setenv("PSKV_SERVE", "1")
-    return monkeypatch
+def serve():
+    """The shard options that turn the request server on."""
+    return {"SERVE": 1}
 
 
 @pytest.mark.parametrize("dt", [np.int32, np.float32, np.float64])
@@ -35,7 +35,7 @@ def test_serve_messages_assign(cuda, oracle_mod, dt, serve):
     msgs = _small_messages(rng, kb, ke, 150)
     ref = oracle_mod.MapStorageRef(dt)
     checks = []
-    with ps.Shard(kb, ke, dt, overflow_slots=64) as sh:
+    with ps.Shard(kb, ke, dt, overflow_slots=64, options=serve) as sh:
         for i, k in enumerate(msgs):
             v = (rng.standard_normal(k.size) * 100).astype(dt)
             sh.add(k, v)
@@ -69,7 +69,7 @@ def test_serve_accumulate_sequential_bits(cuda, dt, serve):
     msgs = _small_messages(rng, kb, ke, 120)
     want = np.zeros(ke - kb, dt)
     want_ovf = {}
-    with ps.Shard(kb, ke, dt, mode="accumulate", overflow_slots=64) as sh:
+    with ps.Shard(kb, ke, dt, mode="accumulate", overflow_slots=64, options=serve) as sh:
         for k in msgs:
             v = (rng.integers(-2**31, 2**31 - 1, size=k.size, dtype=np.int64).astype(np.int32)
                  if dt is np.int32 else rng.standard_normal(k.size).astype(dt))
@@ -92,10 +92,10 @@ def test_serve_idle_restart_and_ring_wrap(cuda, oracle_mod, serve):
     ring (64 slots) wrap it."""
     import parameter_server_amd as ps
 
-    serve.setenv("PSKV_SERVE_IDLE_US", "50")
+    serve = dict(serve, SERVE_IDLE_US=50)
     rng = np.random.default_rng(5)
     ref = oracle_mod.MapStorageRef(np.float32)
-    with ps.Shard(0, 10_000, np.float32) as sh:
+    with ps.Shard(0, 10_000, np.float32, options=serve) as sh:
         for i in range(40):
             for _ in range(int(rng.integers(1, 150))):  # a burst of Adds, up to 2+ ring laps
                 k = rng.integers(0, 10_000, size=int(rng.integers(1, 40))).astype(np.uint32)
@@ -116,7 +116,7 @@ def test_serve_overflow_growth(cuda, oracle_mod, serve):
 
     rng = np.random.default_rng(17)
     ref = oracle_mod.MapStorageRef(np.float64)
-    with ps.Shard(0, 1000, np.float64, overflow_slots=64) as sh:
+    with ps.Shard(0, 1000, np.float64, overflow_slots=64, options=serve) as sh:
         for _ in range(200):
             k = rng.integers(0, 200_000, size=200).astype(np.uint32)
             v = rng.standard_normal(k.size)
@@ -141,7 +141,7 @@ def test_serve_several_shards_one_device(cuda, oracle_mod, serve, nshards):
     import parameter_server_amd as ps
 
     rng = np.random.default_rng(8)
-    shards = [ps.Shard(s * 1000, (s + 1) * 1000, np.float64) for s in range(nshards)]
+    shards = [ps.Shard(s * 1000, (s + 1) * 1000, np.float64, options=serve) for s in range(nshards)]
     refs = [oracle_mod.MapStorageRef(np.float64) for _ in shards]
     try:
         for i in range(400):
