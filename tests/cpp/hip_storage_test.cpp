@@ -298,5 +298,8 @@ int main(int argc, char** argv) {
     CreateTableHip();
   }
   std::printf("%d passed, %d failed\n", g_pass, g_fail);
+  // every shard is gone; hand the cached page-locked frames back while the HIP
+  // runtime is still up (not from a static destructor at exit)
+  if (!host_only) (void)pskv_host_pool_trim();
   return g_fail ? 1 : 0;
 }

@@ -460,5 +460,8 @@ int main(int argc, char** argv) {
   System(ModelType::SSP, "SSP", st, /*hashed=*/true);
   System(ModelType::BSP, "BSP", st, /*hashed=*/true);
   std::printf("%d passed, %d failed\n", g_pass.load(), g_fail.load());
+  // every shard is gone; hand the cached page-locked frames back while the HIP
+  // runtime is still up (not from a static destructor at exit)
+  if (st == StorageType::Hip) (void)pskv_host_pool_trim();
   return g_fail.load() ? 1 : 0;
 }

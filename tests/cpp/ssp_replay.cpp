@@ -742,5 +742,8 @@ int main(int argc, char** argv) {
               (unsigned long long)ref.clocks, (unsigned long long)ref.echoes, ref.log.size());
   std::printf("cpu %.3f s, %s %.3f s\n", ref.seconds, c.cpu_only ? "cpu" : "hip", other.seconds);
   std::printf("%s%s\n", ok ? "REPLAY OK (bit-exact)" : "REPLAY MISMATCH: ", ok ? "" : why.c_str());
+  // every shard is gone (the Replay objects and models above own them); hand
+  // the cached page-locked frames back while the HIP runtime is still up
+  if (!c.cpu_only) (void)pskv_host_pool_trim();
   return ok && fails == 0 ? 0 : 1;
 }
