@@ -265,9 +265,26 @@ __device__ __forceinline__ void gather2(const DenseView& d, const Ovf& o, const 
   }
 }
 
-template <typename VT, bool VEC, int U, bool NT>
+// Pull-key dedup (K1, 4-byte values, DEDUP): a chunk of scattered keys — a
+// Zipf pull repeats its hot keys many times (cfg 3: ~30 % of an 8 Ki-key
+// chunk's keys are repeats) — gathers each distinct key once.  Every scattered
+// key claims a slot of a direct-mapped LDS table, (key, element id) written as
+// one 8-byte store (the last writer of a slot owns it); the owners gather and
+// publish their values in LDS; the other elements with the owner's key read
+// the value from LDS; keys whose slot another key took gather themselves.
+// No atomics, no clearing (a slot is read only by the elements that wrote it),
+// two workgroup barriers.  Chunks whose groups are all runs (dense pulls)
+// skip it after one barrier.  18 KiB of LDS keeps 8 workgroups per CU.
+constexpr uint32_t kDedupSlots = 1536;
+__device__ __forceinline__ uint32_t dedup_slot(uint32_t key) {
+  return __umulhi(fmix32(key), kDedupSlots);
+}
+
+template <typename VT, bool VEC, int U, bool NT, bool DEDUP>
 __global__ __launch_bounds__(kBlock) void k_gather(GroupArgs ga, DenseView d, Ovf o) {
   constexpr int CH = kBlock * 4 * U;
+  __shared__ unsigned long long s_ent[DEDUP ? kDedupSlots : 1];  // key | element id << 32
+  __shared__ VT s_val[DEDUP ? kDedupSlots : 1];
   const uint32_t wg = blockIdx.x;
   const int j = batch_of(ga, wg);
   const uint32_t* __restrict__ keys = ga.b[j].keys;
@@ -299,8 +316,65 @@ __global__ __launch_bounds__(kBlock) void k_gather(GroupArgs ga, DenseView d, Ov
     for (int u = 0; u < U; ++u)
       Vec4<uint32_t>::load<NT>(keys + base + (uint64_t)(u * kBlock + tid) * 4, k[u]);
     VT v[U][4];
+    bool dedup = false;
+    if constexpr (DEDUP && sizeof(VT) == 4) {
+      static_assert(U * 4 <= 32, "one mask bit per element of a lane");
+      uint32_t runs = 0;  // bit u: group u is four consecutive in-range keys
 #pragma unroll
-    for (int u = 0; u < U; ++u) gather4<VT>(d, o, k[u], v[u]);
+      for (int u = 0; u < U; ++u) {
+        const uint32_t off0 = k[u][0] - d.key_begin;
+        const bool run = (k[u][1] == k[u][0] + 1u) & (k[u][2] == k[u][0] + 2u) &
+                         (k[u][3] == k[u][0] + 3u) & ((uint64_t)off0 + 3u < d.range);
+        runs |= run ? (1u << u) : 0u;
+      }
+      dedup = __syncthreads_or(runs != (1u << U) - 1u) != 0;
+      if (dedup) {
+        // claim: every scattered element writes (key, its id) into its slot
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (runs >> u & 1u) continue;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            s_ent[dedup_slot(k[u][e])] =
+                (unsigned long long)k[u][e] | ((unsigned long long)(tid * 32 + u * 4 + e) << 32);
+        }
+        __syncthreads();
+        // owners and slot losers gather; the other holders of an owned key wait
+        uint32_t waits = 0, owns = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (runs >> u & 1u) {
+            gather4<VT>(d, o, k[u], v[u]);
+            continue;
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const unsigned long long ent = s_ent[dedup_slot(k[u][e])];
+            const bool same = (uint32_t)ent == k[u][e];
+            const bool own = same && (uint32_t)(ent >> 32) == (uint32_t)(tid * 32 + u * 4 + e);
+            const uint32_t bit = 1u << (u * 4 + e);
+            waits |= same && !own ? bit : 0u;
+            owns |= own ? bit : 0u;
+            v[u][e] = same && !own ? VT(0) : load_one<VT>(d, o, k[u][e]);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (owns >> (u * 4 + e) & 1u) s_val[dedup_slot(k[u][e])] = v[u][e];
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (waits >> (u * 4 + e) & 1u) v[u][e] = s_val[dedup_slot(k[u][e])];
+      }
+    }
+    if (!dedup) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) gather4<VT>(d, o, k[u], v[u]);
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u)
       Vec4<VT>::template store<NT>(out + base + (uint64_t)(u * kBlock + tid) * 4, v[u]);
@@ -2222,27 +2296,29 @@ __global__ __launch_bounds__(kInlineMax) void k_serve(SrvRing* ring, DenseView d
 
 // ------------------------------------------------------- launch wrappers
 
-template <typename VT, bool VEC>
+template <typename VT, bool VEC, bool DEDUP = false>
 static void gather_dispatch(int unroll, bool nt, uint32_t nwg, const GroupArgs& ga,
                             const DenseView& d, const Ovf& o, hipStream_t st) {
   if (unroll == 8) {
     if (nt)
-      k_gather<VT, VEC, 8, true><<<nwg, kBlock, 0, st>>>(ga, d, o);
+      k_gather<VT, VEC, 8, true, DEDUP><<<nwg, kBlock, 0, st>>>(ga, d, o);
     else
-      k_gather<VT, VEC, 8, false><<<nwg, kBlock, 0, st>>>(ga, d, o);
+      k_gather<VT, VEC, 8, false, DEDUP><<<nwg, kBlock, 0, st>>>(ga, d, o);
   } else {
     if (nt)
-      k_gather<VT, VEC, 4, true><<<nwg, kBlock, 0, st>>>(ga, d, o);
+      k_gather<VT, VEC, 4, true, DEDUP><<<nwg, kBlock, 0, st>>>(ga, d, o);
     else
-      k_gather<VT, VEC, 4, false><<<nwg, kBlock, 0, st>>>(ga, d, o);
+      k_gather<VT, VEC, 4, false, DEDUP><<<nwg, kBlock, 0, st>>>(ga, d, o);
   }
 }
 
-hipError_t launch_gather(int vb, bool vec, int unroll, bool nt, const GroupArgs& ga, uint32_t nwg,
+hipError_t launch_gather(int vb, bool vec, int unroll, bool nt, bool dedup, const GroupArgs& ga, uint32_t nwg,
                          const DenseView& d, const Ovf& o, hipStream_t st) {
   if (nwg == 0) return hipSuccess;
   if (vb == 4) {
-    if (vec)
+    if (vec && dedup)
+      gather_dispatch<uint32_t, true, true>(unroll, nt, nwg, ga, d, o, st);
+    else if (vec)
       gather_dispatch<uint32_t, true>(unroll, nt, nwg, ga, d, o, st);
     else
       gather_dispatch<uint32_t, false>(unroll, nt, nwg, ga, d, o, st);

@@ -252,6 +252,7 @@ struct pskv_shard {
   int tune_unroll = 8;   // PSKV_UNROLL: 4 or 8 (8: measured +5 % on the dense Add)
   bool tune_nt = true;   // PSKV_NT: non-temporal streams (measured +12-15 % on K1 / K2g)
   bool tune_ntp = false; // PSKV_NTP: non-temporal parameter stores (dense Add)
+  bool tune_get_dedup = false;  // GET_DEDUP: K1 gathers each distinct scattered pull key once per chunk
   // PSKV_PAGEABLE_DMA: DMA pageable host buffers directly (the runtime moves
   // them at the PCIe rate, measured 55 GB/s) instead of copying them into
   // pinned staging first; 0 selects the staging path.  cfg-2-shaped Add of
@@ -315,6 +316,10 @@ struct pskv_shard {
 };
 
 namespace {
+
+// K1's keys per lane group: the pull-key dedup variant runs 4 groups per lane
+// (its LDS barriers hold every group's keys and values: 8 groups took 126 VGPRs)
+int gather_unroll(const pskv_shard* s) { return s->tune_get_dedup && s->vb == 4 ? 4 : s->tune_unroll; }
 
 int use_device(pskv_shard* s) {
   PSKV_HIP(hipSetDevice(s->device));
@@ -1451,11 +1456,11 @@ int zero_copy_get_views(pskv_shard* s, const std::vector<pskv_batch>& hv) {
   for (auto& b : hv) vec &= aligned16(b.keys) & aligned16(b.vals);
   for (auto& g : split_groups(hv)) {
     GroupArgs ga;
-    const uint32_t nwg = build_group(hv, g.first, g.second, stream_chunk(s->tune_unroll), &ga);
+    const uint32_t nwg = build_group(hv, g.first, g.second, stream_chunk(gather_unroll(s)), &ga);
     uint64_t elems = 0;
     for (size_t i = g.first; i < g.second; ++i) elems += hv[i].n;
     LaunchTimer t(s, PSKV_K_GATHER, elems);
-    PSKV_HIP(launch_gather(s->vb, vec, s->tune_unroll, s->tune_nt, ga, nwg, s->dview(), s->ovf, s->stream));
+    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, s->tune_get_dedup, ga, nwg, s->dview(), s->ovf, s->stream));
     t.done();
   }
   PSKV_HIP(hipStreamSynchronize(s->stream));
@@ -1482,11 +1487,11 @@ int zero_copy_get(pskv_shard* s, const std::vector<pskv_batch>& v, bool vec) {
   }
   for (auto& g : split_groups(hv)) {
     GroupArgs ga;
-    const uint32_t nwg = build_group(hv, g.first, g.second, stream_chunk(s->tune_unroll), &ga);
+    const uint32_t nwg = build_group(hv, g.first, g.second, stream_chunk(gather_unroll(s)), &ga);
     uint64_t elems = 0;
     for (size_t i = g.first; i < g.second; ++i) elems += hv[i].n;
     LaunchTimer t(s, PSKV_K_GATHER, elems);
-    PSKV_HIP(launch_gather(s->vb, vec, s->tune_unroll, s->tune_nt, ga, nwg, s->dview(), s->ovf, s->stream));
+    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, s->tune_get_dedup, ga, nwg, s->dview(), s->ovf, s->stream));
     t.done();
   }
   PSKV_HIP(hipStreamSynchronize(s->stream));
@@ -1583,11 +1588,11 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
   for (auto& b : dv) vec &= aligned16(b.keys) & aligned16(b.vals);
   for (auto& g : split_groups(dv)) {
     GroupArgs ga;
-    const uint32_t nwg = build_group(dv, g.first, g.second, stream_chunk(s->tune_unroll), &ga);
+    const uint32_t nwg = build_group(dv, g.first, g.second, stream_chunk(gather_unroll(s)), &ga);
     uint64_t elems = 0;
     for (size_t i = g.first; i < g.second; ++i) elems += dv[i].n;
     LaunchTimer t(s, PSKV_K_GATHER, elems);
-    PSKV_HIP(launch_gather(s->vb, vec, s->tune_unroll, s->tune_nt, ga, nwg, s->dview(), s->ovf,
+    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, s->tune_get_dedup, ga, nwg, s->dview(), s->ovf,
                            s->stream));
     t.done();
   }
@@ -1668,6 +1673,7 @@ const Option kOptions[] = {
     PSKV_OPT("UNROLL", 4, 8, tune_unroll, int),              // 4 or 8 (others: 8)
     PSKV_OPT("NT", 0, 1, tune_nt, bool),
     PSKV_OPT("NTP", 0, 1, tune_ntp, bool),
+    PSKV_OPT("GET_DEDUP", 0, 1, tune_get_dedup, bool),
     PSKV_OPT("PAGEABLE_DMA", 0, 1, tune_pageable_dma, bool),
     PSKV_OPT("DMA_MIN_BYTES", 0, INT64_MAX, tune_dma_min_bytes, size_t),
     PSKV_OPT("DMA_MIN_BYTES_GET", 0, INT64_MAX, tune_dma_min_bytes_get, size_t),

@@ -414,6 +414,42 @@ def test_zipf_batches_parity(cuda, oracle_mod):
     assert_bits_equal(got, dense, "zipf")
 
 
+@pytest.mark.parametrize("dedup", [0, 1])
+def test_zipf_pulls_dedup(cuda, oracle_mod, dedup):
+    """K1 with and without the per-chunk pull-key dedup (option GET_DEDUP):
+    Zipf pulls (hot keys repeated hundreds of times per chunk), out-of-range
+    keys, the sentinel 0xFFFFFFFF, never-written keys, and chunks that mix dense
+    runs with scattered keys — bit-exact against the oracle."""
+    import torch
+
+    import parameter_server_amd as ps
+    from parameter_server_amd import workload
+
+    space = 2_000_000
+    zb = workload.zipf_batches(3, space, batch=300_000, device=cuda)
+    ref = oracle_mod.MapStorageRef(np.float32)
+    with ps.Shard(0, space, np.float32, overflow_slots=1 << 12, options={"GET_DEDUP": dedup}) as sh:
+        for k, v in zb:
+            sh.add(k, v)
+            ref.add(k.cpu().numpy().view(np.uint32), v.cpu().numpy())
+        extra = np.array([0xFFFFFFFF, space + 5, space + 5, 2**31 + 9], np.uint32)
+        xv = np.arange(4, dtype=np.float32) + 0.5
+        sh.add(extra, xv)
+        ref.add(extra, xv)
+        q = zb[0][0].cpu().numpy().view(np.uint32).copy()
+        q[1000:1000 + 64] = np.arange(5000, 5064, dtype=np.uint32)       # dense runs inside scattered chunks
+        q[7:40] = 0xFFFFFFFF
+        q[50:60] = space + 5
+        q[-9:] = np.arange(space + 100, space + 109, dtype=np.uint32)     # never written: 0
+        outs = [torch.empty(q.size // 2, dtype=torch.float32, device=cuda),
+                torch.empty(q.size - q.size // 2, dtype=torch.float32, device=cuda)]
+        parts = [tdev(q[:q.size // 2], cuda), tdev(q[q.size // 2:], cuda)]
+        sh.get_grouped(list(zip(parts, outs)))
+        got = torch.cat(outs).cpu().numpy()
+        assert sh.get_option("GET_DEDUP") == dedup
+    assert_bits_equal(got, ref.get(q), f"zipf pulls, dedup {dedup}")
+
+
 @pytest.mark.parametrize("mode", ["assign", "accumulate"])
 def test_cfg3_full_size_zipf_parity(cuda, oracle_mod, mode):
     """cfg 3 at its stated size: a 1e8-key float shard, 8 x 1M unsorted
@@ -1299,7 +1335,7 @@ def test_shard_options_api(cuda):
     import parameter_server_amd as ps
     from parameter_server_amd import PskvError, _lib
 
-    names = ["GENERAL", "UNROLL", "NT", "NTP", "PAGEABLE_DMA", "DMA_MIN_BYTES", "DMA_MIN_BYTES_GET",
+    names = ["GENERAL", "UNROLL", "NT", "NTP", "GET_DEDUP", "PAGEABLE_DMA", "DMA_MIN_BYTES", "DMA_MIN_BYTES_GET",
              "DMA_MIN_BYTES_PINNED", "ZC_MAX_BYTES", "FRAME_ZC_MAX_BYTES", "INLINE", "INLINE_ADD_CHUNKS",
              "INLINE_GET_CHUNKS", "ISPIN", "SERVE", "SERVE_IDLE_US", "TILE_SHIFT", "TILE_GRID", "RB_WBITS",
              "RB_NBD", "RB_TB", "RB_APPLY_LOG2"]
@@ -1308,8 +1344,8 @@ def test_shard_options_api(cuda):
             sh.set_option(n, sh.get_option(n))  # every default is a valid value
         sh.set_option("GENERAL", "stamps")
         assert sh.get_option("GENERAL") == 0
-        sh.set_option("SERVE", 1)
-        assert sh.get_option("INLINE_ADD_CHUNKS") == 2  # the server's small-Add default
+        sh.set_option("SERVE", 1)  # INLINE_ADD_CHUNKS was set explicitly above: it stays
+        assert sh.get_option("INLINE_ADD_CHUNKS") == 1
         sh.set_option("ZC_MAX_BYTES", 12345)
         assert sh.get_option("ZC_MAX_BYTES") == 12345
         for n, bad in (("UNROLL", 5), ("RB_APPLY_LOG2", 12), ("TILE_SHIFT", 3), ("INLINE", 2), ("NOPE", 1)):
@@ -1322,3 +1358,5 @@ def test_shard_options_api(cuda):
         k = np.arange(100, dtype=np.uint32)
         sh.add(k, k.astype(np.float32))
         assert np.array_equal(sh.get(k), k.astype(np.float32))
+    with ps.Shard(0, 1000, np.float32, options={"SERVE": 1}) as sh:
+        assert sh.get_option("INLINE_ADD_CHUNKS") == 2  # the server's small-Add default

@@ -17,7 +17,7 @@ for step in "$@"; do
   case $step in
     tests_focus) timeout -k 10 300 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread \
         "$R/tests/test_gpu_parity.py" "$R/tests/test_replay.py" \
-        -k "phase or dense or lookalike or repaired or hint or golden or replay or options" > "$OUT/tests_focus.log" 2>&1 ;;
+        -k "phase or dense or lookalike or repaired or hint or golden or replay or options or dedup or zipf" > "$OUT/tests_focus.log" 2>&1 ;;
     tests_all) timeout -k 10 900 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread "$R/tests" -m gpu \
         > "$OUT/tests_all.log" 2>&1 ;;
     align) timeout -k 10 200 python3 "$R/tools/align_probe.py" 0,1,2,3 20 > "$OUT/align.log" 2>&1 ;;
@@ -26,7 +26,7 @@ for step in "$@"; do
          PSKV_BENCH_EMULATE=0/2 timeout -k 10 200 python3 "$R/bench.py" --steps 20 --no-zipf --no-cpu-baseline --no-extra \
            > "$OUT/emu02.json" 2> "$OUT/emu02.err" ;;
     bench) timeout -k 10 400 python3 "$R/bench.py" --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
-    zipf) timeout -k 10 300 python3 "$R/tools/zipf_probe.py" > "$OUT/zipf.log" 2>&1 ;;
+    zipf) timeout -k 10 300 python3 "$R/tools/zipf_probe.py" "" "PSKV_GET_DEDUP=1" > "$OUT/zipf.log" 2>&1 ;;
     *) echo "unknown step $step"; exit 9 ;;
   esac
   rc=$?
