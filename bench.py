@@ -4,7 +4,7 @@ One step = one pass of the hot path over one push set and one pull set: a
 grouped Add of the step's push batches, then a grouped Get of the batches the
 NEXT step will push — the parameter-server worker loop, pipelined: push this
 round's parameters, pull the ones the next round updates.  Consecutive steps
-rotate over R window sets (--sets, default 4; set r drawn with seed
+rotate over R window sets (--sets, default 16; set r drawn with seed
 set_seed(r), set 0 being the config's own seed).  The Get therefore reads
 parameters the step did not just write (the windows both sets share aside), and
 a step touches more than 256 MB of parameters (push set ∪ pull set, reported as
@@ -70,7 +70,9 @@ def parse(argv=None):
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--batches", type=int, default=64, help="push batches (N=1) / producer streams (N>1) per step")
     p.add_argument("--batch-keys", type=int, default=1_000_000)
-    p.add_argument("--sets", type=int, default=4, help="window sets rotated over the steps")
+    p.add_argument("--sets", type=int, default=16,
+                   help="window sets rotated over the steps (producers push new windows every step; at N > 1 "
+                        "more sets also even out the ranks' shares over the timed steps)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extra", action="store_true", help="skip the side measurements (e2e, f64, accumulate)")
     p.add_argument("--no-zipf", action="store_true", help="skip the cfg-3 sparse (Zipf) measurement")

@@ -7,6 +7,7 @@
 #   emu          bench.py as rank 0 of 8 and of 2 (one rank's cfg-4 share alone)
 #   bench        bench.py --steps 20 (the driver's command line)
 #   zipf         tools/zipf_probe.py kernel times on cfg 3
+#   profile      tools/gpu_profile.sh: rocprofv3 kernel trace + stats, FETCH / WRITE PMC passes
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$PWD}
 OUT=$R/gpurun_out/$1
@@ -26,6 +27,7 @@ for step in "$@"; do
          PSKV_BENCH_EMULATE=0/2 timeout -k 10 200 python3 "$R/bench.py" --steps 20 --no-zipf --no-cpu-baseline --no-extra \
            > "$OUT/emu02.json" 2> "$OUT/emu02.err" ;;
     bench) timeout -k 10 400 python3 "$R/bench.py" --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
+    profile) bash "$R/tools/gpu_profile.sh" "$(basename "$OUT")/prof" > "$OUT/profile.log" 2>&1 ;;
     zipf) timeout -k 10 300 python3 "$R/tools/zipf_probe.py" "" "PSKV_GET_DEDUP=1" > "$OUT/zipf.log" 2>&1 ;;
     *) echo "unknown step $step"; exit 9 ;;
   esac

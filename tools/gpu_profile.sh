@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 OUT=$R/gpurun_out/${1:-prof}
 shift || true
 mkdir -p "$OUT"
-ARGS="--steps 10 --warmup 2 --no-cpu-baseline --no-extra --no-zipf $*"
+ARGS="--steps 20 --warmup 2 --no-cpu-baseline --no-extra --no-zipf $*"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT" -o trace -- \
   python3 "$R/bench.py" $ARGS > "$OUT/trace.log" 2>&1 || exit 1
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT" -o fetch -- \
