@@ -80,6 +80,9 @@ def parse(argv=None):
                    help="1M-key windows in the 1-thread CPU baseline sample (~10 s)")
     p.add_argument("--vector-sizes", default="100000,200000,300000",
                    help="VectorStorage restatement sample sizes (quadratic fit to 1e6)")
+    p.add_argument("--vector-only", action="store_true",
+                   help="time only the VectorStorage restatement at --vector-sizes (no GPU; e.g. the one "
+                        "measured 1e6-key run of config 1) and print its JSON")
     return p.parse_args(argv)
 
 
@@ -405,8 +408,19 @@ def vector_storage_fit(oracle, sizes):
     server/vector_storage_test.cpp's shape) timed at several n; Get is the
     O(stored x queried) scan of vector_storage.hpp:34-43, so t(n) is fitted with
     a quadratic and extrapolated to the config's 1e6 keys."""
+    import threading
+
     pts = []
     for n in sizes:
+        done = threading.Event()
+        t_start = time.perf_counter()
+
+        def beat(n=n, done=done, t_start=t_start):  # a long scan still shows progress
+            while not done.wait(30.0):
+                print(f"vector_storage n={n}: {time.perf_counter() - t_start:.0f} s", file=sys.stderr, flush=True)
+
+        hb = threading.Thread(target=beat, daemon=True)
+        hb.start()
         vec = oracle.VectorStorageRef(np.float32)
         k = np.arange(n, dtype=np.uint32)
         v = (0.5 * k).astype(np.float32)
@@ -414,6 +428,8 @@ def vector_storage_fit(oracle, sizes):
         vec.add(k, v)
         got = vec.get(k)
         t = time.perf_counter() - t0
+        done.set()
+        hb.join()
         assert np.array_equal(got, v)
         pts.append((n, t))
         vec.close()
@@ -427,7 +443,7 @@ def vector_storage_fit(oracle, sizes):
             "value": 24.0 * 1e6 / t1e6 / 1e9, "unit": "GB/s",
             "sample": "VectorStorage restatement (append + O(stored x queried) last-match scan), config 1's "
                       "contiguous float keys at the sizes listed, 1 thread; value = the quadratic fit at 1e6 keys "
-                      "(a measured 1e6 run: profiles/r03_vector_storage_1e6.log)"}
+                      "(the measured 1e6 run, bench.py --vector-only: profiles/r03_vector_storage_1e6.log, 215 s)"}
 
 
 def _cpu_model():
@@ -746,6 +762,16 @@ def variant_accumulate(rank, world, J, B, dev, sets, steps, lo, hi):
 
 def main(argv=None):
     args = parse(argv)
+    if args.vector_only:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle  # test infrastructure: the CPU baseline leg (VectorStorage restatement)
+
+        oracle.build()
+        sizes = [int(x) for x in args.vector_sizes.split(",") if x]
+        res = vector_storage_fit(oracle, sizes)
+        res["host_cpu"] = _cpu_model()
+        print(json.dumps(res), flush=True)
+        return
     # the JSON line is the only thing on stdout: everything else the run prints
     # (torch.distributed / gloo / RCCL banners, library notices) goes to stderr
     sys.stdout.flush()

@@ -24,7 +24,15 @@ constexpr int kSortedChunk = kBlock * 4 * kSortedUnroll;          // 2048 keys /
 constexpr int kGeneralChunk = 2048;  // keys per workgroup in the dedup path
 constexpr int kGeneralSlots = 4096;  // LDS hash slots (load factor <= 1/2)
 constexpr int kRbMaxBuckets = 2064;  // key buckets incl. the out-of-range bucket (>= 2049)
-constexpr uint32_t kRbMaxSc = 1024;  // K5 super-chunks per launch (one run per resolve thread)
+// K5a workgroup (option RB_BIN_BLOCK): 1024 threads, one per CU.  Two
+// 512-thread workgroups per CU on 4 Ki-key super-chunks measured slower on
+// cfg 3 (K5 164 against 153 us per 8 M Zipf keys, assign; 217 against 204
+// accumulate): the smaller super-chunks keep more duplicate entries and K5b
+// gathers twice as many runs.
+constexpr int kRbBinBlockDefault = 1024;
+constexpr uint32_t kRbMaxSc = 2048;  // K5 super-chunks per launch (two runs per resolve thread)
+// super-chunks per launch piece: 8 Mi keys of 4-byte values at either K5a size
+inline uint32_t rb_max_sc(int bin_block) { return bin_block == 512 ? 2048u : 1024u; }
 constexpr int kInlineMax = 256;      // keys of an inline (kernarg-carried) Add
 constexpr int kInlineGetMax = 512;   // keys of an inline Get
 constexpr int kInlineMaxChunks = 16;   // inline launches per call at most (reply buffer size)
@@ -142,16 +150,17 @@ struct RbMap {
 };
 
 // K5 radix-bucket general Add (2 launches: K5a bin, K5b resolve).  `ga`
-// chunked by rb_superchunk(vb) keys (nsc <= kRbMaxSc super-chunks); nbd dense
-// buckets (RbMap) plus one out-of-range bucket.
+// chunked by rb_superchunk(vb, bin_block) keys (nsc <= kRbMaxSc super-chunks);
+// nbd dense buckets (RbMap) plus one out-of-range bucket.  bin_block: K5a's
+// workgroup size, 1024 (one per CU) or 512 (two per CU, half the super-chunk).
 // Scratch: loff: nsc * (nbd+2) u16 (each super-chunk's bucket starts); tmp:
-// nsc * rb_superchunk(vb) entries (rb_entry_bytes(vb) each).
+// nsc * rb_superchunk(vb, bin_block) entries (rb_entry_bytes(vb) each).
 // apply_log2: log2 of the resolve workgroup's LDS table slots (13: 64 KiB, two
 // workgroups per CU, ~7 Ki entries per bucket in one pass; 14: 128 KiB, ~14 Ki).
 hipError_t launch_rb_add(int dtype, int mode, const GroupArgs& ga, uint32_t nsc,
                          const DenseView& d, const Ovf& o, const RbMap& bm,
-                         int apply_log2, uint16_t* loff, void* tmp, hipStream_t st);
-uint32_t rb_superchunk(int vb);
+                         int apply_log2, int bin_block, uint16_t* loff, void* tmp, hipStream_t st);
+uint32_t rb_superchunk(int vb, int bin_block);
 // K8: one small host message carried in the kernarg segment (one workgroup).
 // Get writes its n values to `out` (page-locked host memory or device memory);
 // with `done` non-null it then stores `seq` there (system-scope release) for a

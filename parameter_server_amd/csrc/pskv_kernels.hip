@@ -1200,9 +1200,11 @@ __device__ __forceinline__ void ready(const T (&x)[N]) {
   for (int i = 0; i < N; ++i) asm volatile("" ::"v"(x[i]));
 }
 
-// K5a k_rb_bin: one 1024-thread workgroup per CU, persistent over
-// super-chunks of SC keys of one batch (8 Ki keys for 4-byte values, 4 Ki for
-// 8-byte ones), the next super-chunk's loads in flight.  Per super-chunk:
+// K5a k_rb_bin: persistent workgroups of BINB threads over super-chunks of
+// SC = 8 * BINB keys of one batch (4-byte values; 4 * BINB for 8-byte ones),
+// the next super-chunk's loads in flight.  BINB = 1024: one workgroup per CU
+// (~139 KiB LDS); BINB = 512: 4 Ki-key super-chunks in ~74 KiB, two
+// workgroups per CU whose barrier-separated phases overlap.  Per super-chunk:
 //   dedup  the SC keys go into ONE LDS hash of 2*SC slots (key -> largest
 //          element index for assign, sum for accumulate): a key keeps one
 //          entry per super-chunk, its last value or its sum
@@ -1213,18 +1215,18 @@ __device__ __forceinline__ void ready(const T (&x)[N]) {
 //   row    the bucket starts go out as one 16-bit row loff[sc][0..nbk]
 //          (loff[sc][nbk] = the entry count)
 // Every global access is a coalesced 16-byte stream; no global atomics.
-constexpr int kBinBlock = 1024;
 template <typename BT>
-constexpr uint32_t rb_sc() {
-  return sizeof(BT) == 8 ? 4096u : 8192u;
+constexpr uint32_t rb_sc(int binb) {
+  return (sizeof(BT) == 8 ? 4u : 8u) * (uint32_t)binb;
 }
 
-template <typename AT, typename BT, int MODE>
-__global__ __launch_bounds__(kBinBlock) void k_rb_bin(GroupArgs ga, DenseView d, RbMap bm,
-                                                      uint32_t nbk,
-                                                      uint16_t* __restrict__ loff, uint32_t nsc,
-                                                      RbEnt<sizeof(BT)>* __restrict__ tmp) {
-  constexpr uint32_t SC = rb_sc<BT>();
+template <typename AT, typename BT, int MODE, int BINB>
+__global__ __launch_bounds__(BINB) void k_rb_bin(GroupArgs ga, DenseView d, RbMap bm,
+                                                 uint32_t nbk,
+                                                 uint16_t* __restrict__ loff, uint32_t nsc,
+                                                 RbEnt<sizeof(BT)>* __restrict__ tmp) {
+  constexpr int kBinBlock = BINB;
+  constexpr uint32_t SC = rb_sc<BT>(BINB);
   constexpr int KPT = (int)(SC / kBinBlock);  // keys per thread: 8 or 4
   constexpr int SLOTS = (int)(2 * SC);
   using Ent = RbEnt<sizeof(BT)>;
@@ -1401,10 +1403,12 @@ __global__ __launch_bounds__(kBinBlock) void k_rb_bin(GroupArgs ga, DenseView d,
 // K5b k_rb_resolve: one 1024-thread workgroup per bucket (LDS: 128 KiB table,
 // one workgroup per CU, 16 waves).  The bucket's entries are the runs
 // [loff[sc][b], loff[sc][b+1]) of the super-chunk regions; thread t loads the
-// run of super-chunk t straight into registers (one contiguous read; the few
-// entries past RPT are read in a loop, and a bucket with a run longer than
+// runs of super-chunk t (nsc <= 1024) or of super-chunks 2t and 2t + 1
+// (nsc <= 2048: K5a's 4 Ki-key super-chunks) straight into registers as ONE
+// virtual run (the second run's entries follow the first's; the few entries
+// past RPT are read in a loop, and a bucket with a virtual run longer than
 // LONG takes the strided path below), and its entries' positions pre[t] + q
-// (pre = exclusive scan of the run lengths) are call order.  An LDS hash resolves the bucket — the largest position wins
+// (pre = exclusive scan of the virtual run lengths) are call order.  An LDS hash resolves the bucket — the largest position wins
 // (assign) / values add (accumulate) — and the winners store into the dense
 // array or the overflow table.  A bucket is owned by one workgroup: no
 // cross-workgroup ordering, no global atomics.  Buckets are dealt XCD by XCD
@@ -1413,12 +1417,12 @@ __global__ __launch_bounds__(kBinBlock) void k_rb_bin(GroupArgs ga, DenseView d,
 // bucket's loff words are read while this one resolves.  Slot SLOTS belongs
 // to the key 0xFFFFFFFF.
 constexpr int kApplyBlock = 1024;
-static_assert(kRbMaxSc <= (uint32_t)kApplyBlock, "one run per resolve thread");
+static_assert(kRbMaxSc <= 2u * kApplyBlock, "at most two runs per resolve thread");
 template <typename AT, typename BT, int MODE, int LOGS>
 __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, RbMap bm,
                                                             uint32_t nbk,
                                                             const uint16_t* __restrict__ loff,
-                                                            uint32_t nsc,
+                                                            uint32_t nsc, uint32_t SC,
                                                             const RbEnt<sizeof(BT)>* __restrict__ tmp) {
   // f64 sums take 8 B per slot: half the slots in the same LDS
   constexpr int SLOTS = (MODE == 1 && sizeof(AT) == 8) ? (1 << LOGS) / 2 : (1 << LOGS);
@@ -1426,7 +1430,6 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
   constexpr int RPT = 10;                             // run entries held in registers (10: no spills for 4-byte values)
   constexpr uint32_t LONG = 4 * RPT;                  // longer runs: the strided path
   static_assert(LONG <= 64, "a run's winners fit one 64-bit mask");
-  constexpr uint32_t SC = rb_sc<BT>();
   using Ent = RbEnt<sizeof(BT)>;
   // assign: keys ak[0..SLOTS] and 1 + max position abest[0..SLOTS] in one
   // array, which the direct path reuses whole as best[0..DSPAN)
@@ -1440,8 +1443,9 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
   constexpr uint32_t DSPAN = MODE == 0 ? 2u * SLOTS : 1u;
   constexpr uint32_t kPosBits = 18;
   uint32_t* best = ak;
-  __shared__ uint32_t pre[kRbMaxSc + 1];  // run starts (positions); pre[nsc] = entries
-  __shared__ uint32_t rst[kRbMaxSc];      // run starts (entry index in tmp)
+  // virtual-run starts (positions; the scan's array), then, in the strided
+  // path, the starts of the nsc runs (pre[nsc] = entries)
+  __shared__ uint32_t pre[kRbMaxSc + 1];
   __shared__ __attribute__((aligned(16))) uint32_t wtmp[kApplyBlock / 64];
   __shared__ uint32_t sent;
   const int tid = threadIdx.x;
@@ -1452,7 +1456,7 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
     while (ak[h] != key) h = (h + 1) & (SLOTS - 1);
     return h;
   };
-  auto first_run = [&](uint32_t p) -> uint32_t {  // last r with pre[r] <= p
+  auto first_run = [&](uint32_t p) -> uint32_t {  // last run r with pre[r] <= p
     uint32_t lo = 0, hi = nsc;
     while (hi - lo > 1) {
       const uint32_t mid = (lo + hi) >> 1;
@@ -1542,22 +1546,45 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
   const uint32_t per_xcd = (gridDim.x + 7u - xcd) >> 3;  // workgroups in this XCD group
   const uint32_t b_hi = (uint32_t)((uint64_t)nbk * (xcd + 1) / 8);
   uint32_t b = (uint32_t)((uint64_t)nbk * xcd / 8) + (blockIdx.x >> 3);
-  const bool has_run = (uint32_t)tid < nsc;
-  const uint32_t rowo = has_run ? (uint32_t)tid * (nbk + 1) : 0u;  // this thread's loff row
-  // software pipeline: the run of bucket b in registers, the run bounds of the
-  // bucket after it in flight.  The bounds loads are unconditional (a thread
-  // without a run, or past the last bucket, reads a valid word it then
+  // this thread's runs: super-chunk r0 and, with two runs per thread, r0 + 1
+  const uint32_t rpt = nsc > (uint32_t)kApplyBlock ? 2u : 1u;  // uniform
+  const uint32_t r0 = (uint32_t)tid * rpt;
+  const bool has_run = r0 < nsc, has_run2 = rpt == 2u && r0 + 1u < nsc;
+  const uint32_t rowo = has_run ? r0 * (nbk + 1) : 0u;    // this thread's loff rows
+  const uint32_t rowo2 = has_run2 ? rowo + nbk + 1 : 0u;
+  const uint32_t st1 = r0 * SC, st2 = (r0 + 1u) * SC;   // the runs' regions in tmp
+  // software pipeline: the runs of bucket b in registers, the run bounds of
+  // the bucket after it in flight.  The bounds loads are unconditional (a
+  // thread without a run, or past the last bucket, reads a valid word it then
   // ignores) so nothing waits for them until the next bucket uses them.
-  auto bounds_ok = [&](uint32_t bb) { return bb < b_hi && has_run; };
-  auto bounds = [&](uint32_t bb, uint32_t& a, uint32_t& e) {
-    const uint32_t i = rowo + (bb < b_hi ? bb : 0u);
-    a = loff[i];
-    e = loff[i + 1];
+  struct Rb {
+    uint32_t a, e, a2, e2;
   };
-  auto load_run = [&](uint32_t a, uint32_t e, Ent (&x)[RPT]) {
+  auto bounds_ok = [&](uint32_t bb) { return bb < b_hi && has_run; };
+  auto bounds = [&](uint32_t bb, Rb& r) {
+    const uint32_t c = bb < b_hi ? bb : 0u;
+    r.a = loff[rowo + c];
+    r.e = loff[rowo + c + 1];
+    r.a2 = r.e2 = 0;
+    if (rpt == 2u) {  // uniform
+      r.a2 = loff[rowo2 + c];
+      r.e2 = loff[rowo2 + c + 1];
+    }
+  };
+  auto none = [&](Rb& r, bool keep, bool keep2) {
+    if (!keep) r.a = r.e = 0;
+    if (!keep2) r.a2 = r.e2 = 0;
+  };
+  // entry q of the virtual run: the first run's entries, then the second's
+  auto ent_at = [&](const Rb& r, uint32_t q) -> uint32_t {
+    const uint32_t l1 = r.e - r.a;
+    return q < l1 ? st1 + r.a + q : st2 + r.a2 + (q - l1);
+  };
+  auto load_run = [&](const Rb& r, Ent (&x)[RPT]) {
+    const uint32_t len = (r.e - r.a) + (r.e2 - r.a2);
 #pragma unroll
     for (int q = 0; q < RPT; ++q)
-      if ((uint32_t)q < e - a) x[q] = tmp[(uint32_t)tid * SC + a + q];
+      if ((uint32_t)q < len) x[q] = tmp[ent_at(r, (uint32_t)q)];
   };
   uint32_t dlog = 0;
   while ((1u << dlog) < DSPAN) ++dlog;
@@ -1568,26 +1595,26 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
     for (uint32_t i = (uint32_t)tid * 4; i < DSPAN; i += kApplyBlock * 4)
       *reinterpret_cast<u32x4*>(&best[i]) = u32x4{0u, 0u, 0u, 0u};
   };
-  uint32_t ra, re, na, ne_;
-  bounds(b, ra, re);
-  if (!bounds_ok(b)) ra = re = 0;
-  bounds(b + per_xcd, na, ne_);
+  Rb cr, nr;
+  bounds(b, cr);
+  none(cr, bounds_ok(b), bounds_ok(b) && has_run2);
+  bounds(b + per_xcd, nr);
   Ent xn[RPT];
-  load_run(ra, re, xn);
+  load_run(cr, xn);
   for (; b < b_hi; b += per_xcd) {
-    const uint32_t len = re - ra, st = (uint32_t)tid * SC + ra;
+    const Rb r = cr;
+    const uint32_t len = (r.e - r.a) + (r.e2 - r.a2);
     Ent x[RPT];
 #pragma unroll
     for (int q = 0; q < RPT; ++q) x[q] = xn[q];
     // next bucket: its run loads now, the bounds of the one after
-    ra = bounds_ok(b + per_xcd) ? na : 0u;
-    re = bounds_ok(b + per_xcd) ? ne_ : 0u;
-    load_run(ra, re, xn);
-    bounds(b + 2 * per_xcd, na, ne_);
+    cr = nr;
+    none(cr, bounds_ok(b + per_xcd), bounds_ok(b + per_xcd) && has_run2);
+    load_run(cr, xn);
+    bounds(b + 2 * per_xcd, nr);
     pre[tid] = len;
-    if (tid == 0) pre[kRbMaxSc] = 0;
     const bool long_run = __syncthreads_or(len > LONG) != 0;
-    const uint32_t ne = block_exscan<kApplyBlock>(pre, kRbMaxSc, wtmp);
+    const uint32_t ne = block_exscan<kApplyBlock>(pre, kApplyBlock, wtmp);
     const uint32_t p0 = pre[tid];
     if (ne == 0) continue;  // uniform
     const bool direct = MODE == 0 && b != nbd && !long_run && halves <= 4 &&
@@ -1613,8 +1640,8 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
           if ((uint32_t)q < len && (rel[q] >> dlog) == h)
             atomicMax(&best[rel[q] & (DSPAN - 1)], tg | (p0 + (uint32_t)q + 1u));
         for (uint32_t q = RPT; q < len; ++q) {  // a run's short tail, from memory
-          const uint32_t r = rb_local(bm, tmp[st + q].key - d.key_begin);
-          if ((r >> dlog) == h) atomicMax(&best[r & (DSPAN - 1)], tg | (p0 + q + 1u));
+          const uint32_t rl = rb_local(bm, tmp[ent_at(r, q)].key - d.key_begin);
+          if ((rl >> dlog) == h) atomicMax(&best[rl & (DSPAN - 1)], tg | (p0 + q + 1u));
         }
         __syncthreads();
 #pragma unroll
@@ -1623,8 +1650,8 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
               best[rel[q] & (DSPAN - 1)] == (tg | (p0 + (uint32_t)q + 1u)))
             win |= 1ull << q;
         for (uint32_t q = RPT; q < len; ++q) {
-          const uint32_t r = rb_local(bm, tmp[st + q].key - d.key_begin);
-          if ((r >> dlog) == h && best[r & (DSPAN - 1)] == (tg | (p0 + q + 1u))) win |= 1ull << q;
+          const uint32_t rl = rb_local(bm, tmp[ent_at(r, q)].key - d.key_begin);
+          if ((rl >> dlog) == h && best[rl & (DSPAN - 1)] == (tg | (p0 + q + 1u))) win |= 1ull << q;
         }
         if (h + 1 < halves) __syncthreads();  // the table is read before the next pass
       }
@@ -1633,7 +1660,7 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
         if (win >> q & 1u) store_winner(b, x[q].key, (BT)x[q].val);
       for (uint32_t q = RPT; q < len; ++q)
         if (win >> q & 1u) {
-          const Ent y = tmp[st + q];
+          const Ent y = tmp[ent_at(r, q)];
           store_winner(b, y.key, (BT)y.val);
         }
       // the next bucket's first atomics come after its scan's barriers, so
@@ -1660,7 +1687,7 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
           lds_add(&asum[slot[q]], from_bits<AT>(to_bits<BT>((BT)x[q].val)));
       }
       for (uint32_t q = RPT; q < len; ++q) {  // a run's short tail (<= LONG - RPT), from memory
-        const Ent y = tmp[st + q];
+        const Ent y = tmp[ent_at(r, q)];
         insert_one(y.key, p0 + q, (BT)y.val);
       }
       __syncthreads();
@@ -1670,7 +1697,7 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
           if ((valid >> q & 1u) && abest[slot[q]] == p0 + (uint32_t)q + 1u)
             store_winner(b, key[q], (BT)x[q].val);
         for (uint32_t q = RPT; q < len; ++q) {
-          const Ent y = tmp[st + q];
+          const Ent y = tmp[ent_at(r, q)];
           if (abest[find(y.key)] == p0 + q + 1u) store_winner(b, y.key, (BT)y.val);
         }
       } else {
@@ -1680,25 +1707,29 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
     } else {
       // a run longer than the registers hold, or more entries than the table
       // holds: every thread takes positions tid, tid + 1024, ... (coalesced
-      // inside long runs), found by binary search over the run starts; rounds
-      // split an oversized bucket by key hash
-      if (has_run) rst[tid] = st;
+      // inside long runs), found by binary search over the starts of the nsc
+      // runs (pre, rewritten per run); rounds split an oversized bucket by key
+      // hash.  Run j's entries start at j * SC + its loff word.
+      __syncthreads();  // every p0 read before pre changes meaning
+      if (has_run) pre[r0] = p0;
+      if (has_run2) pre[r0 + 1] = p0 + (r.e - r.a);
       if (tid == 0) pre[nsc] = ne;
+      auto run_ent = [&](uint32_t j, uint32_t p) -> Ent {
+        return tmp[j * SC + loff[j * (nbk + 1) + b] + (p - pre[j])];
+      };
       const uint32_t R = (ne + CAP - 1) / CAP;
       for (uint32_t round = 0; round < R; ++round) {
         clear_table();
         __syncthreads();
         for (uint32_t p = tid; p < ne; p += kApplyBlock) {
-          const uint32_t r = first_run(p);
-          const Ent y = tmp[rst[r] + (p - pre[r])];
+          const Ent y = run_ent(first_run(p), p);
           if ((fmix32(y.key ^ 0x9E3779B9u) % R) == round) insert_one(y.key, p, (BT)y.val);
         }
         __syncthreads();
         if (MODE == 0) {
           // the entry holding its key's largest position is the last write
           for (uint32_t p = tid; p < ne; p += kApplyBlock) {
-            const uint32_t r = first_run(p);
-            const Ent y = tmp[rst[r] + (p - pre[r])];
+            const Ent y = run_ent(first_run(p), p);
             if ((fmix32(y.key ^ 0x9E3779B9u) % R) != round) continue;
             if (abest[find(y.key)] == p + 1u) store_winner(b, y.key, (BT)y.val);
           }
@@ -2470,25 +2501,34 @@ hipError_t launch_ovf_rehash(int vb, const Ovf& from, uint64_t from_cap, const O
 
 template <typename AT, typename BT, int MODE>
 static hipError_t rb_launch(const GroupArgs& ga, uint32_t nsc, const DenseView& d, const Ovf& o,
-                            const RbMap& bm, int apply_log2, uint16_t* loff, void* tmp, hipStream_t st) {
+                            const RbMap& bm, int apply_log2, int bin_block, uint16_t* loff, void* tmp,
+                            hipStream_t st) {
   const uint32_t nbk = bm.nbd + 1;
   auto* t = reinterpret_cast<RbEnt<sizeof(BT)>*>(tmp);
-  // persistent grid, one 1024-thread workgroup per CU (~140 KiB LDS)
-  const uint32_t gb = nsc < 256u ? nsc : 256u;
-  k_rb_bin<AT, BT, MODE><<<gb, kBinBlock, 0, st>>>(ga, d, bm, nbk, loff, nsc, t);
-  if (apply_log2 == 13)  // 2^13 slots: two workgroups per CU
-    k_rb_resolve<AT, BT, MODE, 13><<<512, kApplyBlock, 0, st>>>(d, o, bm, nbk, loff, nsc, t);
+  // persistent grid: one 1024-thread workgroup per CU (~139 KiB LDS), or two
+  // 512-thread ones (~74 KiB each)
+  const uint32_t wgs = bin_block == 512 ? 512u : 256u;
+  const uint32_t gb = nsc < wgs ? nsc : wgs;
+  if (bin_block == 512)
+    k_rb_bin<AT, BT, MODE, 512><<<gb, 512, 0, st>>>(ga, d, bm, nbk, loff, nsc, t);
   else
-    k_rb_resolve<AT, BT, MODE, 14><<<256, kApplyBlock, 0, st>>>(d, o, bm, nbk, loff, nsc, t);
+    k_rb_bin<AT, BT, MODE, 1024><<<gb, 1024, 0, st>>>(ga, d, bm, nbk, loff, nsc, t);
+  const uint32_t sc = rb_sc<BT>(bin_block);
+  if (apply_log2 == 13)  // 2^13 slots: two workgroups per CU
+    k_rb_resolve<AT, BT, MODE, 13><<<512, kApplyBlock, 0, st>>>(d, o, bm, nbk, loff, nsc, sc, t);
+  else
+    k_rb_resolve<AT, BT, MODE, 14><<<256, kApplyBlock, 0, st>>>(d, o, bm, nbk, loff, nsc, sc, t);
   return hipGetLastError();
 }
 
 hipError_t launch_rb_add(int dtype, int mode, const GroupArgs& ga, uint32_t nsc,
                          const DenseView& d, const Ovf& o, const RbMap& bm,
-                         int apply_log2, uint16_t* loff, void* tmp, hipStream_t st) {
+                         int apply_log2, int bin_block, uint16_t* loff, void* tmp, hipStream_t st) {
   if (nsc == 0) return hipSuccess;
-  if (bm.nbd + 1 > (uint32_t)kRbMaxBuckets || nsc > kRbMaxSc || bm.nbd == 0) return hipErrorInvalidValue;
-#define PSKV_RB(AT, BT, M) rb_launch<AT, BT, M>(ga, nsc, d, o, bm, apply_log2, loff, tmp, st)
+  if (bm.nbd + 1 > (uint32_t)kRbMaxBuckets || nsc > kRbMaxSc || bm.nbd == 0 ||
+      (bin_block != 512 && bin_block != 1024))
+    return hipErrorInvalidValue;
+#define PSKV_RB(AT, BT, M) rb_launch<AT, BT, M>(ga, nsc, d, o, bm, apply_log2, bin_block, loff, tmp, st)
   if (mode == 0) {
     if (dtype == 0) return PSKV_RB(int, uint32_t, 0);
     if (dtype == 1) return PSKV_RB(float, uint32_t, 0);
@@ -2520,7 +2560,9 @@ hipError_t launch_acc_dense(int dtype, const GroupArgs& ga, uint32_t grid, const
 }
 
 // Super-chunk size (keys) and entry size of the K5 path for a value size.
-uint32_t rb_superchunk(int vb) { return vb == 8 ? rb_sc<unsigned long long>() : rb_sc<uint32_t>(); }
+uint32_t rb_superchunk(int vb, int bin_block) {
+  return vb == 8 ? rb_sc<unsigned long long>(bin_block) : rb_sc<uint32_t>(bin_block);
+}
 size_t rb_entry_bytes(int vb) { return vb == 8 ? sizeof(RbEnt<8>) : sizeof(RbEnt<4>); }
 
 

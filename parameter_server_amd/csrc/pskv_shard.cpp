@@ -7,15 +7,17 @@
 // key range, an overflow hash table for every other key, a stream, and
 // pinned/device staging for host (zmq-buffer) inputs.
 //
-// Call flow of an assign-mode Add (DESIGN.md "Add"):
-//   host inputs   → copy into pinned staging while checking "sorted and in
-//                   range" on the CPU → H2D → K2 if verified, else K4a+K4b.
+// Call flow of an assign-mode Add:
+//   small host messages → K8 (kernarg-carried) or the K9 request server.
+//   host inputs   → copy into pinned staging (or DMA / read in place when
+//                   page-locked) while checking "sorted and in range" on the
+//                   CPU → K2 / K2g if verified, else K5.
 //   device inputs → PSKV_SORTED_HINT: K2 (one batch) or K2g (group), each
-//                   verifying on device, followed by K4a+K4b launched
-//                   conditional on the verification tag (they exit at once
-//                   when the hint held).  No hint: K4a+K4b.
-// Accumulate-mode Add: K4a (always correct, order free).
-// Get: K1 (one launch per group of <= 64 batches).
+//                   verifying on device, followed by the one-workgroup K4r
+//                   replay, which exits at once unless the verification
+//                   tagged the call.  No hint: K5 (key buckets).
+// Accumulate-mode Add: K6 density proof + K7 for dense windows, else K5.
+// Get: K1 (one launch per group of <= 64 batches), K8 for small messages.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -231,6 +233,9 @@ struct pskv_shard {
   void* dstage = nullptr;
   size_t dstage_bytes = 0;
   std::vector<hipEvent_t> win_events;  // per-window D2H completion (pull to host)
+  // page-locked Get: values DMA'd out on their own stream, window by window
+  hipStream_t out_stream = nullptr;
+  std::vector<hipEvent_t> out_events;
   // timing
   uint32_t timing_mask = 0;  // bit k: bracket kernel k with events
   std::vector<TimedLaunch> pending;
@@ -296,6 +301,7 @@ struct pskv_shard {
   bool tune_ispin = true;  // PSKV_ISPIN: poll the reply's sequence word instead of a stream wait
   unsigned int ireply_seq = 0;
   int tune_rb_apply_log2 = 0; // PSKV_RB_APPLY_LOG2: 13 or 14 (0 = by bucket size)
+  int tune_rb_bin_block = kRbBinBlockDefault;  // PSKV_RB_BIN_BLOCK: K5a workgroup, 512 or 1024
   // K9 request server (PSKV_SERVE=1): the inline-size messages go to a ring in
   // coherent page-locked memory that one resident workgroup polls
   // (PSKV_SERVE_IDLE_US: it leaves after this long without a request)
@@ -399,6 +405,7 @@ int drain_timing(pskv_shard* s) {
 // queued behind other work does not hang its caller: srv_wait bounds the wait
 // for it to start (kSrvStartTimeoutMs) and fails the call.
 std::atomic<int> g_device_shards[64];
+std::atomic<int> g_device_extra_streams[64];  // pinned-Get output streams
 
 bool serve_on(const pskv_shard* s) {
   if (!s->tune_serve || s->device < 0 || s->device >= 64) return false;
@@ -407,7 +414,9 @@ bool serve_on(const pskv_shard* s) {
     const int q = e ? std::atoi(e) : 4;
     return q > 0 ? q : 4;
   }();
-  return 2 * g_device_shards[s->device].load(std::memory_order_relaxed) + 1 <= queues;
+  return 2 * g_device_shards[s->device].load(std::memory_order_relaxed) + 1 +
+             g_device_extra_streams[s->device].load(std::memory_order_relaxed) <=
+         queues;
 }
 
 constexpr int kSrvStartTimeoutMs = 2000;
@@ -692,11 +701,11 @@ int ensure_scratch(pskv_shard* s, void** p, size_t* have, size_t need) {
 }
 
 // K5: radix-bucket general Add (no random global atomics), one launch pair
-// per <= kRbMaxSc super-chunks; a longer group is cut into consecutive pieces
+// per <= rb_max_sc super-chunks; a longer group is cut into consecutive pieces
 // (a batch may be split), which run in stream order, so call order holds.
 int radix_launch(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t e) {
   GroupArgs ga;
-  const uint32_t nsc = build_group(v, b, e, rb_superchunk(s->vb), &ga);
+  const uint32_t nsc = build_group(v, b, e, rb_superchunk(s->vb, s->tune_rb_bin_block), &ga);
   uint64_t elems = 0;
   for (size_t i = b; i < e; ++i) elems += v[i].n;
   // bucket = key offset >> bshift (more buckets: longer loff rows, shorter
@@ -731,26 +740,29 @@ int radix_launch(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size
   int apply_log2 = elems / nbd <= 2048 ? 13 : 14;
   if (s->tune_rb_apply_log2) apply_log2 = s->tune_rb_apply_log2;
   if (nbk > (uint32_t)kRbMaxBuckets) return fail(PSKV_EINVAL, "radix path: too many buckets");
-  if (nsc > kRbMaxSc) return fail(PSKV_EINVAL, "radix path: launch piece too large");
+  if (nsc > rb_max_sc(s->tune_rb_bin_block)) return fail(PSKV_EINVAL, "radix path: launch piece too large");
   const size_t eb = rb_entry_bytes(s->vb);
   int rc = ensure_scratch(s, reinterpret_cast<void**>(&s->rb_loff), &s->rb_loff_bytes,
                           (size_t)nsc * (nbk + 1) * sizeof(uint16_t));
-  if (!rc) rc = ensure_scratch(s, &s->rb_ent, &s->rb_ent_bytes, (size_t)nsc * rb_superchunk(s->vb) * eb);
+  if (!rc)
+    rc = ensure_scratch(s, &s->rb_ent, &s->rb_ent_bytes,
+                        (size_t)nsc * rb_superchunk(s->vb, s->tune_rb_bin_block) * eb);
   if (rc) return rc;
   LaunchTimer t(s, PSKV_K_RADIX, elems);
   PSKV_HIP(launch_rb_add(s->dtype, s->mode, ga, nsc, s->dview(), s->ovf, bm, apply_log2,
-                         s->rb_loff, s->rb_ent, s->stream));
+                         s->tune_rb_bin_block, s->rb_loff, s->rb_ent, s->stream));
   t.done();
   s->n_general += 2;
   return PSKV_OK;
 }
 
 int radix_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t e) {
-  const uint64_t sc = rb_superchunk(s->vb);
+  const uint64_t sc = rb_superchunk(s->vb, s->tune_rb_bin_block);
   uint64_t nsc = 0;
   for (size_t i = b; i < e; ++i) nsc += (v[i].n + sc - 1) / sc;
-  if (nsc <= kRbMaxSc) return radix_launch(s, v, b, e);
-  // pieces of whole super-chunks, each <= kRbMaxSc of them
+  const uint64_t max_sc = rb_max_sc(s->tune_rb_bin_block);
+  if (nsc <= max_sc) return radix_launch(s, v, b, e);
+  // pieces of whole super-chunks, each <= max_sc of them
   std::vector<pskv_batch> piece;
   uint64_t used = 0;  // super-chunks in `piece`
   auto flush = [&]() -> int {
@@ -763,10 +775,10 @@ int radix_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t 
   for (size_t i = b; i < e; ++i) {
     uint64_t off = 0;
     while (off < v[i].n) {
-      if (used == kRbMaxSc || piece.size() == (size_t)kMaxBatches) {
+      if (used == max_sc || piece.size() == (size_t)kMaxBatches) {
         if (int rc = flush()) return rc;
       }
-      const uint64_t room = (kRbMaxSc - used) * sc;
+      const uint64_t room = (max_sc - used) * sc;
       const uint64_t n = std::min<uint64_t>(v[i].n - off, room);
       piece.push_back(pskv_batch{v[i].keys + off,
                                  static_cast<char*>(v[i].vals) + off * (uint64_t)s->vb, n});
@@ -1499,6 +1511,78 @@ int zero_copy_get(pskv_shard* s, const std::vector<pskv_batch>& v, bool vec) {
   return PSKV_OK;
 }
 
+// Get from page-locked caller buffers by DMA: the batches go in windows of
+// about kWindowBytes of keys; per window the keys are DMA'd in and K1 runs on
+// the shard's stream, and the window's values are DMA'd out on a second
+// stream once its K1 is done, so the values of window w travel to the host
+// while the keys of window w+1 travel to the device (PCIe is full duplex; the
+// two directions use different DMA engines).  The call returns when every
+// value has arrived.
+int pinned_get(pskv_shard* s, const std::vector<pskv_batch>& v) {
+  size_t bytes = 0;
+  for (auto& b : v) bytes += round16(b.n * 4) + round16(b.n * (size_t)s->vb);
+  int rc = ensure_dstage(s, bytes);
+  if (rc) return rc;
+  if (!s->out_stream) {
+    PSKV_HIP(hipStreamCreateWithFlags(&s->out_stream, hipStreamNonBlocking));
+    g_device_extra_streams[s->device].fetch_add(1, std::memory_order_relaxed);
+  }
+  std::vector<pskv_batch> dv = v;
+  char* d = static_cast<char*>(s->dstage);
+  size_t off = 0;
+  bool vec = true;
+  for (size_t i = 0; i < v.size(); ++i) {
+    dv[i].keys = reinterpret_cast<const uint32_t*>(d + off);
+    off += round16(v[i].n * 4);
+    dv[i].vals = d + off;
+    off += round16(v[i].n * (size_t)s->vb);
+    vec &= aligned16(dv[i].keys) & aligned16(dv[i].vals);
+  }
+  // windows [first batch, end batch): >= kWindowBytes of keys, <= kMaxBatches
+  // batches, < 2^32 elements (split_groups' limits for one launch)
+  std::vector<std::pair<size_t, size_t>> wins;
+  for (size_t i = 0; i < v.size();) {
+    size_t j = i, kb = 0;
+    uint64_t elems = 0;
+    while (j < v.size() && (j == i || (kb < kWindowBytes && j - i < (size_t)kMaxBatches &&
+                                       elems + v[j].n < (1ull << 32)))) {
+      kb += v[j].n * 4;
+      elems += v[j].n;
+      ++j;
+    }
+    wins.emplace_back(i, j);
+    i = j;
+  }
+  while (s->out_events.size() < wins.size()) {
+    hipEvent_t e = nullptr;
+    PSKV_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    s->out_events.push_back(e);
+  }
+  for (size_t w = 0; w < wins.size(); ++w) {
+    const size_t b = wins[w].first, e = wins[w].second;
+    for (size_t i = b; i < e; ++i)
+      PSKV_HIP(hipMemcpyAsync(const_cast<uint32_t*>(dv[i].keys), v[i].keys, v[i].n * 4, hipMemcpyHostToDevice,
+                              s->stream));
+    GroupArgs ga;
+    const uint32_t nwg = build_group(dv, b, e, stream_chunk(gather_unroll(s)), &ga);
+    uint64_t elems = 0;
+    for (size_t i = b; i < e; ++i) elems += dv[i].n;
+    LaunchTimer t(s, PSKV_K_GATHER, elems);
+    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, s->tune_get_dedup, ga, nwg, s->dview(),
+                           s->ovf, s->stream));
+    t.done();
+    PSKV_HIP(hipEventRecord(s->out_events[w], s->stream));
+    PSKV_HIP(hipStreamWaitEvent(s->out_stream, s->out_events[w], 0));
+    for (size_t i = b; i < e; ++i)
+      PSKV_HIP(hipMemcpyAsync(v[i].vals, dv[i].vals, v[i].n * (size_t)s->vb, hipMemcpyDeviceToHost,
+                              s->out_stream));
+  }
+  // the stage is free again once the out stream is done; both streams drained
+  PSKV_HIP(hipStreamSynchronize(s->out_stream));
+  PSKV_HIP(hipStreamSynchronize(s->stream));
+  return PSKV_OK;
+}
+
 int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
   std::vector<pskv_batch> v;
   for (auto& b : in) {
@@ -1541,22 +1625,8 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
     for (auto& b : v) bytes += round16(b.n * 4) + round16(b.n * (size_t)s->vb);
     pinned = bytes >= s->tune_dma_min_bytes_get;
   }
-  if (pinned) {
-    // page-locked caller buffers: keys DMA'd in directly, values DMA'd out directly
-    size_t bytes = 0;
-    for (auto& b : v) bytes += round16(b.n * 4) + round16(b.n * (size_t)s->vb);
-    rc = ensure_dstage(s, bytes);
-    if (rc) return rc;
-    char* d = static_cast<char*>(s->dstage);
-    size_t off = 0;
-    for (size_t i = 0; i < v.size(); ++i) {
-      PSKV_HIP(hipMemcpyAsync(d + off, v[i].keys, v[i].n * 4, hipMemcpyHostToDevice, s->stream));
-      dv[i].keys = reinterpret_cast<const uint32_t*>(d + off);
-      off += round16(v[i].n * 4);
-      dv[i].vals = d + off;
-      off += round16(v[i].n * (size_t)s->vb);
-    }
-  } else if (!device) {
+  if (pinned) return pinned_get(s, v);
+  if (!device) {
     // keys -> pinned -> device (pipelined); outputs land after the keys in the stage
     size_t kbytes = 0, obytes = 0;
     for (auto& b : v) {
@@ -1596,12 +1666,7 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
                            s->stream));
     t.done();
   }
-  if (pinned) {
-    for (size_t i = 0; i < v.size(); ++i)
-      PSKV_HIP(hipMemcpyAsync(v[i].vals, dv[i].vals, v[i].n * (size_t)s->vb, hipMemcpyDeviceToHost,
-                              s->stream));
-    PSKV_HIP(hipStreamSynchronize(s->stream));
-  } else if (!device) {
+  if (!device) {
     // D2H window by window; the pool copies window w out to the caller while
     // window w+1 is still in flight
     char* h = static_cast<char*>(s->hstage);
@@ -1692,6 +1757,7 @@ const Option kOptions[] = {
     PSKV_OPT("RB_NBD", 0, kRbMaxBuckets - 1, tune_rb_nbd, uint32_t),
     PSKV_OPT("RB_TB", 0, 11, tune_rb_tb, uint32_t),
     PSKV_OPT("RB_APPLY_LOG2", 0, 14, tune_rb_apply_log2, int),  // 0 = by size, 13 or 14
+    PSKV_OPT("RB_BIN_BLOCK", 512, 1024, tune_rb_bin_block, int),  // 512 or 1024
 };
 #undef PSKV_OPT
 
@@ -1707,6 +1773,8 @@ int set_option(pskv_shard* s, const Option& o, int64_t v) {
   if (std::strcmp(o.name, "TILE_SHIFT") == 0 && v != 0 && v < 10) return fail(PSKV_EINVAL, "option TILE_SHIFT: 0 or 10..20");
   if (std::strcmp(o.name, "RB_APPLY_LOG2") == 0 && v != 0 && v != 13 && v != 14)
     return fail(PSKV_EINVAL, "option RB_APPLY_LOG2: 0, 13 or 14");
+  if (std::strcmp(o.name, "RB_BIN_BLOCK") == 0 && v != 512 && v != 1024)
+    return fail(PSKV_EINVAL, "option RB_BIN_BLOCK: 512 or 1024");
   o.set(s, v);
   if (std::strcmp(o.name, "INLINE_ADD_CHUNKS") == 0) s->add_chunks_set = true;
   // a ring slot costs the host ~0.2 us where a K8 launch costs 3-7: with the
@@ -1826,6 +1894,12 @@ int pskv_shard_destroy(pskv_shard* s) {
   if (s->counted) g_device_shards[s->device].fetch_sub(1, std::memory_order_relaxed);
   if (s->srv_stream) (void)hipStreamDestroy(s->srv_stream);
   if (s->srv_dep) (void)hipEventDestroy(s->srv_dep);
+  if (s->out_stream) {
+    (void)hipStreamSynchronize(s->out_stream);
+    (void)hipStreamDestroy(s->out_stream);
+    g_device_extra_streams[s->device].fetch_sub(1, std::memory_order_relaxed);
+  }
+  for (auto e : s->out_events) (void)hipEventDestroy(e);
   if (s->own_stream) (void)hipStreamSynchronize(s->own_stream);
   if (s->stream && s->stream != s->own_stream) (void)hipStreamSynchronize(s->stream);
   for (auto& t : s->pending) {

@@ -1338,7 +1338,7 @@ def test_shard_options_api(cuda):
     names = ["GENERAL", "UNROLL", "NT", "NTP", "GET_DEDUP", "PAGEABLE_DMA", "DMA_MIN_BYTES", "DMA_MIN_BYTES_GET",
              "DMA_MIN_BYTES_PINNED", "ZC_MAX_BYTES", "FRAME_ZC_MAX_BYTES", "INLINE", "INLINE_ADD_CHUNKS",
              "INLINE_GET_CHUNKS", "ISPIN", "SERVE", "SERVE_IDLE_US", "TILE_SHIFT", "TILE_GRID", "RB_WBITS",
-             "RB_NBD", "RB_TB", "RB_APPLY_LOG2"]
+             "RB_NBD", "RB_TB", "RB_APPLY_LOG2", "RB_BIN_BLOCK"]
     with ps.Shard(0, 1000, np.float32) as sh:
         for n in names:
             sh.set_option(n, sh.get_option(n))  # every default is a valid value
@@ -1348,7 +1348,8 @@ def test_shard_options_api(cuda):
         assert sh.get_option("INLINE_ADD_CHUNKS") == 1
         sh.set_option("ZC_MAX_BYTES", 12345)
         assert sh.get_option("ZC_MAX_BYTES") == 12345
-        for n, bad in (("UNROLL", 5), ("RB_APPLY_LOG2", 12), ("TILE_SHIFT", 3), ("INLINE", 2), ("NOPE", 1)):
+        for n, bad in (("UNROLL", 5), ("RB_APPLY_LOG2", 12), ("TILE_SHIFT", 3), ("INLINE", 2),
+                        ("RB_BIN_BLOCK", 768), ("NOPE", 1)):
             before = sh.get_option(n) if n != "NOPE" else None
             with pytest.raises(PskvError) as ei:
                 sh.set_option(n, bad)

@@ -5,9 +5,14 @@
 #   tests_all    pytest -m gpu (everything)
 #   align        tools/align_probe.py (window phase cost)
 #   emu          bench.py as rank 0 of 8 and of 2 (one rank's cfg-4 share alone)
+#   emu_unroll   rank 0 of 8 at 4 x 4 keys per lane (PSKV_UNROLL=4) and at the default 8
+#   e2e          tools/e2e_probe.py (host-buffer Add / Get against raw PCIe copy rates)
 #   bench        bench.py --steps 20 (the driver's command line)
 #   zipf         tools/zipf_probe.py kernel times on cfg 3
+#   zipf_bin     the same for K5a at 1024- and 512-thread workgroups
 #   profile      tools/gpu_profile.sh: rocprofv3 kernel trace + stats, FETCH / WRITE PMC passes
+#   vector       bench.py --vector-only at 1e6 keys (config 1's VectorStorage restatement, CPU, once)
+#   asan         tools/asan_build.sh (host ASan + UBSan) and the C++ boundary programs under it
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$PWD}
 OUT=$R/gpurun_out/$1
@@ -26,9 +31,29 @@ for step in "$@"; do
            > "$OUT/emu08.json" 2> "$OUT/emu08.err" &&
          PSKV_BENCH_EMULATE=0/2 timeout -k 10 200 python3 "$R/bench.py" --steps 20 --no-zipf --no-cpu-baseline --no-extra \
            > "$OUT/emu02.json" 2> "$OUT/emu02.err" ;;
+    emu_unroll) PSKV_BENCH_EMULATE=0/8 PSKV_UNROLL=4 timeout -k 10 200 python3 "$R/bench.py" --steps 20 --no-zipf \
+           --no-cpu-baseline --no-extra > "$OUT/emu08_u4.json" 2> "$OUT/emu08_u4.err" &&
+         PSKV_BENCH_EMULATE=0/8 timeout -k 10 200 python3 "$R/bench.py" --steps 20 --no-zipf --no-cpu-baseline \
+           --no-extra > "$OUT/emu08_u8.json" 2> "$OUT/emu08_u8.err" ;;
+    e2e) timeout -k 10 200 python3 "$R/tools/e2e_probe.py" > "$OUT/e2e.log" 2>&1 ;;
     bench) timeout -k 10 400 python3 "$R/bench.py" --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     profile) bash "$R/tools/gpu_profile.sh" "$(basename "$OUT")/prof" > "$OUT/profile.log" 2>&1 ;;
     zipf) timeout -k 10 300 python3 "$R/tools/zipf_probe.py" "" "PSKV_GET_DEDUP=1" > "$OUT/zipf.log" 2>&1 ;;
+    zipf_bin) timeout -k 10 300 python3 "$R/tools/zipf_probe.py" "" "PSKV_RB_BIN_BLOCK=1024" "PSKV_RB_BIN_BLOCK=512" \
+        > "$OUT/zipf_bin.log" 2>&1 ;;
+    vector) timeout -k 10 600 python3 -u "$R/bench.py" --vector-only --vector-sizes 1000000 \
+        > "$OUT/vector_1e6.json" 2> "$OUT/vector_1e6.err" ;;
+    asan) SAN=address,undefined timeout -k 10 400 bash "$R/tools/asan_build.sh" > "$OUT/asan_build.log" 2>&1 &&
+        A=$R/scratch/asan && export ASAN_OPTIONS=detect_leaks=0 &&
+        timeout -k 10 200 "$A/hip_storage_test" > "$OUT/asan_hst.log" 2>&1 &&
+        timeout -k 10 200 "$A/kv_client_table_test" --storage hip > "$OUT/asan_kvt.log" 2>&1 &&
+        ASAN_OPTIONS=detect_leaks=0:quarantine_size_mb=0 timeout -k 10 200 "$A/ssp_replay" --known-answers \
+          --model ssp --staleness 3 --iters 8 --shards 8 --workers 4 > "$OUT/asan_replay.log" 2>&1 &&
+        ASAN_OPTIONS=detect_leaks=0:quarantine_size_mb=0 timeout -k 10 200 "$A/ssp_replay" --threads \
+          --partition hash --model bsp --iters 8 --shards 8 --workers 4 --features 200000 \
+          > "$OUT/asan_replay_hash.log" 2>&1 &&
+        { timeout -k 10 200 "$A/ssp_replay" --model ssp --iters 4 --shards 8 --workers 4 \
+            > "$OUT/asan_replay_quarantine.log" 2>&1; echo "default quarantine rc=$?" >> "$OUT/asan_replay_quarantine.log"; } ;;
     *) echo "unknown step $step"; exit 9 ;;
   esac
   rc=$?
