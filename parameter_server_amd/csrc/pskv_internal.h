@@ -25,14 +25,14 @@ constexpr int kGeneralChunk = 2048;  // keys per workgroup in the dedup path
 constexpr int kGeneralSlots = 4096;  // LDS hash slots (load factor <= 1/2)
 constexpr int kRbMaxBuckets = 2064;  // key buckets incl. the out-of-range bucket (>= 2049)
 // K5a workgroup (option RB_BIN_BLOCK): 1024 threads, one per CU.  Two
-// 512-thread workgroups per CU on 4 Ki-key super-chunks measured slower on
-// cfg 3 (K5 164 against 153 us per 8 M Zipf keys, assign; 217 against 204
-// accumulate): the smaller super-chunks keep more duplicate entries and K5b
-// gathers twice as many runs.
+// 512-thread workgroups per CU on 4 Ki-key super-chunks bin at the same rate
+// (K5a 55.0 against 56.0 us per 8 M cfg-3 Zipf keys): K5a is bound by the CU's
+// LDS and issue throughput, not by its barrier phases.  With one run per
+// resolve thread the 512 form needs two launch pieces per 8 M keys, and the
+// whole Add is slower (assign 2 x (32.0 + 58.7) against 56.8 + 86.4 us;
+// profiles/r03_probes/ztrace_k5_split_*.txt).
 constexpr int kRbBinBlockDefault = 1024;
-constexpr uint32_t kRbMaxSc = 2048;  // K5 super-chunks per launch (two runs per resolve thread)
-// super-chunks per launch piece: 8 Mi keys of 4-byte values at either K5a size
-inline uint32_t rb_max_sc(int bin_block) { return bin_block == 512 ? 2048u : 1024u; }
+constexpr uint32_t kRbMaxSc = 1024;  // K5 super-chunks per launch (one run per resolve thread)
 constexpr int kInlineMax = 256;      // keys of an inline (kernarg-carried) Add
 constexpr int kInlineGetMax = 512;   // keys of an inline Get
 constexpr int kInlineMaxChunks = 16;   // inline launches per call at most (reply buffer size)

@@ -1105,7 +1105,8 @@ __device__ __forceinline__ uint32_t rb_local(const RbMap& m, uint32_t off) {
 }
 
 // Block-wide exclusive scan of a[0..n) in LDS, in place (n <= kRbMaxBuckets + 1).
-// Returns the total.  Every thread of the block must call it.
+// Returns the total.  Every thread of the block must call it, after a barrier
+// behind the last write of a[] (a thread reads words other threads wrote).
 template <int BLOCK>
 __device__ __forceinline__ uint32_t block_exscan(uint32_t* a, uint32_t n, uint32_t* wtmp) {
   constexpr int PER = (kRbMaxBuckets + 1 + BLOCK - 1) / BLOCK;
@@ -1333,7 +1334,7 @@ __global__ __launch_bounds__(BINB) void k_rb_bin(GroupArgs ga, DenseView d, RbMa
         lds_add(reinterpret_cast<AT*>(&hv[slot[q]]), from_bits<AT>(to_bits<BT>(vc[q])));
     }
     __syncthreads();
-    uint32_t emask = 0, rk[KPT];
+    uint32_t emask = 0, rk[KPT], bk[KPT];  // bk: the kept entries' buckets
     BT kv[KPT];
 #pragma unroll
     for (int q = 0; q < KPT; ++q) {
@@ -1346,9 +1347,11 @@ __global__ __launch_bounds__(BINB) void k_rb_bin(GroupArgs ga, DenseView d, RbMa
         kv[q] = keep ? from_bits<BT>(to_bits<AT>(*reinterpret_cast<const AT*>(&hv[slot[q]]))) : BT(0);
       }
       rk[q] = 0;
+      bk[q] = 0;
       if (keep) {
         emask |= 1u << q;
-        rk[q] = atomicAdd(&cnt[rb_bucket(d, kc[q], bm)], 1u);
+        bk[q] = rb_bucket(d, kc[q], bm);
+        rk[q] = atomicAdd(&cnt[bk[q]], 1u);
       }
     }
     __syncthreads();  // table read and every entry counted
@@ -1362,7 +1365,7 @@ __global__ __launch_bounds__(BINB) void k_rb_bin(GroupArgs ga, DenseView d, RbMa
       e.key = kc[q];
       if (sizeof(BT) == 8) reinterpret_cast<uint32_t*>(&e)[1] = 0;
       e.val = kv[q];
-      stg[cnt[rb_bucket(d, kc[q], bm)] + rk[q]] = e;
+      stg[cnt[bk[q]] + rk[q]] = e;
     }
     __syncthreads();
     // the staged, bucket-sorted entries out as one coalesced stream.  The
@@ -1403,12 +1406,9 @@ __global__ __launch_bounds__(BINB) void k_rb_bin(GroupArgs ga, DenseView d, RbMa
 // K5b k_rb_resolve: one 1024-thread workgroup per bucket (LDS: 128 KiB table,
 // one workgroup per CU, 16 waves).  The bucket's entries are the runs
 // [loff[sc][b], loff[sc][b+1]) of the super-chunk regions; thread t loads the
-// runs of super-chunk t (nsc <= 1024) or of super-chunks 2t and 2t + 1
-// (nsc <= 2048: K5a's 4 Ki-key super-chunks) straight into registers as ONE
-// virtual run (the second run's entries follow the first's; the few entries
-// past RPT are read in a loop, and a bucket with a virtual run longer than
-// LONG takes the strided path below), and its entries' positions pre[t] + q
-// (pre = exclusive scan of the virtual run lengths) are call order.  An LDS hash resolves the bucket — the largest position wins
+// run of super-chunk t straight into registers (one contiguous read; the few
+// entries past RPT are read in a loop, and a bucket with a run longer than
+// LONG takes the strided path below).  An LDS hash resolves the bucket — the largest position wins
 // (assign) / values add (accumulate) — and the winners store into the dense
 // array or the overflow table.  A bucket is owned by one workgroup: no
 // cross-workgroup ordering, no global atomics.  Buckets are dealt XCD by XCD
@@ -1417,7 +1417,7 @@ __global__ __launch_bounds__(BINB) void k_rb_bin(GroupArgs ga, DenseView d, RbMa
 // bucket's loff words are read while this one resolves.  Slot SLOTS belongs
 // to the key 0xFFFFFFFF.
 constexpr int kApplyBlock = 1024;
-static_assert(kRbMaxSc <= 2u * kApplyBlock, "at most two runs per resolve thread");
+static_assert(kRbMaxSc <= (uint32_t)kApplyBlock, "one run per resolve thread");
 template <typename AT, typename BT, int MODE, int LOGS>
 __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, RbMap bm,
                                                             uint32_t nbk,
@@ -1436,20 +1436,35 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
   __shared__ __attribute__((aligned(16))) uint32_t ak[MODE == 0 ? 2 * SLOTS + 8 : SLOTS + 1];
   uint32_t* abest = ak + SLOTS + 4;  // 16-byte aligned
   __shared__ __attribute__((aligned(16))) AT asum[MODE == 1 ? SLOTS + 1 : 1];
+  // Positions.  K5a keeps ONE entry per key per super-chunk (its last value /
+  // its sum), so inside a run every key is distinct and the run's super-chunk
+  // index alone orders two entries of a key: the later super-chunk is the
+  // later write.  Assign therefore ranks entries by run index (no scan of the
+  // run lengths is needed to order them); only the strided path scans, to
+  // deal positions to threads.
   // assign, dense buckets: a direct-indexed table best[key offset in the
-  // bucket's DSPAN-key window] = tag << kPosBits | (1 + position); the tag
+  // bucket's DSPAN-key window] = tag << kPosBits | (1 + run index); the tag
   // grows every pass, so stale values always lose and the table is never
   // cleared between buckets (only after a hash-path bucket used the memory)
   constexpr uint32_t DSPAN = MODE == 0 ? 2u * SLOTS : 1u;
   constexpr uint32_t kPosBits = 18;
   uint32_t* best = ak;
-  // virtual-run starts (positions; the scan's array), then, in the strided
-  // path, the starts of the nsc runs (pre[nsc] = entries)
+  // strided path: the starts of the nsc runs in position order (pre[nsc] =
+  // entries)
   __shared__ uint32_t pre[kRbMaxSc + 1];
   __shared__ __attribute__((aligned(16))) uint32_t wtmp[kApplyBlock / 64];
   __shared__ uint32_t sent;
+  // per-bucket totals (entries, longest virtual run), three slots in rotation:
+  // iteration i adds into slot i % 3 and clears slot (i + 2) % 3, which was
+  // last read in iteration i - 1, before this iteration's barrier
+  __shared__ uint32_t s_tot[3], s_max[3];
   const int tid = threadIdx.x;
   const uint32_t nbd = bm.nbd;
+  if (tid < 3) {
+    s_tot[tid] = 0;
+    s_max[tid] = 0;
+  }
+  __syncthreads();
   auto find = [&](uint32_t key) -> uint32_t {
     if (key == kEmpty32) return SLOTS;
     uint32_t h = fmix32(key) & (SLOTS - 1);
@@ -1546,45 +1561,24 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
   const uint32_t per_xcd = (gridDim.x + 7u - xcd) >> 3;  // workgroups in this XCD group
   const uint32_t b_hi = (uint32_t)((uint64_t)nbk * (xcd + 1) / 8);
   uint32_t b = (uint32_t)((uint64_t)nbk * xcd / 8) + (blockIdx.x >> 3);
-  // this thread's runs: super-chunk r0 and, with two runs per thread, r0 + 1
-  const uint32_t rpt = nsc > (uint32_t)kApplyBlock ? 2u : 1u;  // uniform
-  const uint32_t r0 = (uint32_t)tid * rpt;
-  const bool has_run = r0 < nsc, has_run2 = rpt == 2u && r0 + 1u < nsc;
-  const uint32_t rowo = has_run ? r0 * (nbk + 1) : 0u;    // this thread's loff rows
-  const uint32_t rowo2 = has_run2 ? rowo + nbk + 1 : 0u;
-  const uint32_t st1 = r0 * SC, st2 = (r0 + 1u) * SC;   // the runs' regions in tmp
-  // software pipeline: the runs of bucket b in registers, the run bounds of
-  // the bucket after it in flight.  The bounds loads are unconditional (a
-  // thread without a run, or past the last bucket, reads a valid word it then
+  const bool has_run = (uint32_t)tid < nsc;
+  const uint32_t rowo = has_run ? (uint32_t)tid * (nbk + 1) : 0u;  // this thread's loff row
+  const uint32_t st0 = (uint32_t)tid * SC;                           // its region in tmp
+  const uint32_t pos = (uint32_t)tid + 1u;  // its run index (the entries' position), plus one
+  // software pipeline: the run of bucket b in registers, the run bounds of the
+  // bucket after it in flight.  The bounds loads are unconditional (a thread
+  // without a run, or past the last bucket, reads a valid word it then
   // ignores) so nothing waits for them until the next bucket uses them.
-  struct Rb {
-    uint32_t a, e, a2, e2;
-  };
   auto bounds_ok = [&](uint32_t bb) { return bb < b_hi && has_run; };
-  auto bounds = [&](uint32_t bb, Rb& r) {
-    const uint32_t c = bb < b_hi ? bb : 0u;
-    r.a = loff[rowo + c];
-    r.e = loff[rowo + c + 1];
-    r.a2 = r.e2 = 0;
-    if (rpt == 2u) {  // uniform
-      r.a2 = loff[rowo2 + c];
-      r.e2 = loff[rowo2 + c + 1];
-    }
+  auto bounds = [&](uint32_t bb, uint32_t& a, uint32_t& e) {
+    const uint32_t i = rowo + (bb < b_hi ? bb : 0u);
+    a = loff[i];
+    e = loff[i + 1];
   };
-  auto none = [&](Rb& r, bool keep, bool keep2) {
-    if (!keep) r.a = r.e = 0;
-    if (!keep2) r.a2 = r.e2 = 0;
-  };
-  // entry q of the virtual run: the first run's entries, then the second's
-  auto ent_at = [&](const Rb& r, uint32_t q) -> uint32_t {
-    const uint32_t l1 = r.e - r.a;
-    return q < l1 ? st1 + r.a + q : st2 + r.a2 + (q - l1);
-  };
-  auto load_run = [&](const Rb& r, Ent (&x)[RPT]) {
-    const uint32_t len = (r.e - r.a) + (r.e2 - r.a2);
+  auto load_run = [&](uint32_t a, uint32_t e, Ent (&x)[RPT]) {
 #pragma unroll
     for (int q = 0; q < RPT; ++q)
-      if ((uint32_t)q < len) x[q] = tmp[ent_at(r, (uint32_t)q)];
+      if ((uint32_t)q < e - a) x[q] = tmp[st0 + a + q];
   };
   uint32_t dlog = 0;
   while ((1u << dlog) < DSPAN) ++dlog;
@@ -1595,30 +1589,45 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
     for (uint32_t i = (uint32_t)tid * 4; i < DSPAN; i += kApplyBlock * 4)
       *reinterpret_cast<u32x4*>(&best[i]) = u32x4{0u, 0u, 0u, 0u};
   };
-  Rb cr, nr;
-  bounds(b, cr);
-  none(cr, bounds_ok(b), bounds_ok(b) && has_run2);
-  bounds(b + per_xcd, nr);
+  uint32_t ra, re, na, ne_;
+  bounds(b, ra, re);
+  if (!bounds_ok(b)) ra = re = 0;
+  bounds(b + per_xcd, na, ne_);
   Ent xn[RPT];
-  load_run(cr, xn);
-  for (; b < b_hi; b += per_xcd) {
-    const Rb r = cr;
-    const uint32_t len = (r.e - r.a) + (r.e2 - r.a2);
+  load_run(ra, re, xn);
+  uint32_t it = 0;
+  for (; b < b_hi; b += per_xcd, it = it == 2u ? 0u : it + 1u) {
+    const uint32_t len = re - ra, st = st0 + ra;
     Ent x[RPT];
 #pragma unroll
     for (int q = 0; q < RPT; ++q) x[q] = xn[q];
     // next bucket: its run loads now, the bounds of the one after
-    cr = nr;
-    none(cr, bounds_ok(b + per_xcd), bounds_ok(b + per_xcd) && has_run2);
-    load_run(cr, xn);
-    bounds(b + 2 * per_xcd, nr);
-    pre[tid] = len;
-    const bool long_run = __syncthreads_or(len > LONG) != 0;
-    const uint32_t ne = block_exscan<kApplyBlock>(pre, kApplyBlock, wtmp);
-    const uint32_t p0 = pre[tid];
+    ra = bounds_ok(b + per_xcd) ? na : 0u;
+    re = bounds_ok(b + per_xcd) ? ne_ : 0u;
+    load_run(ra, re, xn);
+    bounds(b + 2 * per_xcd, na, ne_);
+    {
+      uint32_t ws = len, wm = len;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        ws += __shfl_xor(ws, o, 64);
+        wm = max(wm, (uint32_t)__shfl_xor(wm, o, 64));
+      }
+      if ((tid & 63) == 0 && ws != 0) {
+        atomicAdd(&s_tot[it], ws);
+        atomicMax(&s_max[it], wm);
+      }
+    }
+    __syncthreads();
+    const uint32_t ne = s_tot[it];
+    const bool long_run = s_max[it] > LONG;
+    if (tid == 0) {
+      const uint32_t z = it == 0u ? 2u : it - 1u;  // (it + 2) % 3
+      s_tot[z] = 0;
+      s_max[z] = 0;
+    }
     if (ne == 0) continue;  // uniform
-    const bool direct = MODE == 0 && b != nbd && !long_run && halves <= 4 &&
-                        ne < (1u << kPosBits) - 1u;
+    const bool direct = MODE == 0 && b != nbd && !long_run && halves <= 4;
     if (direct) {
       uint32_t rel[RPT];
 #pragma unroll
@@ -1638,20 +1647,19 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
 #pragma unroll
         for (int q = 0; q < RPT; ++q)
           if ((uint32_t)q < len && (rel[q] >> dlog) == h)
-            atomicMax(&best[rel[q] & (DSPAN - 1)], tg | (p0 + (uint32_t)q + 1u));
+            atomicMax(&best[rel[q] & (DSPAN - 1)], tg | pos);
         for (uint32_t q = RPT; q < len; ++q) {  // a run's short tail, from memory
-          const uint32_t rl = rb_local(bm, tmp[ent_at(r, q)].key - d.key_begin);
-          if ((rl >> dlog) == h) atomicMax(&best[rl & (DSPAN - 1)], tg | (p0 + q + 1u));
+          const uint32_t rl = rb_local(bm, tmp[st + q].key - d.key_begin);
+          if ((rl >> dlog) == h) atomicMax(&best[rl & (DSPAN - 1)], tg | pos);
         }
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < RPT; ++q)
-          if ((uint32_t)q < len && (rel[q] >> dlog) == h &&
-              best[rel[q] & (DSPAN - 1)] == (tg | (p0 + (uint32_t)q + 1u)))
+          if ((uint32_t)q < len && (rel[q] >> dlog) == h && best[rel[q] & (DSPAN - 1)] == (tg | pos))
             win |= 1ull << q;
         for (uint32_t q = RPT; q < len; ++q) {
-          const uint32_t rl = rb_local(bm, tmp[ent_at(r, q)].key - d.key_begin);
-          if ((rl >> dlog) == h && best[rl & (DSPAN - 1)] == (tg | (p0 + q + 1u))) win |= 1ull << q;
+          const uint32_t rl = rb_local(bm, tmp[st + q].key - d.key_begin);
+          if ((rl >> dlog) == h && best[rl & (DSPAN - 1)] == (tg | pos)) win |= 1ull << q;
         }
         if (h + 1 < halves) __syncthreads();  // the table is read before the next pass
       }
@@ -1660,7 +1668,7 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
         if (win >> q & 1u) store_winner(b, x[q].key, (BT)x[q].val);
       for (uint32_t q = RPT; q < len; ++q)
         if (win >> q & 1u) {
-          const Ent y = tmp[ent_at(r, q)];
+          const Ent y = tmp[st + q];
           store_winner(b, y.key, (BT)y.val);
         }
       // the next bucket's first atomics come after its scan's barriers, so
@@ -1682,23 +1690,23 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
       for (int q = 0; q < RPT; ++q) {
         if (!(valid >> q & 1u)) continue;
         if (MODE == 0)
-          atomicMax(&abest[slot[q]], p0 + (uint32_t)q + 1u);
+          atomicMax(&abest[slot[q]], pos);
         else
           lds_add(&asum[slot[q]], from_bits<AT>(to_bits<BT>((BT)x[q].val)));
       }
       for (uint32_t q = RPT; q < len; ++q) {  // a run's short tail (<= LONG - RPT), from memory
-        const Ent y = tmp[ent_at(r, q)];
-        insert_one(y.key, p0 + q, (BT)y.val);
+        const Ent y = tmp[st + q];
+        insert_one(y.key, pos - 1u, (BT)y.val);
       }
       __syncthreads();
       if (MODE == 0) {
 #pragma unroll
         for (int q = 0; q < RPT; ++q)
-          if ((valid >> q & 1u) && abest[slot[q]] == p0 + (uint32_t)q + 1u)
+          if ((valid >> q & 1u) && abest[slot[q]] == pos)
             store_winner(b, key[q], (BT)x[q].val);
         for (uint32_t q = RPT; q < len; ++q) {
-          const Ent y = tmp[ent_at(r, q)];
-          if (abest[find(y.key)] == p0 + q + 1u) store_winner(b, y.key, (BT)y.val);
+          const Ent y = tmp[st + q];
+          if (abest[find(y.key)] == pos) store_winner(b, y.key, (BT)y.val);
         }
       } else {
         accumulate_all(b);
@@ -1710,10 +1718,11 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
       // inside long runs), found by binary search over the starts of the nsc
       // runs (pre, rewritten per run); rounds split an oversized bucket by key
       // hash.  Run j's entries start at j * SC + its loff word.
-      __syncthreads();  // every p0 read before pre changes meaning
-      if (has_run) pre[r0] = p0;
-      if (has_run2) pre[r0 + 1] = p0 + (r.e - r.a);
+      pre[tid] = len;
+      __syncthreads();  // block_exscan reads other threads' words first
+      (void)block_exscan<kApplyBlock>(pre, kApplyBlock, wtmp);
       if (tid == 0) pre[nsc] = ne;
+      __syncthreads();
       auto run_ent = [&](uint32_t j, uint32_t p) -> Ent {
         return tmp[j * SC + loff[j * (nbk + 1) + b] + (p - pre[j])];
       };
@@ -1722,16 +1731,18 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
         clear_table();
         __syncthreads();
         for (uint32_t p = tid; p < ne; p += kApplyBlock) {
-          const Ent y = run_ent(first_run(p), p);
-          if ((fmix32(y.key ^ 0x9E3779B9u) % R) == round) insert_one(y.key, p, (BT)y.val);
+          const uint32_t j = first_run(p);
+          const Ent y = run_ent(j, p);
+          if ((fmix32(y.key ^ 0x9E3779B9u) % R) == round) insert_one(y.key, j, (BT)y.val);
         }
         __syncthreads();
         if (MODE == 0) {
           // the entry holding its key's largest position is the last write
           for (uint32_t p = tid; p < ne; p += kApplyBlock) {
-            const Ent y = run_ent(first_run(p), p);
+            const uint32_t j = first_run(p);
+            const Ent y = run_ent(j, p);
             if ((fmix32(y.key ^ 0x9E3779B9u) % R) != round) continue;
-            if (abest[find(y.key)] == p + 1u) store_winner(b, y.key, (BT)y.val);
+            if (abest[find(y.key)] == j + 1u) store_winner(b, y.key, (BT)y.val);
           }
         } else {
           accumulate_all(b);

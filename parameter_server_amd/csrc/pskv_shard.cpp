@@ -701,7 +701,7 @@ int ensure_scratch(pskv_shard* s, void** p, size_t* have, size_t need) {
 }
 
 // K5: radix-bucket general Add (no random global atomics), one launch pair
-// per <= rb_max_sc super-chunks; a longer group is cut into consecutive pieces
+// per <= kRbMaxSc super-chunks; a longer group is cut into consecutive pieces
 // (a batch may be split), which run in stream order, so call order holds.
 int radix_launch(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t e) {
   GroupArgs ga;
@@ -740,7 +740,7 @@ int radix_launch(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size
   int apply_log2 = elems / nbd <= 2048 ? 13 : 14;
   if (s->tune_rb_apply_log2) apply_log2 = s->tune_rb_apply_log2;
   if (nbk > (uint32_t)kRbMaxBuckets) return fail(PSKV_EINVAL, "radix path: too many buckets");
-  if (nsc > rb_max_sc(s->tune_rb_bin_block)) return fail(PSKV_EINVAL, "radix path: launch piece too large");
+  if (nsc > kRbMaxSc) return fail(PSKV_EINVAL, "radix path: launch piece too large");
   const size_t eb = rb_entry_bytes(s->vb);
   int rc = ensure_scratch(s, reinterpret_cast<void**>(&s->rb_loff), &s->rb_loff_bytes,
                           (size_t)nsc * (nbk + 1) * sizeof(uint16_t));
@@ -760,7 +760,7 @@ int radix_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t 
   const uint64_t sc = rb_superchunk(s->vb, s->tune_rb_bin_block);
   uint64_t nsc = 0;
   for (size_t i = b; i < e; ++i) nsc += (v[i].n + sc - 1) / sc;
-  const uint64_t max_sc = rb_max_sc(s->tune_rb_bin_block);
+  const uint64_t max_sc = kRbMaxSc;
   if (nsc <= max_sc) return radix_launch(s, v, b, e);
   // pieces of whole super-chunks, each <= max_sc of them
   std::vector<pskv_batch> piece;
