@@ -1575,10 +1575,29 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
     a = loff[i];
     e = loff[i + 1];
   };
+  // 8-byte entries go two per 16-byte load (dword alignment suffices): half
+  // the load instructions, and each lane of one touches a line of its own
+  // run, so the address unit's work per bucket halves too.  A run of odd
+  // length reads one entry past its end: the next run's, or the scratch
+  // buffer's tail pad (launch_rb_add's caller allocates kRbTmpPad bytes more).
   auto load_run = [&](uint32_t a, uint32_t e, Ent (&x)[RPT]) {
+    if constexpr (sizeof(Ent) == 8) {
+      static_assert(RPT % 2 == 0, "whole pairs");
 #pragma unroll
-    for (int q = 0; q < RPT; ++q)
-      if ((uint32_t)q < e - a) x[q] = tmp[st0 + a + q];
+      for (int q = 0; q < RPT; q += 2)
+        if ((uint32_t)q < e - a) {
+          uint32_t w[4];
+          ld16a4<false>(reinterpret_cast<const uint32_t*>(tmp + st0 + a + q), w);
+          x[q].key = w[0];
+          reinterpret_cast<uint32_t*>(&x[q])[1] = w[1];
+          x[q + 1].key = w[2];
+          reinterpret_cast<uint32_t*>(&x[q + 1])[1] = w[3];
+        }
+    } else {
+#pragma unroll
+      for (int q = 0; q < RPT; ++q)
+        if ((uint32_t)q < e - a) x[q] = tmp[st0 + a + q];
+    }
   };
   uint32_t dlog = 0;
   while ((1u << dlog) < DSPAN) ++dlog;

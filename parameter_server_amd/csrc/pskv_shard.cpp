@@ -746,7 +746,7 @@ int radix_launch(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size
                           (size_t)nsc * (nbk + 1) * sizeof(uint16_t));
   if (!rc)
     rc = ensure_scratch(s, &s->rb_ent, &s->rb_ent_bytes,
-                        (size_t)nsc * rb_superchunk(s->vb, s->tune_rb_bin_block) * eb);
+                        (size_t)nsc * rb_superchunk(s->vb, s->tune_rb_bin_block) * eb + kRbTmpPad);
   if (rc) return rc;
   LaunchTimer t(s, PSKV_K_RADIX, elems);
   PSKV_HIP(launch_rb_add(s->dtype, s->mode, ga, nsc, s->dview(), s->ovf, bm, apply_log2,
