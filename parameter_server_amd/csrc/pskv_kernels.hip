@@ -1216,6 +1216,17 @@ __device__ __forceinline__ void ready(const T (&x)[N]) {
 //   row    the bucket starts go out as one 16-bit row loff[sc][0..nbk]
 //          (loff[sc][nbk] = the entry count)
 // Every global access is a coalesced 16-byte stream; no global atomics.
+// Diagnostic build only (-DPSKV_K5_STAMPS, tools/micro/k5_phases.cpp): the
+// shader-clock time at each phase boundary of the first 8 passes of every K5a
+// / K5b workgroup, read back through pskv_diag_k5_stamps.
+#ifdef PSKV_K5_STAMPS
+__device__ unsigned long long g_k5_stamps[2][512 * 8 * 8];
+#define K5_STAMP(K, IT, PH) \
+  if (threadIdx.x == 0 && (IT) < 8u) g_k5_stamps[K][(blockIdx.x * 8u + (IT)) * 8u + (PH)] = __builtin_readcyclecounter()
+#else
+#define K5_STAMP(K, IT, PH) (void)0
+#endif
+
 template <typename BT>
 constexpr uint32_t rb_sc(int binb) {
   return (sizeof(BT) == 8 ? 4u : 8u) * (uint32_t)binb;
@@ -1308,7 +1319,8 @@ __global__ __launch_bounds__(BINB) void k_rb_bin(GroupArgs ga, DenseView d, RbMa
   }
   ready(kc);  // complete on entry as on the back edge: no wait at the loop top
   ready(vc);
-  for (uint32_t sc = blockIdx.x; sc < nsc; sc += gridDim.x) {
+  for (uint32_t sc = blockIdx.x, pass = 0; sc < nsc; sc += gridDim.x, ++pass) {
+    K5_STAMP(0, pass, 0);
     // kc / vc are complete here (waited for at the end of the previous pass,
     // before its copy-out stores; the prologue's loads by the compiler): the
     // wait-count pass cannot count the next loads (their number depends on the
@@ -1334,6 +1346,7 @@ __global__ __launch_bounds__(BINB) void k_rb_bin(GroupArgs ga, DenseView d, RbMa
         lds_add(reinterpret_cast<AT*>(&hv[slot[q]]), from_bits<AT>(to_bits<BT>(vc[q])));
     }
     __syncthreads();
+    K5_STAMP(0, pass, 1);
     uint32_t emask = 0, rk[KPT], bk[KPT];  // bk: the kept entries' buckets
     BT kv[KPT];
 #pragma unroll
@@ -1355,7 +1368,9 @@ __global__ __launch_bounds__(BINB) void k_rb_bin(GroupArgs ga, DenseView d, RbMa
       }
     }
     __syncthreads();  // table read and every entry counted
+    K5_STAMP(0, pass, 2);
     const uint32_t total = block_exscan<kBinBlock>(cnt, nbk + 1, wtmp);
+    K5_STAMP(0, pass, 3);
     uint16_t* row = loff + (size_t)sc * (nbk + 1);
     for (uint32_t b = tid; b <= nbk; b += kBinBlock) row[b] = (uint16_t)cnt[b];
 #pragma unroll
@@ -1368,6 +1383,7 @@ __global__ __launch_bounds__(BINB) void k_rb_bin(GroupArgs ga, DenseView d, RbMa
       stg[cnt[bk[q]] + rk[q]] = e;
     }
     __syncthreads();
+    K5_STAMP(0, pass, 4);
     // the staged, bucket-sorted entries out as one coalesced stream.  The
     // thread that copies a 16-byte piece also returns it to its cleared state
     // (hv zero, hk EMPTY; nobody else reads it), the pieces past the staged
@@ -1394,6 +1410,7 @@ __global__ __launch_bounds__(BINB) void k_rb_bin(GroupArgs ga, DenseView d, RbMa
     }
     for (uint32_t b = tid; b <= nbk; b += kBinBlock) cnt[b] = 0;
     __syncthreads();
+    K5_STAMP(0, pass, 5);
 #pragma unroll
     for (int q = 0; q < KPT; ++q) {
       kc[q] = kn[q];
@@ -1615,7 +1632,8 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
   Ent xn[RPT];
   load_run(ra, re, xn);
   uint32_t it = 0;
-  for (; b < b_hi; b += per_xcd, it = it == 2u ? 0u : it + 1u) {
+  for (uint32_t pass = 0; b < b_hi; b += per_xcd, it = it == 2u ? 0u : it + 1u, ++pass) {
+    K5_STAMP(1, pass, 0);
     const uint32_t len = re - ra, st = st0 + ra;
     Ent x[RPT];
 #pragma unroll
@@ -1638,6 +1656,7 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
       }
     }
     __syncthreads();
+    K5_STAMP(1, pass, 1);
     const uint32_t ne = s_tot[it];
     const bool long_run = s_max[it] > LONG;
     if (tid == 0) {
@@ -1682,6 +1701,7 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
         }
         if (h + 1 < halves) __syncthreads();  // the table is read before the next pass
       }
+      K5_STAMP(1, pass, 2);
 #pragma unroll
       for (int q = 0; q < RPT; ++q)
         if (win >> q & 1u) store_winner(b, x[q].key, (BT)x[q].val);
@@ -2645,3 +2665,14 @@ hipError_t launch_inline_get(int vb, const InlineGet& a, const DenseView& d, con
 }
 
 }  // namespace pskv
+
+#ifdef PSKV_K5_STAMPS
+// Diagnostic build only: copy out (then clear) the K5 phase stamps, 2 x 512 x 8
+// x 8 u64 ([K5a|K5b][workgroup][pass][phase], 0 = not reached).
+extern "C" int pskv_diag_k5_stamps(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pskv::g_k5_stamps), sizeof(pskv::g_k5_stamps)) != hipSuccess) return -2;
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(pskv::g_k5_stamps)) != hipSuccess) return -2;
+  return hipMemset(p, 0, sizeof(pskv::g_k5_stamps)) == hipSuccess ? 0 : -2;
+}
+#endif

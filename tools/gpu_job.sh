@@ -8,6 +8,7 @@
 #   emu_unroll   rank 0 of 8 at 4 x 4 keys per lane (PSKV_UNROLL=4) and at the default 8
 #   ztrace       rocprofv3 kernel trace of zipf_probe at K5a 1024 and 512 threads (K5a / K5b split)
 #   zpmc         tools/zipf_pmc.sh: wave-state, LDS and HBM counters of the cfg-3 path
+#   k5phases     tools/micro/k5_phases (diagnostic build: K5a / K5b phase stamps), assign and accumulate
 #   e2e          tools/e2e_probe.py (host-buffer Add / Get against raw PCIe copy rates)
 #   bench        bench.py --steps 20 (the driver's command line)
 #   zipf         tools/zipf_probe.py kernel times on cfg 3
@@ -42,6 +43,9 @@ for step in "$@"; do
             -o run -- python3 "$R/tools/zipf_probe.py" > "$OUT/ztrace_$v.log" 2>&1 || exit 1
         done ;;
     zpmc) timeout -k 10 600 bash "$R/tools/zipf_pmc.sh" "$(basename "$OUT")/zpmc" > "$OUT/zpmc.log" 2>&1 ;;
+    k5phases) timeout -k 10 200 "$R/tools/micro/k5_phases" 0 > "$OUT/k5_phases_assign.log" 2>&1 &&
+        timeout -k 10 200 "$R/tools/micro/k5_phases" 1 > "$OUT/k5_phases_accumulate.log" 2>&1 ;;
+    ldsrand) timeout -k 10 120 "$R/tools/micro/lds_atomic_rand" > "$OUT/lds_atomic_rand.log" 2>&1 ;;
     e2e) timeout -k 10 200 python3 "$R/tools/e2e_probe.py" > "$OUT/e2e.log" 2>&1 ;;
     bench) timeout -k 10 400 python3 "$R/bench.py" --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     profile) bash "$R/tools/gpu_profile.sh" "$(basename "$OUT")/prof" > "$OUT/profile.log" 2>&1 ;;
