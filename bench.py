@@ -695,6 +695,17 @@ def zipf_sparse(rank, world, dev, lo, hi, B, steps, J=8):
         b = add_b if n.startswith("k_rb") else get_b
         kernels[n] = {"avg_ms": ms, "algorithmic_bytes": b, "GB/s": b / (ms * 1e-3) / 1e9,
                       "frac": b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    floor = random_access_floor(zb, lo, space, dev)
+    k5_ms = kernels["k_rb_bin+k_rb_resolve (K5 Add)"]["avg_ms"]
+    k1_ms = kernels["k_gather (K1 Get)"]["avg_ms"]
+    # the floor of each kernel: one random access per distinct key (the same
+    # keys, each touched once, caches flushed) plus its streaming bytes at the
+    # dense kernels' measured rate
+    stream_gbs = 6500.0
+    floor["K5_floor_ms"] = floor["scatter_ms"] + J * B * (4 + V) / stream_gbs / 1e6
+    floor["K1_floor_ms"] = floor["gather_ms"] + J * B * (4 + V) / stream_gbs / 1e6
+    floor["K5_frac_of_floor"] = floor["K5_floor_ms"] / k5_ms
+    floor["K1_frac_of_floor"] = floor["K1_floor_ms"] / k1_ms
     return {
         "workload": f"cfg 3 sparse: {J} x {B} unsorted Zipf(0.99) pushes then the same pulls per step per GPU "
                     f"over a {space:.3g}-key range shard, assign mode (K5 key buckets + K1 gather)",
@@ -706,8 +717,66 @@ def zipf_sparse(rank, world, dev, lo, hi, B, steps, J=8):
                      "note": "algorithmic bytes (SURVEY §8d, u = distinct keys) per GPU per second; "
                              "random single-value accesses fetch whole lines, so the line traffic is higher"},
         "kernels": kernels,
+        "random_access_floor": floor,
         "unique_keys_per_batch": uniq, "distinct_keys_per_step": u_all,
         "bytes_per_step_per_gpu": add_b + get_b}, zb
+
+
+def random_access_floor(zb, lo, space, dev, reps=5):
+    """The random-access ceiling the cfg-3 kernels work against, measured on
+    this box: the step's distinct keys, each touched ONCE in random order, by
+    the gather / scatter kernels of tools/micro/random_access.hip (16 offsets
+    per lane in flight) on a fresh float array of the shard's size, with L2
+    and the 256 MB Infinity Cache flushed by a read of 1 GiB before every
+    timed op.  A random single-value access costs a DRAM row activation and a
+    64-byte sector (stores: a partial-line merge), so this rate -- not 8 TB/s
+    -- bounds a key-at-a-time kernel; the K5 / K1 floors add their streaming
+    bytes.  Measurement infrastructure, not the product (libpskv never calls
+    it)."""
+    import ctypes
+
+    import torch
+
+    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "micro", "librandom_access.so"))
+    keys = torch.unique(torch.cat([k for k, _ in zb]).to(torch.int64) - lo)
+    g = torch.Generator(device=dev)
+    g.manual_seed(11)
+    idx = keys[torch.randperm(keys.numel(), device=dev, generator=g)].to(torch.int32)
+    u = idx.numel()
+    assert int(idx.min()) >= 0 and int(idx.max()) < space
+    arr = torch.zeros(space, dtype=torch.float32, device=dev)
+    vals = torch.rand(u, device=dev, generator=g)
+    out = torch.empty(u, dtype=torch.float32, device=dev)
+    # a read-only sweep of 1 GiB evicts L2 and the Infinity Cache without
+    # leaving dirty lines for the timed kernel to write back (a fill would)
+    flush = torch.ones(1 << 28, dtype=torch.float32, device=dev)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    res = {"gather_ms": [], "scatter_ms": []}
+    for r in range(reps + 1):
+        for name in ("gather_ms", "scatter_ms"):
+            flush.sum()
+            ev[0].record()
+            if name == "gather_ms":
+                rc = lib.ra_gather(ctypes.c_void_p(idx.data_ptr()), ctypes.c_uint32(u),
+                                   ctypes.c_void_p(arr.data_ptr()), ctypes.c_void_p(out.data_ptr()), st)
+            else:
+                rc = lib.ra_scatter(ctypes.c_void_p(idx.data_ptr()), ctypes.c_uint32(u),
+                                    ctypes.c_void_p(vals.data_ptr()), ctypes.c_void_p(arr.data_ptr()), st)
+            ev[1].record()
+            torch.cuda.synchronize()
+            assert rc == 0, f"random_access {name}: hip error {rc}"
+            if r:
+                res[name].append(ev[0].elapsed_time(ev[1]))
+    assert torch.equal(out, arr.index_select(0, idx.long())), "random_access gather check"
+    del out, flush, arr
+    rec = {"distinct_keys": u, "how": "tools/micro/random_access.hip gather / scatter of the step's distinct "
+                                      "keys, each once, random order, caches flushed; median of %d" % reps}
+    for name in ("gather_ms", "scatter_ms"):
+        ms = float(np.median(res[name]))
+        rec[name] = ms
+        rec[name.replace("_ms", "_G_accesses/s")] = u / (ms * 1e-3) / 1e9
+    return rec
 
 
 def variant_f64(rank, world, J, B, dev, R, steps, lo, hi):

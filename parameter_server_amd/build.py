@@ -80,11 +80,23 @@ def build_oracle():
         sys.path.pop(0)
 
 
+RA_SRC = os.path.join(ROOT, "tools", "micro", "random_access.hip")
+RA_OUT = os.path.join(ROOT, "tools", "micro", "librandom_access.so")
+
+
+def build_random_access(force=False):
+    """bench.py's random-access calibration (not part of libpskv)."""
+    if force or _stale(RA_OUT, [RA_SRC]):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", RA_SRC, "-o", RA_OUT])
+    return RA_OUT
+
+
 def build_all(force=False):
     lib = build_lib(force)
     orc = build_oracle()
     progs = build_cpp_tests(force)
-    return {"lib": lib, "cpp": progs, "oracle": orc}
+    ra = build_random_access(force)
+    return {"lib": lib, "cpp": progs, "oracle": orc, "random_access": ra}
 
 
 if __name__ == "__main__":

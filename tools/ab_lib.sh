@@ -1,7 +1,9 @@
 #!/bin/bash
 # A/B two builds of libpskv.so on one box (ab/libpskv_base.so, ab/libpskv_new.so,
-# built beforehand): alternate them under bench.py
-# (swapping the in-tree library file), N rounds each.
+# built beforehand): alternate them (swapping the in-tree library file), 3
+# rounds each, under bench.py (default) or, with AB_PROG=zipf, under
+# tools/zipf_probe.py (the cfg-3 K5 / K1 kernel times).
+#   bash tools/ab_lib.sh OUTNAME ["bench.py args"]
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$PWD}
 OUT=$R/gpurun_out/${1:-ab}
@@ -10,7 +12,11 @@ mkdir -p "$OUT"
 for i in 1 2 3; do
   for v in base new; do
     cp "$R/ab/libpskv_$v.so" "$R/parameter_server_amd/libpskv.so" || exit 1
-    timeout -k 10 200 python3 "$R/bench.py" $ARGS > "$OUT/$v$i.json" 2> "$OUT/$v$i.err" || exit 2
+    if [ "${AB_PROG:-bench}" = zipf ]; then
+      timeout -k 10 200 python3 "$R/tools/zipf_probe.py" > "$OUT/$v$i.log" 2>&1 || exit 2
+    else
+      timeout -k 10 200 python3 "$R/bench.py" $ARGS > "$OUT/$v$i.json" 2> "$OUT/$v$i.err" || exit 2
+    fi
   done
 done
 cp "$R/ab/libpskv_new.so" "$R/parameter_server_amd/libpskv.so"

@@ -9,6 +9,7 @@
 #   ztrace       rocprofv3 kernel trace of zipf_probe at K5a 1024 and 512 threads (K5a / K5b split)
 #   zpmc         tools/zipf_pmc.sh: wave-state, LDS and HBM counters of the cfg-3 path
 #   k5phases     tools/micro/k5_phases (diagnostic build: K5a / K5b phase stamps), assign and accumulate
+#   abz          tools/ab_lib.sh with AB_PROG=zipf: ab/libpskv_base.so vs ab/libpskv_new.so on cfg 3, 3 rounds each
 #   e2e          tools/e2e_probe.py (host-buffer Add / Get against raw PCIe copy rates)
 #   bench        bench.py --steps 20 (the driver's command line)
 #   zipf         tools/zipf_probe.py kernel times on cfg 3
@@ -26,7 +27,7 @@ for step in "$@"; do
   case $step in
     tests_focus) timeout -k 10 300 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread \
         "$R/tests/test_gpu_parity.py" "$R/tests/test_replay.py" \
-        -k "phase or dense or lookalike or repaired or hint or golden or replay or options or dedup or zipf" > "$OUT/tests_focus.log" 2>&1 ;;
+        -k "phase or dense or lookalike or repaired or hint or golden or replay or options or dedup or zipf or radix or sentinel or random" > "$OUT/tests_focus.log" 2>&1 ;;
     tests_all) timeout -k 10 900 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread "$R/tests" -m gpu \
         > "$OUT/tests_all.log" 2>&1 ;;
     align) timeout -k 10 200 python3 "$R/tools/align_probe.py" 0,1,2,3 20 > "$OUT/align.log" 2>&1 ;;
@@ -46,6 +47,7 @@ for step in "$@"; do
     k5phases) timeout -k 10 200 "$R/tools/micro/k5_phases" 0 > "$OUT/k5_phases_assign.log" 2>&1 &&
         timeout -k 10 200 "$R/tools/micro/k5_phases" 1 > "$OUT/k5_phases_accumulate.log" 2>&1 ;;
     ldsrand) timeout -k 10 120 "$R/tools/micro/lds_atomic_rand" > "$OUT/lds_atomic_rand.log" 2>&1 ;;
+    abz) AB_PROG=zipf timeout -k 10 900 bash "$R/tools/ab_lib.sh" "$(basename "$OUT")/abz" > "$OUT/abz.log" 2>&1 ;;
     e2e) timeout -k 10 200 python3 "$R/tools/e2e_probe.py" > "$OUT/e2e.log" 2>&1 ;;
     bench) timeout -k 10 400 python3 "$R/bench.py" --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     profile) bash "$R/tools/gpu_profile.sh" "$(basename "$OUT")/prof" > "$OUT/profile.log" 2>&1 ;;
