@@ -53,6 +53,24 @@ def test_replay_hip_vs_cpu(model, staleness):
         assert f"[hip] case {name}: ok" in out, name
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("model,staleness,threads", [("ssp", 3, False), ("ssp", 3, True), ("bsp", 0, True)])
+def test_replay_example_script_sizes(model, staleness, threads):
+    """cfg 5 at the reference example's own sizes
+    (scripts/logistic_regression.py.example:31-47): n_features 1e6,
+    batch_size 100, 5 workers per node (10 workers: two nodes' worth), over 8
+    HBM shards with SSP staleness 3 (and BSP), one server thread per shard in
+    the threaded form; every reply and every shard's final contents
+    bit-identical to the oracle storage run."""
+    args = ["--model", model, "--staleness", str(staleness), "--iters", "6", "--shards", "8",
+            "--workers", "10", "--batch", "100", "--features", "1000000"]
+    if threads:
+        args.append("--threads")
+    rc, out = run(*args)
+    assert rc == 0, out
+    assert "batch=100" in out and "workers=10" in out and "REPLAY OK (bit-exact)" in out
+
+
 @pytest.mark.parametrize("model", ["ssp", "bsp", "asp"])
 def test_replay_threaded_cpu_deterministic(model):
     """One ServerThread per shard (server/server_thread.cpp:20-50): the replies

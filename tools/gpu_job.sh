@@ -5,11 +5,14 @@
 #   tests_all    pytest -m gpu (everything)
 #   align        tools/align_probe.py (window phase cost)
 #   emu          bench.py as rank 0 of 8 and of 2 (one rank's cfg-4 share alone)
+#   emu8all      bench.py as each of the 8 ranks of N = 8 in turn (every rank's cfg-4 share alone)
+#   emutrace     rocprofv3 kernel trace of rank 0 of 8 (kernel durations and gaps of a small share)
 #   emu_unroll   rank 0 of 8 at 4 x 4 keys per lane (PSKV_UNROLL=4) and at the default 8
 #   ztrace       rocprofv3 kernel trace of zipf_probe at K5a 1024 and 512 threads (K5a / K5b split)
 #   zpmc         tools/zipf_pmc.sh: wave-state, LDS and HBM counters of the cfg-3 path
 #   k5phases     tools/micro/k5_phases (diagnostic build: K5a / K5b phase stamps), assign and accumulate
 #   abz          tools/ab_lib.sh with AB_PROG=zipf: ab/libpskv_base.so vs ab/libpskv_new.so on cfg 3, 3 rounds each
+#   sizes        tools/size_probe.py: K2g / K1 time against window count (fixed cost per launch)
 #   e2e          tools/e2e_probe.py (host-buffer Add / Get against raw PCIe copy rates)
 #   bench        bench.py --steps 20 (the driver's command line)
 #   zipf         tools/zipf_probe.py kernel times on cfg 3
@@ -35,6 +38,12 @@ for step in "$@"; do
            > "$OUT/emu08.json" 2> "$OUT/emu08.err" &&
          PSKV_BENCH_EMULATE=0/2 timeout -k 10 200 python3 "$R/bench.py" --steps 20 --no-zipf --no-cpu-baseline --no-extra \
            > "$OUT/emu02.json" 2> "$OUT/emu02.err" ;;
+    emu8all) for r in 0 1 2 3 4 5 6 7; do
+          PSKV_BENCH_EMULATE=$r/8 timeout -k 10 200 python3 "$R/bench.py" --steps 50 --no-zipf --no-cpu-baseline \
+            --no-extra > "$OUT/emu8_$r.json" 2> "$OUT/emu8_$r.err" || exit 1
+        done ;;
+    emutrace) PSKV_BENCH_EMULATE=0/8 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/emutrace" -o run \
+          -- python3 "$R/bench.py" --steps 50 --no-zipf --no-cpu-baseline --no-extra > "$OUT/emutrace.log" 2>&1 ;;
     emu_unroll) PSKV_BENCH_EMULATE=0/8 PSKV_UNROLL=4 timeout -k 10 200 python3 "$R/bench.py" --steps 20 --no-zipf \
            --no-cpu-baseline --no-extra > "$OUT/emu08_u4.json" 2> "$OUT/emu08_u4.err" &&
          PSKV_BENCH_EMULATE=0/8 timeout -k 10 200 python3 "$R/bench.py" --steps 20 --no-zipf --no-cpu-baseline \
@@ -48,6 +57,7 @@ for step in "$@"; do
         timeout -k 10 200 "$R/tools/micro/k5_phases" 1 > "$OUT/k5_phases_accumulate.log" 2>&1 ;;
     ldsrand) timeout -k 10 120 "$R/tools/micro/lds_atomic_rand" > "$OUT/lds_atomic_rand.log" 2>&1 ;;
     abz) AB_PROG=zipf timeout -k 10 900 bash "$R/tools/ab_lib.sh" "$(basename "$OUT")/abz" > "$OUT/abz.log" 2>&1 ;;
+    sizes) timeout -k 10 300 python3 "$R/tools/size_probe.py" > "$OUT/size_probe.log" 2>&1 ;;
     e2e) timeout -k 10 200 python3 "$R/tools/e2e_probe.py" > "$OUT/e2e.log" 2>&1 ;;
     bench) timeout -k 10 400 python3 "$R/bench.py" --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     profile) bash "$R/tools/gpu_profile.sh" "$(basename "$OUT")/prof" > "$OUT/profile.log" 2>&1 ;;
