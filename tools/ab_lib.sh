@@ -2,7 +2,8 @@
 # A/B two builds of libpskv.so on one box (ab/libpskv_base.so, ab/libpskv_new.so,
 # built beforehand): alternate them (swapping the in-tree library file), 3
 # rounds each, under bench.py (default) or, with AB_PROG=zipf, under
-# tools/zipf_probe.py (the cfg-3 K5 / K1 kernel times).
+# tools/zipf_probe.py (the cfg-3 K5 / K1 kernel times), with AB_PROG=sizes under
+# tools/size_probe.py (K2g / K1 fixed cost per launch).
 #   bash tools/ab_lib.sh OUTNAME ["bench.py args"]
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$PWD}
@@ -12,7 +13,9 @@ mkdir -p "$OUT"
 for i in 1 2 3; do
   for v in base new; do
     cp "$R/ab/libpskv_$v.so" "$R/parameter_server_amd/libpskv.so" || exit 1
-    if [ "${AB_PROG:-bench}" = zipf ]; then
+    if [ "${AB_PROG:-bench}" = sizes ]; then
+      timeout -k 10 200 python3 "$R/tools/size_probe.py" > "$OUT/$v$i.log" 2>&1 || exit 2
+    elif [ "${AB_PROG:-bench}" = zipf ]; then
       timeout -k 10 200 python3 "$R/tools/zipf_probe.py" > "$OUT/$v$i.log" 2>&1 || exit 2
     else
       timeout -k 10 200 python3 "$R/bench.py" $ARGS > "$OUT/$v$i.json" 2> "$OUT/$v$i.err" || exit 2

@@ -1,11 +1,11 @@
 """Fixed cost per launch of the streaming kernels: K2g (grouped sorted Add)
-and K1 (grouped Get) over J = 1..64 contiguous 1M-key windows of a 1e8-key
+and K1 (grouped Get) over J = 2..64 contiguous 1M-key windows of a 1e8-key
 float shard (distinct, non-overlapping windows, 1M-aligned; every call pulls
 / pushes windows the previous call did not touch), HIP-event time per kernel
 and wall time per Add+Get pair, then the least-squares fit t = t0 + bytes / BW
 per kernel.  A rank's cfg-4 share at N = 8 is ~8 windows: what t0 costs there.
 
-  python tools/size_probe.py [J list, default 1,2,4,8,16,32,64] [reps]
+  python tools/size_probe.py [J list, default 2,4,8,16,32,64] [reps]
 """
 import os
 import sys
@@ -23,7 +23,7 @@ def main():
     import parameter_server_amd as ps
     from parameter_server_amd import _lib
 
-    js = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "1,2,4,8,16,32,64").split(",")]
+    js = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "2,4,8,16,32,64").split(",")]
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 30
     dev = torch.device("cuda:0")
     space, B, V = 100_000_000, 1_000_000, 4
