@@ -14,6 +14,8 @@
 #   abz          tools/ab_lib.sh with AB_PROG=zipf: ab/libpskv_base.so vs ab/libpskv_new.so on cfg 3, 3 rounds each
 #   sizes        tools/size_probe.py: K2g / K1 time against window count (fixed cost per launch)
 #   abs          tools/ab_lib.sh with AB_PROG=sizes: base vs new library under tools/size_probe.py
+#   fuzz         tests/test_fuzz.py over FUZZ_SCENARIOS (1500) new seeds from FUZZ_SEED0 (3500), single and concurrent
+#   sizetrace    rocprofv3 kernel trace of tools/size_probe.py (exact K2g / K4r / K1 durations and gaps)
 #   e2e          tools/e2e_probe.py (host-buffer Add / Get against raw PCIe copy rates)
 #   bench        bench.py --steps 20 (the driver's command line)
 #   zipf         tools/zipf_probe.py kernel times on cfg 3
@@ -60,6 +62,10 @@ for step in "$@"; do
     abz) AB_PROG=zipf timeout -k 10 900 bash "$R/tools/ab_lib.sh" "$(basename "$OUT")/abz" > "$OUT/abz.log" 2>&1 ;;
     sizes) timeout -k 10 300 python3 "$R/tools/size_probe.py" > "$OUT/size_probe.log" 2>&1 ;;
     abs) AB_PROG=sizes timeout -k 10 900 bash "$R/tools/ab_lib.sh" "$(basename "$OUT")/abs" > "$OUT/abs.log" 2>&1 ;;
+    fuzz) FUZZ_SEED0=${FUZZ_SEED0:-3500} FUZZ_SCENARIOS=${FUZZ_SCENARIOS:-1500} timeout -k 10 1000 python3 -u -m pytest \
+        "$R/tests/test_fuzz.py" -m gpu -q --timeout 300 --timeout-method thread > "$OUT/fuzz.log" 2>&1 ;;
+    sizetrace) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/sizetrace" -o run \
+          -- python3 "$R/tools/size_probe.py" 2,4,8,16,64 20 > "$OUT/sizetrace.log" 2>&1 ;;
     e2e) timeout -k 10 200 python3 "$R/tools/e2e_probe.py" > "$OUT/e2e.log" 2>&1 ;;
     bench) timeout -k 10 400 python3 "$R/bench.py" --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     profile) bash "$R/tools/gpu_profile.sh" "$(basename "$OUT")/prof" > "$OUT/profile.log" 2>&1 ;;
