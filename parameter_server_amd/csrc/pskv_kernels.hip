@@ -569,6 +569,15 @@ __device__ __forceinline__ bool apply_segment(const DevBatch& b, uint64_t s, uin
 // once (a 64-lane ballot) and elements test only the few that overlap.
 // Every element verifies k == first_j + i; a batch whose endpoints look dense
 // but whose keys are not is caught there and tagged for the repair.
+// An element is stored at first_j + i only when ITS OWN key verified (a lane's
+// group of four, or a wave's span for 8-byte values, as a whole): the replay
+// behind a tagged group rewrites exactly the keys the group holds, so the
+// sorted pass must never write any other key — a look-alike batch (same
+// endpoints, a duplicate hiding a missing key) would otherwise leave a value
+// at a key no batch of the group pushed.  So each chunk verifies exactly the
+// elements it stores, [s_lo, s_hi): its own range shifted down by the window's
+// phase p (below), whose keys are read at the same dword-aligned offsets as
+// the values.
 template <typename VT, bool VEC, int U, bool NT, bool NTP>
 __device__ __forceinline__ bool dense_chunk(const GroupArgs& ga, const DenseView& d, uint32_t c,
                                             const uint32_t* s_first, const uint32_t* s_last) {
@@ -584,9 +593,9 @@ __device__ __forceinline__ bool dense_chunk(const GroupArgs& ga, const DenseView
   const uint32_t first = s_first[j];
   // Phase of the window against the 16-byte parameter slots (4-byte values):
   // when the window starts off a slot (p != 0; cfg 4's producer windows start
-  // at any key), the chunk STORES the elements [s_lo, s_hi) — its own range
-  // shifted down by p (the first chunk from 0, the last to n) — so its 16-byte
-  // parameter stores are aligned, and VERIFIES its own range [base, end).
+  // at any key), the chunk STORES and VERIFIES the elements [s_lo, s_hi) — its
+  // own range shifted down by p (the first chunk from 0, the last to n) — so
+  // its 16-byte parameter stores are aligned.
   const uint32_t p0 = first - d.key_begin;
   const uint32_t ph = (sizeof(VT) == 4 && VEC) ? (p0 & 3u) : 0u;
   const uint64_t s_lo = (ph == 0u || base == 0) ? base : base - ph;
@@ -610,20 +619,12 @@ __device__ __forceinline__ bool dense_chunk(const GroupArgs& ga, const DenseView
     }
     return sh;
   };
-  if (VEC && end - base == CH && covered) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint64_t i = base + (uint64_t)(u * kBlock + tid) * 4;
-      uint32_t k[4];
-      Vec4<uint32_t>::load<NT>(keys + i, k);
-      const uint32_t k0 = first + (uint32_t)i;
-      bad |= (k[0] != k0) | (k[1] != k0 + 1u) | (k[2] != k0 + 2u) | (k[3] != k0 + 3u);
-    }
-  } else if (sizeof(VT) == 8 && VEC && end - base == CH) {
+  if (sizeof(VT) == 8 && VEC && end - base == CH) {
     // 8-byte values: keys four per lane (16-byte loads; each lane checks its
     // own four against first + index), values and parameters as PAIRS over the
     // wave's 256-element span (lane l: elements 2l, 2l+1 and 128+2l, 128+2l+1),
-    // so every access instruction covers one contiguous span
+    // so every access instruction covers one contiguous span.  The wave's keys
+    // cover the same span as its stores: it stores only if all 256 verified.
     using T = unsigned long long;
     uint32_t k[U][4];
     T va[U][2], vb[U][2];
@@ -632,15 +633,19 @@ __device__ __forceinline__ bool dense_chunk(const GroupArgs& ga, const DenseView
       const uint64_t i = base + (uint64_t)(u * kBlock + tid) * 4;
       const uint64_t ew = base + (uint64_t)(u * kBlock + (tid & ~63)) * 4;
       Vec4<uint32_t>::load<NT>(keys + i, k[u]);
-      Vec2x8::load<NT>(reinterpret_cast<const T*>(vals) + ew + 2 * lane, va[u]);
-      Vec2x8::load<NT>(reinterpret_cast<const T*>(vals) + ew + 128 + 2 * lane, vb[u]);
+      if (!covered) {
+        Vec2x8::load<NT>(reinterpret_cast<const T*>(vals) + ew + 2 * lane, va[u]);
+        Vec2x8::load<NT>(reinterpret_cast<const T*>(vals) + ew + 128 + 2 * lane, vb[u]);
+      }
     }
     T* __restrict__ p8 = reinterpret_cast<T*>(param);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint64_t i = base + (uint64_t)(u * kBlock + tid) * 4;
       const uint32_t k0 = first + (uint32_t)i;
-      bad |= (k[u][0] != k0) | (k[u][1] != k0 + 1u) | (k[u][2] != k0 + 2u) | (k[u][3] != k0 + 3u);
+      const bool lbad = (k[u][0] != k0) | (k[u][1] != k0 + 1u) | (k[u][2] != k0 + 2u) | (k[u][3] != k0 + 3u);
+      bad |= lbad;
+      if (covered || __ballot(lbad) != 0) continue;  // wave-uniform
       const uint32_t ka = first + (uint32_t)(base + (uint64_t)(u * kBlock + (tid & ~63)) * 4) + 2u * lane;
       const uint32_t offa = ka - d.key_begin;
       if (later == 0 && (offa & 1u) == 0u) {
@@ -655,47 +660,55 @@ __device__ __forceinline__ bool dense_chunk(const GroupArgs& ga, const DenseView
       }
     }
   } else if (VEC && end - base == CH) {
-    // 4-byte values, a whole chunk.  Each lane verifies its 16-byte key piece
-    // i .. i+3 and stores the 16-byte parameter slot of the elements
-    // g = i - ph .. +3 (slot-aligned: p0 + g == 0 mod 4), their values read by
-    // one dword-aligned 16-byte load (phase 0: the aligned piece i itself).
-    // So a window at any key streams like an aligned one.  (The two aligned
-    // pieces the group straddles, selected in registers, took the kernel from
-    // 95 to 127 VGPRs; shuffling the previous lane's piece, to 134.)
+    // 4-byte values, a whole chunk.  Each lane takes the elements
+    // g = i - ph .. +3 of its 16-byte piece i (slot-aligned: p0 + g == 0 mod 4;
+    // phase 0: the aligned piece i itself), their keys and values read by one
+    // dword-aligned 16-byte load each, verifies the four keys and stores the
+    // parameter slot if all four hold.  So a window at any key streams like an
+    // aligned one.  (The two aligned pieces the group straddles, selected in
+    // registers, took the kernel from 95 to 127 VGPRs; shuffling the previous
+    // lane's piece, to 134.)
     using BT = typename std::conditional<sizeof(VT) == 4, uint32_t, VT>::type;
     const BT* __restrict__ vb = reinterpret_cast<const BT*>(vals);
     BT* __restrict__ pb = reinterpret_cast<BT*>(param);
     // chunk-uniform bases (scalar registers) and 32-bit lane offsets: one
     // address register per access instead of a 64-bit pair
-    const uint32_t* __restrict__ kc = keys + base;
     const bool head = base == 0 && ph != 0u;  // the batch's first piece starts its group before element 0
-    const BT* __restrict__ vc = vb + (base - (head ? 0u : ph));
-    BT* __restrict__ pc = pb + p0 + (base - (head ? 0u : ph));
+    const uint64_t sb = base - (head ? 0u : ph);  // element of lane offset 0
+    const uint32_t* __restrict__ kc = keys + sb;
+    const BT* __restrict__ vc = vb + sb;
+    BT* __restrict__ pc = pb + p0 + sb;
+    const uint32_t hs = head ? ph : 0u;  // the head lane's offset shift
     uint32_t k[U][4];
     BT v[U][4];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t o = (uint32_t)(u * kBlock + tid) * 4u;
-      Vec4<uint32_t>::load<NT>(kc + o, k[u]);
       if (!head || o != 0u) {
-        ld16a4<NT>(vc + (o - (head ? ph : 0u)), v[u]);
+        ld16a4<NT>(kc + (o - hs), k[u]);
+        if (!covered) ld16a4<NT>(vc + (o - hs), v[u]);
       } else {  // group starts before element 0: its valid part one by one
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[u][e] = (uint32_t)e >= ph ? vb[e - ph] : BT(0);
+        for (int e = 0; e < 4; ++e) {
+          k[u][e] = (uint32_t)e >= ph ? keys[e - ph] : first + (uint32_t)e - ph;
+          v[u][e] = (uint32_t)e >= ph && !covered ? vb[e - ph] : BT(0);
+        }
       }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t o = (uint32_t)(u * kBlock + tid) * 4u;
-      const uint32_t k0 = first + (uint32_t)base + o;
-      bad |= (k[u][0] != k0) | (k[u][1] != k0 + 1u) | (k[u][2] != k0 + 2u) | (k[u][3] != k0 + 3u);
+      const uint32_t k0 = first + (uint32_t)sb + o - hs;  // the key element g = sb + o - hs must hold
+      const bool lbad = (k[u][0] != k0) | (k[u][1] != k0 + 1u) | (k[u][2] != k0 + 2u) | (k[u][3] != k0 + 3u);
+      bad |= lbad;
+      if (covered || lbad) continue;
       if (later == 0 && (!head || o != 0u)) {
-        Vec4<BT>::template store<NTP>(pc + (o - (head ? ph : 0u)), v[u]);
+        Vec4<BT>::template store<NTP>(pc + (o - hs), v[u]);
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const uint32_t g = (uint32_t)base + o + (uint32_t)e;  // element g - ph of the batch
-          if (g >= ph && !shadowed(first + (g - ph))) pb[p0 + (g - ph)] = v[u][e];
+          const uint32_t g = (uint32_t)sb + o - hs + (uint32_t)e;  // element g of the batch (head: g may be < 0)
+          if ((!head || o != 0u || (uint32_t)e >= ph) && !shadowed(first + g)) pb[p0 + g] = v[u][e];
         }
       }
     }
@@ -703,38 +716,31 @@ __device__ __forceinline__ bool dense_chunk(const GroupArgs& ga, const DenseView
     // holds them
     if (ph != 0u && end == n && (uint32_t)tid < ph) {
       const uint64_t ie = n - ph + tid;
-      if (!shadowed(first + (uint32_t)ie)) pb[p0 + ie] = vb[ie];
+      const bool lbad = keys[ie] != first + (uint32_t)ie;
+      bad |= lbad;
+      if (!covered && !lbad && !shadowed(first + (uint32_t)ie)) pb[p0 + ie] = vb[ie];
     }
   } else {
     // a partial (or unaligned) chunk — the last one of every window: eight
     // elements per lane loaded together, then checked and stored, so the
     // chunk costs one dependent round trip per eight elements per lane rather
     // than one per element (a window's 576-key tail took three in a row).
-    // It verifies its own elements [base, end) and stores [s_lo, s_hi) (the
-    // same range unless the phase shifted it, above)
-    for (uint64_t i0 = base + tid; i0 < end; i0 += 8ull * kBlock) {
+    // It verifies and stores [s_lo, s_hi), each element on its own key.
+    for (uint64_t i0 = s_lo + tid; i0 < s_hi; i0 += 8ull * kBlock) {
       uint32_t kk[8];
+      VT vv[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const uint64_t i = i0 + (uint64_t)q * kBlock;
-        kk[q] = i < end ? keys[i] : first + (uint32_t)i;
+        kk[q] = i < s_hi ? keys[i] : first + (uint32_t)i;
+        vv[q] = i < s_hi && !covered ? vals[i] : VT(0);
       }
 #pragma unroll
-      for (int q = 0; q < 8; ++q) bad |= kk[q] != first + (uint32_t)(i0 + (uint64_t)q * kBlock);
-    }
-    if (!covered) {
-      for (uint64_t i0 = s_lo + tid; i0 < s_hi; i0 += 8ull * kBlock) {
-        VT vv[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const uint64_t i = i0 + (uint64_t)q * kBlock;
-          vv[q] = i < s_hi ? vals[i] : VT(0);
-        }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const uint64_t i = i0 + (uint64_t)q * kBlock;
-          if (i < s_hi && !shadowed(first + (uint32_t)i)) param[p0 + i] = vv[q];
-        }
+      for (int q = 0; q < 8; ++q) {
+        const uint64_t i = i0 + (uint64_t)q * kBlock;
+        const bool ebad = kk[q] != first + (uint32_t)i;
+        bad |= ebad;
+        if (i < s_hi && !covered && !ebad && !shadowed(first + (uint32_t)i)) param[p0 + i] = vv[q];
       }
     }
   }

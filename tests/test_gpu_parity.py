@@ -678,6 +678,45 @@ def test_grouped_dense_lookalike_is_repaired(cuda, oracle_mod):
     assert_bits_equal(got, dense, "lookalike")
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("phase", [0, 1, 3])
+def test_grouped_dense_lookalike_never_writes_missing_keys(cuda, oracle_mod, dtype, phase):
+    """A wrong sorted hint on batches whose endpoints span exactly n - 1 keys
+    but which repeat one key and so MISS another, where no other batch of the
+    group holds the missing key: the sorted pass must not write the missing
+    key (the replay rewrites only the group's own keys), so it keeps its prior
+    value (map_storage.hpp:22-23: an Add touches only the keys it carries).
+    Whole chunks (>= 8 Ki keys), the chunk holding the window's phase shift,
+    partial chunks and the batch tail, at window phases 0 / 1 / 3."""
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(11 + phase)
+    size = 200_000
+    prior = rng.standard_normal(size).astype(dtype)
+    dense = prior.copy()
+    specs = [(1_000 + phase, 30_000, [5, 9_000, 20_000, 29_998]),   # whole chunks + tail
+             (60_000 + phase, 8_200, [8_190]),                      # the phase-shift chunk boundary
+             (100_000 + phase, 700, [0, 350]),                      # one partial chunk
+             (150_000 + phase, 20_000, [])]                         # a clean window
+    batches = []
+    for b, n, dups in specs:
+        k = np.arange(b, b + n, dtype=np.uint32)
+        for i in dups:  # k[i] repeats k[i + 1] (same endpoints): key b + i is missing
+            if i + 1 < n:
+                k[i] = k[i + 1]
+            else:
+                k[i] = k[i - 1]
+        v = rng.standard_normal(n).astype(dtype)
+        batches.append((k, v))
+    with ps.Shard(0, size, dtype) as sh:
+        sh.add(np.arange(size, dtype=np.uint32), prior)
+        for k, v in batches:
+            oracle_mod.dense_last_wins(dense, 0, k, v)
+        sh.add_grouped([(tdev(k, cuda), tdev(v, cuda)) for k, v in batches], sorted_hint=True)
+        got = sh.get(np.arange(size, dtype=np.uint32))
+    assert_bits_equal(got, dense, f"lookalike missing keys, phase {phase}")
+
+
 @pytest.mark.parametrize("mode,dtype", [("assign", np.float32), ("assign", np.float64),
                                         ("accumulate", np.float64), ("accumulate", np.int32)])
 def test_radix_path_hot_bucket_many_rounds(cuda, oracle_mod, mode, dtype):
