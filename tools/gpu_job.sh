@@ -16,6 +16,7 @@
 #   abs          tools/ab_lib.sh with AB_PROG=sizes: base vs new library under tools/size_probe.py
 #   fuzz         tests/test_fuzz.py over FUZZ_SCENARIOS (1500) new seeds from FUZZ_SEED0 (3500), single and concurrent
 #   sizetrace    rocprofv3 kernel trace of tools/size_probe.py (exact K2g / K4r / K1 durations and gaps)
+#   idle         tools/micro/idle_launch: an idle conditional launch's cost between two streaming kernels
 #   e2e          tools/e2e_probe.py (host-buffer Add / Get against raw PCIe copy rates)
 #   bench        bench.py --steps 20 (the driver's command line)
 #   zipf         tools/zipf_probe.py kernel times on cfg 3
@@ -66,6 +67,7 @@ for step in "$@"; do
         "$R/tests/test_fuzz.py" -m gpu -q --timeout 300 --timeout-method thread > "$OUT/fuzz.log" 2>&1 ;;
     sizetrace) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/sizetrace" -o run \
           -- python3 "$R/tools/size_probe.py" 2,4,8,16,64 20 > "$OUT/sizetrace.log" 2>&1 ;;
+    idle) timeout -k 10 120 "$R/tools/micro/idle_launch" > "$OUT/idle_launch.log" 2>&1 ;;
     e2e) timeout -k 10 200 python3 "$R/tools/e2e_probe.py" > "$OUT/e2e.log" 2>&1 ;;
     bench) timeout -k 10 400 python3 "$R/bench.py" --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     profile) bash "$R/tools/gpu_profile.sh" "$(basename "$OUT")/prof" > "$OUT/profile.log" 2>&1 ;;
