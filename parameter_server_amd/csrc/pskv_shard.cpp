@@ -1432,8 +1432,13 @@ int add_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
           rc = general_add(s, v, g.first, g.second, epoch, nullptr);
         }
       } else if (!device && host_verified) {
-        // the CPU proved the batches sorted and in range while staging them
-        rc = sorted_add(s, v, g.first, g.second, vec, epoch, /*repair=*/false);
+        // the CPU proved the batches sorted and in range while staging them.
+        // Sorted is not dense: a sorted batch that repeats a key and misses
+        // another spans exactly n - 1 keys like a window (keys 5, 6, 6, 8), so
+        // K2g's dense mode takes it and its per-element check tags it; the
+        // replay then applies the group in order.  Only batches the CPU proved
+        // strictly contiguous cannot trip that check and skip the replay.
+        rc = sorted_add(s, v, g.first, g.second, vec, epoch, /*repair=*/!host_dense);
       } else if (device && (flags & PSKV_SORTED_HINT)) {
         rc = sorted_add(s, v, g.first, g.second, vec, epoch, /*repair=*/true);
       } else {

@@ -40,6 +40,26 @@ def test_library_is_gfx950_hip_code():
     assert b"gfx950" in blob
 
 
+def test_random_access_calibration_library():
+    """bench.py's cfg-3 random-access floor (tools/micro/random_access.hip):
+    built by __graft_entry__.build() beside libpskv, gfx950 code, exporting the
+    two entry points bench.py binds.  Measurement infrastructure only: libpskv
+    does not link it."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("pskv_build", os.path.join(ROOT, "parameter_server_amd", "build.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    path = b.build_random_access()
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True).stdout
+    assert {"ra_gather", "ra_scatter"} <= set(re.findall(r" T (\w+)", out))
+    assert b"gfx950" in open(path, "rb").read()
+    from parameter_server_amd import _lib
+
+    deps = subprocess.run(["readelf", "-d", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    assert "random_access" not in deps
+
+
 def test_abi_version_and_no_device_here():
     from parameter_server_amd import _lib
 

@@ -5,8 +5,9 @@ one-key shard, dtype, mode, a tuning knob that selects another host or kernel
 path) and a random sequence of calls — single, grouped (beyond the 64-batch
 launch group), host, device (unaligned pointers, right and WRONG sorted hints),
 inline-sized and large, uniform / Zipf / sorted / dense-window / out-of-range /
-sentinel keys, empty batches, clears — and checks every Get against the
-reference state right away:
+sentinel keys, sorted look-alikes of windows (a repeated key hiding a missing
+one), empty batches, clears — and checks every Get against the reference state
+right away:
 
   assign      the oracle's MapStorage restatement (server/map_storage.hpp:17-45),
               bit-exact
@@ -84,15 +85,22 @@ def _keys(rng, kb, ke, n, kind):
     size = ke - kb
     if n == 0:
         return np.empty(0, np.uint32)
-    if kind == "dense" and n <= size:
+    if kind in ("dense", "lookalike") and n <= size:
         first = int(rng.integers(kb, ke - n + 1))
-        return np.arange(first, first + n, dtype=np.uint64).astype(np.uint32)
+        k = np.arange(first, first + n, dtype=np.uint64).astype(np.uint32)
+        if kind == "lookalike" and n >= 3:
+            # still sorted, but a key repeats its predecessor and so hides a
+            # missing one: the endpoints usually still span n - 1 keys, like a
+            # window (the sorted / dense paths must not treat it as one)
+            for i in rng.integers(0, n - 1, size=int(rng.integers(1, 4))).tolist():
+                k[i + 1] = k[i]
+        return k
     if kind == "zipf":
         hot = rng.integers(kb, ke, size=min(size, 64), dtype=np.int64)
         k = hot[(rng.zipf(1.3, size=n) - 1) % hot.size]
     else:
         k = rng.integers(kb, ke, size=n, dtype=np.int64)
-    if kind in ("sorted", "dense"):
+    if kind in ("sorted", "dense", "lookalike"):
         k = np.sort(k)
     if kind == "oor":
         # a few keys outside the shard (both sides when they exist), the
@@ -165,7 +173,7 @@ def _run(cuda, oracle_mod, seed, rng, dt, mode, kb, ke, knobs):
 
     ref = oracle_mod.MapStorageRef(dt) if mode == "assign" else AccRef(dt)
     keep = []  # device buffers stay alive until the final sync (stream-ordered use)
-    kinds = ["uniform", "zipf", "sorted", "dense", "oor"]
+    kinds = ["uniform", "zipf", "sorted", "dense", "oor", "lookalike"]
     where = f"seed {seed} ({np.dtype(dt).name} {mode} [{kb}, {ke}) {knobs})"
 
     def check(q, got, step):
@@ -201,7 +209,7 @@ def _run(cuda, oracle_mod, seed, rng, dt, mode, kb, ke, knobs):
                 ref.add(k, v)
             elif op in ("add_grouped", "add_grouped_dev"):
                 nb = int(rng.choice([1, 2, 7, 64, 65, 70]))
-                dense = kind == "dense"
+                dense = kind in ("dense", "lookalike")
                 batches = []
                 for _ in range(nb):
                     n = int(rng.choice([0, 1, 33, 1000, 8192, 20_001] if not dense else [1, 1000, 8192, 30_000]))

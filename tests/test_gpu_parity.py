@@ -717,6 +717,37 @@ def test_grouped_dense_lookalike_never_writes_missing_keys(cuda, oracle_mod, dty
     assert_bits_equal(got, dense, f"lookalike missing keys, phase {phase}")
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("n", [4, 700, 30_000])
+def test_host_sorted_group_with_duplicates_spanning_n_minus_1(cuda, oracle_mod, dtype, n):
+    """HOST batches (the reference's zmq frames) that are sorted, so the CPU
+    check passes them to the sorted path, but repeat a key and miss another, so
+    their endpoints span exactly n - 1 keys like a dense window: the grouped
+    Add must still give the LAST occurrence of the repeated key and leave the
+    missing key alone (map_storage.hpp:22-23).  E.g. keys [5, 6, 6, 8]."""
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(n)
+    size = 200_000
+    prior = rng.standard_normal(size).astype(dtype)
+    dense = prior.copy()
+    batches = []
+    for j, b in enumerate((1_000, 40_000, 70_001)):
+        k = np.arange(b, b + n, dtype=np.uint32)
+        if j != 1:  # batch 1 stays a true dense window
+            i = n // 2 if n > 4 else 1
+            k[i + 1] = k[i]  # sorted, a repeat of k[i], key b + i + 1 missing
+        v = rng.standard_normal(n).astype(dtype)
+        batches.append((k, v))
+    with ps.Shard(0, size, dtype, options={"INLINE": 0}) as sh:  # n = 4 too: the staged path
+        sh.add(np.arange(size, dtype=np.uint32), prior)
+        for k, v in batches:
+            oracle_mod.dense_last_wins(dense, 0, k, v)
+        sh.add_grouped(batches)  # host buffers: the CPU check proves them sorted
+        got = sh.get(np.arange(size, dtype=np.uint32))
+    assert_bits_equal(got, dense, f"host sorted look-alike, n={n}")
+
+
 @pytest.mark.parametrize("mode,dtype", [("assign", np.float32), ("assign", np.float64),
                                         ("accumulate", np.float64), ("accumulate", np.int32)])
 def test_radix_path_hot_bucket_many_rounds(cuda, oracle_mod, mode, dtype):
