@@ -17,6 +17,7 @@
 #   fuzz         tests/test_fuzz.py over FUZZ_SCENARIOS (1500) new seeds from FUZZ_SEED0 (3500), single and concurrent
 #   sizetrace    rocprofv3 kernel trace of tools/size_probe.py (exact K2g / K4r / K1 durations and gaps)
 #   idle         tools/micro/idle_launch: an idle conditional launch's cost between two streaming kernels
+#   ztb          tools/zipf_probe.py: K5 bucket count / window width variants at the current K5b
 #   e2e          tools/e2e_probe.py (host-buffer Add / Get against raw PCIe copy rates)
 #   bench        bench.py --steps 20 (the driver's command line)
 #   zipf         tools/zipf_probe.py kernel times on cfg 3
@@ -68,6 +69,8 @@ for step in "$@"; do
     sizetrace) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/sizetrace" -o run \
           -- python3 "$R/tools/size_probe.py" 2,4,8,16,64 20 > "$OUT/sizetrace.log" 2>&1 ;;
     idle) timeout -k 10 120 "$R/tools/micro/idle_launch" > "$OUT/idle_launch.log" 2>&1 ;;
+    ztb) timeout -k 10 300 python3 "$R/tools/zipf_probe.py" "" "PSKV_RB_TB=10" "PSKV_RB_TB=10,PSKV_RB_WBITS=12" \
+          "PSKV_RB_WBITS=12" > "$OUT/ztb.log" 2>&1 ;;
     e2e) timeout -k 10 200 python3 "$R/tools/e2e_probe.py" > "$OUT/e2e.log" 2>&1 ;;
     bench) timeout -k 10 400 python3 "$R/bench.py" --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     profile) bash "$R/tools/gpu_profile.sh" "$(basename "$OUT")/prof" > "$OUT/profile.log" 2>&1 ;;
