@@ -75,6 +75,16 @@ template <bool NT>
 __device__ __forceinline__ void ld16a4(const unsigned long long* p, unsigned long long (&v)[4]) {
   (void)p; v[0] = v[1] = v[2] = v[3] = 0ull;  // 8-byte values never take the phase path
 }
+// ... and a 16-byte STORE to a dword-aligned address (K2g's early mode stores
+// a window's elements where they land, whatever the window's phase).
+template <bool NT>
+__device__ __forceinline__ void st16a4(uint32_t* p, const uint32_t (&v)[4]) {
+  const u32x4 t = u32x4{v[0], v[1], v[2], v[3]};
+  if (NT)
+    __builtin_nontemporal_store(t, reinterpret_cast<u32x4a4*>(p));
+  else
+    *reinterpret_cast<u32x4a4*>(p) = t;
+}
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 template <bool NT>
@@ -747,11 +757,106 @@ __device__ __forceinline__ bool dense_chunk(const GroupArgs& ga, const DenseView
   return bad;
 }
 
+// Early mode (4-byte values, 16-byte aligned batches; chosen per launch by the
+// host, option EARLY): every chunk verifies and stores its OWN elements
+// [base, end) — no phase shift — so a whole chunk's keys and values are plain
+// aligned loads that depend on nothing and can be issued before the
+// workgroup's prologue (the first and last key of every batch) has come back;
+// the price is a dword-aligned 16-byte parameter store for a window off the
+// 16-byte slots, and no skipping of the values of a chunk a later window
+// covers (the values are already in flight).  It pays where a launch is small
+// (a rank's ~8 windows at N = 8: the prologue's round trip is then a visible
+// part of the launch) and windows rarely overlap.  PRE: k / v already hold
+// the chunk (a whole one); else this loads them.  Verification and stores
+// cover the same elements, each stored only if its own key verified (above).
+template <int U, bool NT, bool NTP, bool PRE>
+__device__ __forceinline__ bool dense_chunk_own(const GroupArgs& ga, const DenseView& d, uint32_t c,
+                                                const uint32_t* s_first, const uint32_t* s_last,
+                                                uint32_t (&k)[U][4], uint32_t (&v)[U][4]) {
+  constexpr int CH = kBlock * 4 * U;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int j = batch_of(ga, c);
+  const uint32_t* __restrict__ keys = ga.b[j].keys;
+  const uint32_t* __restrict__ vals = reinterpret_cast<const uint32_t*>(ga.b[j].vals);
+  const uint64_t n = ga.b[j].n;
+  const uint64_t base = (uint64_t)(c - ga.wg_prefix[j]) * CH;
+  const uint64_t end = n < base + CH ? n : base + CH;
+  const uint32_t first = s_first[j];
+  const uint32_t p0 = first - d.key_begin;
+  const uint32_t c_lo = first + (uint32_t)base, c_hi = first + (uint32_t)(end - 1);
+  const bool ov = lane > j && lane < ga.nb && s_first[lane] <= c_hi && s_last[lane] >= c_lo;
+  const unsigned long long later = __ballot(ov);
+  const bool covered = __ballot(ov && s_first[lane] <= c_lo && s_last[lane] >= c_hi) != 0;
+  uint32_t* __restrict__ param = reinterpret_cast<uint32_t*>(d.param);
+  bool bad = false;
+  auto shadowed = [&](uint32_t key) {
+    unsigned long long m = later;
+    bool sh = false;
+    while (m) {
+      const int q = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      sh |= (key >= s_first[q]) & (key <= s_last[q]);
+    }
+    return sh;
+  };
+  if (end - base == CH) {
+    const uint32_t* __restrict__ kc = keys + base;
+    const uint32_t* __restrict__ vc = vals + base;
+    uint32_t* __restrict__ pc = param + p0 + base;
+    if (!PRE) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t o = (uint32_t)(u * kBlock + tid) * 4u;
+        Vec4<uint32_t>::load<NT>(kc + o, k[u]);
+        if (!covered) Vec4<uint32_t>::load<NT>(vc + o, v[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t o = (uint32_t)(u * kBlock + tid) * 4u;
+      const uint32_t k0 = first + (uint32_t)base + o;
+      const bool lbad = (k[u][0] != k0) | (k[u][1] != k0 + 1u) | (k[u][2] != k0 + 2u) | (k[u][3] != k0 + 3u);
+      bad |= lbad;
+      if (covered || lbad) continue;
+      if (later == 0) {
+        st16a4<NTP>(pc + o, v[u]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (!shadowed(k0 + (uint32_t)e)) pc[o + e] = v[u][e];
+      }
+    }
+  } else {
+    // a partial chunk (the last of a window): eight elements per lane loaded
+    // together, then checked and stored
+    for (uint64_t i0 = base + tid; i0 < end; i0 += 8ull * kBlock) {
+      uint32_t kk[8], vv[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const uint64_t i = i0 + (uint64_t)q * kBlock;
+        kk[q] = i < end ? keys[i] : first + (uint32_t)i;
+        vv[q] = i < end && !covered ? vals[i] : 0u;
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const uint64_t i = i0 + (uint64_t)q * kBlock;
+        const bool ebad = kk[q] != first + (uint32_t)i;
+        bad |= ebad;
+        if (i < end && !covered && !ebad && !shadowed(first + (uint32_t)i)) param[p0 + i] = vv[q];
+      }
+    }
+  }
+  return bad;
+}
+
 // Mode B (general sorted batches): key-tile owner, static strided schedule.
-template <typename VT, bool VEC, int U, bool NT, bool NTP>
+template <typename VT, bool VEC, int U, bool NT, bool NTP, bool EARLY = false>
 __global__ __launch_bounds__(kBlock) void k_assign_group(GroupArgs ga, DenseView d,
                                                          uint32_t tile_shift, uint64_t ntiles,
                                                          uint32_t* flag, uint32_t epoch) {
+  static_assert(!EARLY || (sizeof(VT) == 4 && VEC), "early mode: 4-byte values, aligned batches");
+  constexpr int CH = kBlock * 4 * U;
   __shared__ uint64_t s_seg_s[kMaxBatches];
   __shared__ uint64_t s_seg_e[kMaxBatches];
   __shared__ uint32_t s_first[kMaxBatches];
@@ -760,6 +865,27 @@ __global__ __launch_bounds__(kBlock) void k_assign_group(GroupArgs ga, DenseView
   __shared__ int s_dense;
   const int tid = threadIdx.x;
   const int jb = tid & 63;
+  // early mode: this workgroup's first chunk, when whole, is requested now,
+  // before the prologue below (its loads need no batch endpoint)
+  uint32_t ek[EARLY ? U : 1][4], ev[EARLY ? U : 1][4];
+  bool pre = false;
+  if constexpr (EARLY) {
+    if (blockIdx.x < ga.wg_prefix[ga.nb]) {
+      const int j0 = batch_of(ga, blockIdx.x);
+      const uint64_t base0 = (uint64_t)(blockIdx.x - ga.wg_prefix[j0]) * CH;
+      if (ga.b[j0].n >= base0 + CH) {
+        pre = true;
+        const uint32_t* __restrict__ kc = ga.b[j0].keys + base0;
+        const uint32_t* __restrict__ vc = reinterpret_cast<const uint32_t*>(ga.b[j0].vals) + base0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t o = (uint32_t)(u * kBlock + tid) * 4u;
+          Vec4<uint32_t>::load<NT>(kc + o, ek[u]);
+          Vec4<uint32_t>::load<NT>(vc + o, ev[u]);
+        }
+      }
+    }
+  }
   // Lanes of waves 0 and 1 keep batch jb's endpoints for the whole launch.
   uint32_t first = 0, last = 0;
   uint64_t n = 0;
@@ -790,8 +916,18 @@ __global__ __launch_bounds__(kBlock) void k_assign_group(GroupArgs ga, DenseView
   bool bad = false;
   if (s_dense) {
     const uint32_t nchunks = ga.wg_prefix[ga.nb];
-    for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x)
-      bad |= dense_chunk<VT, VEC, U, NT, NTP>(ga, d, c, s_first, s_last);
+    if constexpr (EARLY) {
+      uint32_t c = blockIdx.x;
+      if (pre) {
+        bad |= dense_chunk_own<U, NT, NTP, true>(ga, d, c, s_first, s_last, ek, ev);
+        c += gridDim.x;
+      }
+      for (; c < nchunks; c += gridDim.x)
+        bad |= dense_chunk_own<U, NT, NTP, false>(ga, d, c, s_first, s_last, ek, ev);
+    } else {
+      for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x)
+        bad |= dense_chunk<VT, VEC, U, NT, NTP>(ga, d, c, s_first, s_last);
+    }
     if (bad) *flag = epoch;
     return;
   }
@@ -2440,9 +2576,15 @@ hipError_t launch_assign_sorted(int vb, bool vec, const uint32_t* keys, const vo
 }
 
 template <typename VT, bool VEC, bool NTP>
-static void group_dispatch2(int unroll, bool nt, uint32_t grid, const GroupArgs& ga,
+static void group_dispatch2(int unroll, bool nt, bool early, uint32_t grid, const GroupArgs& ga,
                             const DenseView& d, uint32_t shift, uint64_t ntiles, uint32_t* flag,
                             uint32_t epoch, hipStream_t st) {
+  if constexpr (sizeof(VT) == 4 && VEC) {
+    if (early && unroll == 8 && nt) {  // early mode: the default unroll and streams only
+      k_assign_group<VT, VEC, 8, true, NTP, true><<<grid, kBlock, 0, st>>>(ga, d, shift, ntiles, flag, epoch);
+      return;
+    }
+  }
   if (unroll == 8) {
     if (nt)
       k_assign_group<VT, VEC, 8, true, NTP><<<grid, kBlock, 0, st>>>(ga, d, shift, ntiles, flag, epoch);
@@ -2457,30 +2599,31 @@ static void group_dispatch2(int unroll, bool nt, uint32_t grid, const GroupArgs&
 }
 
 template <typename VT, bool VEC>
-static void group_dispatch(int unroll, bool nt, bool ntp, uint32_t grid, const GroupArgs& ga,
+static void group_dispatch(int unroll, bool nt, bool ntp, bool early, uint32_t grid, const GroupArgs& ga,
                            const DenseView& d, uint32_t shift, uint64_t ntiles, uint32_t* flag,
                            uint32_t epoch, hipStream_t st) {
   if (ntp)
-    group_dispatch2<VT, VEC, true>(unroll, nt, grid, ga, d, shift, ntiles, flag, epoch, st);
+    group_dispatch2<VT, VEC, true>(unroll, nt, early, grid, ga, d, shift, ntiles, flag, epoch, st);
   else
-    group_dispatch2<VT, VEC, false>(unroll, nt, grid, ga, d, shift, ntiles, flag, epoch, st);
+    group_dispatch2<VT, VEC, false>(unroll, nt, early, grid, ga, d, shift, ntiles, flag, epoch, st);
 }
 
-hipError_t launch_assign_group(int vb, bool vec, int unroll, bool nt, bool ntp, const GroupArgs& ga,
+hipError_t launch_assign_group(int vb, bool vec, int unroll, bool nt, bool ntp, bool early,
+                               const GroupArgs& ga,
                                const DenseView& d, uint32_t tile_shift, uint64_t ntiles,
                                uint32_t grid, uint32_t* flag, uint32_t epoch, hipStream_t st) {
   if (grid == 0) return hipSuccess;
   if (vb == 4) {
     if (vec)
-      group_dispatch<uint32_t, true>(unroll, nt, ntp, grid, ga, d, tile_shift, ntiles, flag, epoch, st);
+      group_dispatch<uint32_t, true>(unroll, nt, ntp, early, grid, ga, d, tile_shift, ntiles, flag, epoch, st);
     else
-      group_dispatch<uint32_t, false>(unroll, nt, ntp, grid, ga, d, tile_shift, ntiles, flag, epoch, st);
+      group_dispatch<uint32_t, false>(unroll, nt, ntp, early, grid, ga, d, tile_shift, ntiles, flag, epoch, st);
   } else {
     if (vec)
-      group_dispatch<unsigned long long, true>(unroll, nt, ntp, grid, ga, d, tile_shift, ntiles, flag,
+      group_dispatch<unsigned long long, true>(unroll, nt, ntp, early, grid, ga, d, tile_shift, ntiles, flag,
                                                epoch, st);
     else
-      group_dispatch<unsigned long long, false>(unroll, nt, ntp, grid, ga, d, tile_shift, ntiles, flag,
+      group_dispatch<unsigned long long, false>(unroll, nt, ntp, early, grid, ga, d, tile_shift, ntiles, flag,
                                                 epoch, st);
   }
   return hipGetLastError();

@@ -257,6 +257,7 @@ struct pskv_shard {
   int tune_unroll = 8;   // PSKV_UNROLL: 4 or 8 (8: measured +5 % on the dense Add)
   bool tune_nt = true;   // PSKV_NT: non-temporal streams (measured +12-15 % on K1 / K2g)
   bool tune_ntp = false; // PSKV_NTP: non-temporal parameter stores (dense Add)
+  int tune_early = 2;    // PSKV_EARLY: K2g early loads (0 never, 1 always, 2 when the group's keys cover < 1/4 of the range)
   bool tune_get_dedup = false;  // GET_DEDUP: K1 gathers each distinct scattered pull key once per chunk
   // PSKV_PAGEABLE_DMA: DMA pageable host buffers directly (the runtime moves
   // them at the PCIe rate, measured 55 GB/s) instead of copying them into
@@ -866,9 +867,15 @@ int sorted_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t
     // loads per batch) and leaves
     const uint32_t grid = (uint32_t)std::min<uint64_t>(
         std::max<uint64_t>(std::min<uint64_t>(ntiles, 1024), nchunks), s->tune_tile_grid);
+    // Early mode (K2g's whole-chunk loads issued before its prologue, its
+    // chunks storing their own elements): for launches whose windows are
+    // unlikely to overlap — the pushed keys cover under a quarter of the
+    // shard's range, e.g. a rank's share of cfg 4 — since it cannot skip the
+    // values of a chunk a later window covers.  Results are the same either way.
+    const bool early = s->tune_early == 1 || (s->tune_early == 2 && elems * 4 < s->range);
     LaunchTimer t(s, PSKV_K_ASSIGN_TILES, elems);
-    PSKV_HIP(launch_assign_group(s->vb, vec, s->tune_unroll, s->tune_nt, s->tune_ntp, ga, s->dview(), shift,
-                                 ntiles, grid, s->flag, epoch, s->stream));
+    PSKV_HIP(launch_assign_group(s->vb, vec, s->tune_unroll, s->tune_nt, s->tune_ntp, early, ga, s->dview(),
+                                 shift, ntiles, grid, s->flag, epoch, s->stream));
     t.done();
   }
   s->n_sorted++;
@@ -1743,6 +1750,7 @@ const Option kOptions[] = {
     PSKV_OPT("UNROLL", 4, 8, tune_unroll, int),              // 4 or 8 (others: 8)
     PSKV_OPT("NT", 0, 1, tune_nt, bool),
     PSKV_OPT("NTP", 0, 1, tune_ntp, bool),
+    PSKV_OPT("EARLY", 0, 2, tune_early, int),
     PSKV_OPT("GET_DEDUP", 0, 1, tune_get_dedup, bool),
     PSKV_OPT("PAGEABLE_DMA", 0, 1, tune_pageable_dma, bool),
     PSKV_OPT("DMA_MIN_BYTES", 0, INT64_MAX, tune_dma_min_bytes, size_t),

@@ -580,9 +580,12 @@ def test_external_stream_and_timing(cuda):
 
 @pytest.mark.parametrize("nb", [2, 9, 64, 65])
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-def test_grouped_dense_windows_mode(cuda, oracle_mod, nb, dtype):
+@pytest.mark.parametrize("early", [0, 1])
+def test_grouped_dense_windows_mode(cuda, oracle_mod, nb, dtype, early):
     """All batches contiguous windows (dense mode of the grouped sorted Add):
-    unaligned bases, overlaps, ragged lengths; later batches win."""
+    unaligned bases, overlaps, ragged lengths; later batches win.  early:
+    option EARLY forced off / on (K2g's own-range chunks, loads before the
+    prologue; f64 ignores it)."""
     import parameter_server_amd as ps
 
     rng = np.random.default_rng(100 + nb)
@@ -596,7 +599,7 @@ def test_grouped_dense_windows_mode(cuda, oracle_mod, nb, dtype):
         v = rng.standard_normal(n).astype(dtype)
         batches.append((k, v))
         oracle_mod.dense_last_wins(dense, 0, k, v)
-    with ps.Shard(0, size, dtype) as sh:
+    with ps.Shard(0, size, dtype, options={"EARLY": early}) as sh:
         before = sh.info()["n_general_launches"]
         sh.add_grouped([(tdev(k, cuda), tdev(v, cuda)) for k, v in batches], sorted_hint=True)
         got = sh.get(np.arange(size, dtype=np.uint32))
@@ -605,7 +608,8 @@ def test_grouped_dense_windows_mode(cuda, oracle_mod, nb, dtype):
 
 @pytest.mark.parametrize("key_begin", [0, 1, 2, 3])
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-def test_dense_windows_every_phase(cuda, oracle_mod, key_begin, dtype):
+@pytest.mark.parametrize("early", [0, 1])
+def test_dense_windows_every_phase(cuda, oracle_mod, key_begin, dtype, early):
     """cfg 4's producer windows start at any key: windows at every phase against
     the 16-byte parameter slots (the shard's key_begin shifts it once more),
     lengths around the dense chunk (8192 keys) and its multiples, whole windows
@@ -635,7 +639,7 @@ def test_dense_windows_every_phase(cuda, oracle_mod, key_begin, dtype):
         k = np.arange(kb + b, kb + b + n, dtype=np.uint32)
         v = rng.standard_normal(n).astype(dtype)
         batches.append((k, v))
-    with ps.Shard(kb, kb + size, dtype) as sh:
+    with ps.Shard(kb, kb + size, dtype, options={"EARLY": early}) as sh:
         for g in (batches[:27], batches[27:]):         # two grouped calls
             sh.add_grouped([(tdev(k, cuda), tdev(v, cuda)) for k, v in g], sorted_hint=True)
             for k, v in g:
@@ -680,7 +684,8 @@ def test_grouped_dense_lookalike_is_repaired(cuda, oracle_mod):
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 @pytest.mark.parametrize("phase", [0, 1, 3])
-def test_grouped_dense_lookalike_never_writes_missing_keys(cuda, oracle_mod, dtype, phase):
+@pytest.mark.parametrize("early", [0, 1])
+def test_grouped_dense_lookalike_never_writes_missing_keys(cuda, oracle_mod, dtype, phase, early):
     """A wrong sorted hint on batches whose endpoints span exactly n - 1 keys
     but which repeat one key and so MISS another, where no other batch of the
     group holds the missing key: the sorted pass must not write the missing
@@ -708,7 +713,7 @@ def test_grouped_dense_lookalike_never_writes_missing_keys(cuda, oracle_mod, dty
                 k[i] = k[i - 1]
         v = rng.standard_normal(n).astype(dtype)
         batches.append((k, v))
-    with ps.Shard(0, size, dtype) as sh:
+    with ps.Shard(0, size, dtype, options={"EARLY": early}) as sh:
         sh.add(np.arange(size, dtype=np.uint32), prior)
         for k, v in batches:
             oracle_mod.dense_last_wins(dense, 0, k, v)
@@ -1405,7 +1410,7 @@ def test_shard_options_api(cuda):
     import parameter_server_amd as ps
     from parameter_server_amd import PskvError, _lib
 
-    names = ["GENERAL", "UNROLL", "NT", "NTP", "GET_DEDUP", "PAGEABLE_DMA", "DMA_MIN_BYTES", "DMA_MIN_BYTES_GET",
+    names = ["GENERAL", "UNROLL", "NT", "NTP", "EARLY", "GET_DEDUP", "PAGEABLE_DMA", "DMA_MIN_BYTES", "DMA_MIN_BYTES_GET",
              "DMA_MIN_BYTES_PINNED", "ZC_MAX_BYTES", "FRAME_ZC_MAX_BYTES", "INLINE", "INLINE_ADD_CHUNKS",
              "INLINE_GET_CHUNKS", "ISPIN", "SERVE", "SERVE_IDLE_US", "TILE_SHIFT", "TILE_GRID", "RB_WBITS",
              "RB_NBD", "RB_TB", "RB_APPLY_LOG2", "RB_BIN_BLOCK"]

@@ -18,6 +18,8 @@
 #   sizetrace    rocprofv3 kernel trace of tools/size_probe.py (exact K2g / K4r / K1 durations and gaps)
 #   idle         tools/micro/idle_launch: an idle conditional launch's cost between two streaming kernels
 #   ztb          tools/zipf_probe.py: K5 bucket count / window width variants at the current K5b
+#   sizes_early  tools/size_probe.py with K2g early mode off / on (PSKV_EARLY=0/1), twice
+#   emu_early    ranks 0 and 1 of N = 8 emulated with early mode off / auto
 #   e2e          tools/e2e_probe.py (host-buffer Add / Get against raw PCIe copy rates)
 #   bench        bench.py --steps 20 (the driver's command line)
 #   zipf         tools/zipf_probe.py kernel times on cfg 3
@@ -71,6 +73,13 @@ for step in "$@"; do
     idle) timeout -k 10 120 "$R/tools/micro/idle_launch" > "$OUT/idle_launch.log" 2>&1 ;;
     ztb) timeout -k 10 300 python3 "$R/tools/zipf_probe.py" "" "PSKV_RB_TB=10" "PSKV_RB_TB=10,PSKV_RB_WBITS=12" \
           "PSKV_RB_WBITS=12" > "$OUT/ztb.log" 2>&1 ;;
+    sizes_early) for r in 1 2; do for e in 0 1; do
+          PSKV_EARLY=$e timeout -k 10 200 python3 "$R/tools/size_probe.py" 2,4,8,16,64 > "$OUT/size_early${e}_$r.log" 2>&1 || exit 1
+        done; done ;;
+    emu_early) for r in 0 1; do for e in 0 2; do
+          PSKV_EARLY=$e PSKV_BENCH_EMULATE=$r/8 timeout -k 10 200 python3 "$R/bench.py" --steps 50 --no-zipf \
+            --no-cpu-baseline --no-extra > "$OUT/emu8_${r}_early$e.json" 2> "$OUT/emu8_${r}_early$e.err" || exit 1
+        done; done ;;
     e2e) timeout -k 10 200 python3 "$R/tools/e2e_probe.py" > "$OUT/e2e.log" 2>&1 ;;
     bench) timeout -k 10 400 python3 "$R/bench.py" --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     profile) bash "$R/tools/gpu_profile.sh" "$(basename "$OUT")/prof" > "$OUT/profile.log" 2>&1 ;;
