@@ -20,6 +20,7 @@
 #   ztb          tools/zipf_probe.py: K5 bucket count / window width variants at the current K5b
 #   sizes_early  tools/size_probe.py with K2g early mode off / on (PSKV_EARLY=0/1), twice
 #   emu_early    ranks 0 and 1 of N = 8 emulated with early mode off / auto
+#   bench_early  the cfg-2 headline with early mode auto (off there) and forced on, twice
 #   e2e          tools/e2e_probe.py (host-buffer Add / Get against raw PCIe copy rates)
 #   bench        bench.py --steps 20 (the driver's command line)
 #   zipf         tools/zipf_probe.py kernel times on cfg 3
@@ -79,6 +80,10 @@ for step in "$@"; do
     emu_early) for r in 0 1; do for e in 0 2; do
           PSKV_EARLY=$e PSKV_BENCH_EMULATE=$r/8 timeout -k 10 200 python3 "$R/bench.py" --steps 50 --no-zipf \
             --no-cpu-baseline --no-extra > "$OUT/emu8_${r}_early$e.json" 2> "$OUT/emu8_${r}_early$e.err" || exit 1
+        done; done ;;
+    bench_early) for r in 1 2; do for e in 2 1; do
+          PSKV_EARLY=$e timeout -k 10 200 python3 "$R/bench.py" --steps 50 --no-zipf --no-cpu-baseline --no-extra \
+            > "$OUT/bench_early${e}_$r.json" 2> "$OUT/bench_early${e}_$r.err" || exit 1
         done; done ;;
     e2e) timeout -k 10 200 python3 "$R/tools/e2e_probe.py" > "$OUT/e2e.log" 2>&1 ;;
     bench) timeout -k 10 400 python3 "$R/bench.py" --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
