@@ -843,9 +843,10 @@ int replay(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t e, 
 }
 
 // Sorted path over one launch group of device-resident batches (verifying);
-// `repair` adds the conditional replay launch behind it.
+// `repair` adds the conditional replay launch behind it; `maybe_windows` false
+// (a host group proven sorted but not all windows) keeps K2g out of early mode.
 int sorted_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t e, bool vec,
-               uint32_t epoch, bool repair) {
+               uint32_t epoch, bool repair, bool maybe_windows) {
   uint64_t elems = 0;
   for (size_t i = b; i < e; ++i) elems += v[i].n;
   if (e - b == 1) {
@@ -872,7 +873,9 @@ int sorted_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t
     // unlikely to overlap — the pushed keys cover under a quarter of the
     // shard's range, e.g. a rank's share of cfg 4 — since it cannot skip the
     // values of a chunk a later window covers.  Results are the same either way.
-    const bool early = s->tune_early == 1 || (s->tune_early == 2 && elems * 4 < s->range);
+    // A host group the CPU found sorted but not all windows goes to the tile
+    // mode, where early loads would only be read again (maybe_windows false).
+    const bool early = s->tune_early == 1 || (s->tune_early == 2 && maybe_windows && elems * 4 < s->range);
     LaunchTimer t(s, PSKV_K_ASSIGN_TILES, elems);
     PSKV_HIP(launch_assign_group(s->vb, vec, s->tune_unroll, s->tune_nt, s->tune_ntp, early, ga, s->dview(),
                                  shift, ntiles, grid, s->flag, epoch, s->stream));
@@ -1445,9 +1448,9 @@ int add_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
         // K2g's dense mode takes it and its per-element check tags it; the
         // replay then applies the group in order.  Only batches the CPU proved
         // strictly contiguous cannot trip that check and skip the replay.
-        rc = sorted_add(s, v, g.first, g.second, vec, epoch, /*repair=*/!host_dense);
+        rc = sorted_add(s, v, g.first, g.second, vec, epoch, /*repair=*/!host_dense, host_dense);
       } else if (device && (flags & PSKV_SORTED_HINT)) {
-        rc = sorted_add(s, v, g.first, g.second, vec, epoch, /*repair=*/true);
+        rc = sorted_add(s, v, g.first, g.second, vec, epoch, /*repair=*/true, /*maybe_windows=*/true);
       } else {
         rc = general_add(s, v, g.first, g.second, epoch, nullptr);
       }
