@@ -62,8 +62,7 @@ __device__ __forceinline__ void st16(void* p, u32x4 v) {
 }
 
 // A 16-byte load from a DWORD-aligned address (global_load_dwordx4 needs only
-// dword alignment): a window that starts off a 16-byte slot still streams in
-// 16-byte pieces (K2g dense mode, phase != 0).
+// dword alignment): K5b reads 8-byte run entries two at a time from any entry.
 typedef unsigned int u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 template <bool NT>
 __device__ __forceinline__ void ld16a4(const uint32_t* p, uint32_t (&v)[4]) {
@@ -71,11 +70,7 @@ __device__ __forceinline__ void ld16a4(const uint32_t* p, uint32_t (&v)[4]) {
                      : *reinterpret_cast<const u32x4a4*>(p);
   v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
 }
-template <bool NT>
-__device__ __forceinline__ void ld16a4(const unsigned long long* p, unsigned long long (&v)[4]) {
-  (void)p; v[0] = v[1] = v[2] = v[3] = 0ull;  // 8-byte values never take the phase path
-}
-// ... and a 16-byte STORE to a dword-aligned address (K2g's early mode stores
+// ... and a 16-byte STORE to a dword-aligned address (K2g's own-range chunks store
 // a window's elements where they land, whatever the window's phase).
 template <bool NT>
 __device__ __forceinline__ void st16a4(uint32_t* p, const uint32_t (&v)[4]) {
@@ -574,20 +569,20 @@ __device__ __forceinline__ bool apply_segment(const DevBatch& b, uint64_t s, uin
 // first_j .. first_j + n_j - 1 (the vector_storage push of a whole parameter
 // slice).  "A later call wins" is then an interval test: key k of batch j is
 // stored unless some later batch j' > j covers k.  Work is split by elements
-// (4096 per chunk, grid-stride), so the launch is balanced like the gather;
-// each chunk intersects its key interval with the later batches' intervals
-// once (a 64-lane ballot) and elements test only the few that overlap.
-// Every element verifies k == first_j + i; a batch whose endpoints look dense
-// but whose keys are not is caught there and tagged for the repair.
+// (8192 per chunk, one workgroup each), so the launch is balanced like the
+// gather; each chunk intersects its key interval with the later batches'
+// intervals once (a 64-lane ballot) and elements test only the few that
+// overlap.  Every element verifies k == first_j + i; a batch whose endpoints
+// look dense but whose keys are not is caught there and tagged for the repair.
 // An element is stored at first_j + i only when ITS OWN key verified (a lane's
 // group of four, or a wave's span for 8-byte values, as a whole): the replay
 // behind a tagged group rewrites exactly the keys the group holds, so the
 // sorted pass must never write any other key — a look-alike batch (same
 // endpoints, a duplicate hiding a missing key) would otherwise leave a value
-// at a key no batch of the group pushed.  So each chunk verifies exactly the
-// elements it stores, [s_lo, s_hi): its own range shifted down by the window's
-// phase p (below), whose keys are read at the same dword-aligned offsets as
-// the values.
+// at a key no batch of the group pushed.
+
+// dense_chunk: 8-byte values, and batches not 16-byte aligned (4-byte values
+// in aligned batches take dense_chunk_own below).
 template <typename VT, bool VEC, int U, bool NT, bool NTP>
 __device__ __forceinline__ bool dense_chunk(const GroupArgs& ga, const DenseView& d, uint32_t c,
                                             const uint32_t* s_first, const uint32_t* s_last) {
@@ -601,16 +596,8 @@ __device__ __forceinline__ bool dense_chunk(const GroupArgs& ga, const DenseView
   const uint64_t base = (uint64_t)(c - ga.wg_prefix[j]) * CH;
   const uint64_t end = n < base + CH ? n : base + CH;
   const uint32_t first = s_first[j];
-  // Phase of the window against the 16-byte parameter slots (4-byte values):
-  // when the window starts off a slot (p != 0; cfg 4's producer windows start
-  // at any key), the chunk STORES and VERIFIES the elements [s_lo, s_hi) — its
-  // own range shifted down by p (the first chunk from 0, the last to n) — so
-  // its 16-byte parameter stores are aligned.
   const uint32_t p0 = first - d.key_begin;
-  const uint32_t ph = (sizeof(VT) == 4 && VEC) ? (p0 & 3u) : 0u;
-  const uint64_t s_lo = (ph == 0u || base == 0) ? base : base - ph;
-  const uint64_t s_hi = (ph == 0u || end == n) ? end : end - ph;
-  const uint32_t c_lo = first + (uint32_t)s_lo, c_hi = first + (uint32_t)(end - 1);
+  const uint32_t c_lo = first + (uint32_t)base, c_hi = first + (uint32_t)(end - 1);
   // later batches whose interval meets this chunk's interval (every wave computes it)
   const bool ov = lane > j && lane < ga.nb && s_first[lane] <= c_hi && s_last[lane] >= c_lo;
   const unsigned long long later = __ballot(ov);
@@ -669,106 +656,46 @@ __device__ __forceinline__ bool dense_chunk(const GroupArgs& ga, const DenseView
         }
       }
     }
-  } else if (VEC && end - base == CH) {
-    // 4-byte values, a whole chunk.  Each lane takes the elements
-    // g = i - ph .. +3 of its 16-byte piece i (slot-aligned: p0 + g == 0 mod 4;
-    // phase 0: the aligned piece i itself), their keys and values read by one
-    // dword-aligned 16-byte load each, verifies the four keys and stores the
-    // parameter slot if all four hold.  So a window at any key streams like an
-    // aligned one.  (The two aligned pieces the group straddles, selected in
-    // registers, took the kernel from 95 to 127 VGPRs; shuffling the previous
-    // lane's piece, to 134.)
-    using BT = typename std::conditional<sizeof(VT) == 4, uint32_t, VT>::type;
-    const BT* __restrict__ vb = reinterpret_cast<const BT*>(vals);
-    BT* __restrict__ pb = reinterpret_cast<BT*>(param);
-    // chunk-uniform bases (scalar registers) and 32-bit lane offsets: one
-    // address register per access instead of a 64-bit pair
-    const bool head = base == 0 && ph != 0u;  // the batch's first piece starts its group before element 0
-    const uint64_t sb = base - (head ? 0u : ph);  // element of lane offset 0
-    const uint32_t* __restrict__ kc = keys + sb;
-    const BT* __restrict__ vc = vb + sb;
-    BT* __restrict__ pc = pb + p0 + sb;
-    const uint32_t hs = head ? ph : 0u;  // the head lane's offset shift
-    uint32_t k[U][4];
-    BT v[U][4];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t o = (uint32_t)(u * kBlock + tid) * 4u;
-      if (!head || o != 0u) {
-        ld16a4<NT>(kc + (o - hs), k[u]);
-        if (!covered) ld16a4<NT>(vc + (o - hs), v[u]);
-      } else {  // group starts before element 0: its valid part one by one
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          k[u][e] = (uint32_t)e >= ph ? keys[e - ph] : first + (uint32_t)e - ph;
-          v[u][e] = (uint32_t)e >= ph && !covered ? vb[e - ph] : BT(0);
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t o = (uint32_t)(u * kBlock + tid) * 4u;
-      const uint32_t k0 = first + (uint32_t)sb + o - hs;  // the key element g = sb + o - hs must hold
-      const bool lbad = (k[u][0] != k0) | (k[u][1] != k0 + 1u) | (k[u][2] != k0 + 2u) | (k[u][3] != k0 + 3u);
-      bad |= lbad;
-      if (covered || lbad) continue;
-      if (later == 0 && (!head || o != 0u)) {
-        Vec4<BT>::template store<NTP>(pc + (o - hs), v[u]);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const uint32_t g = (uint32_t)sb + o - hs + (uint32_t)e;  // element g of the batch (head: g may be < 0)
-          if ((!head || o != 0u || (uint32_t)e >= ph) && !shadowed(first + g)) pb[p0 + g] = v[u][e];
-        }
-      }
-    }
-    // the last ph elements of the batch, when this chunk ends it: no group
-    // holds them
-    if (ph != 0u && end == n && (uint32_t)tid < ph) {
-      const uint64_t ie = n - ph + tid;
-      const bool lbad = keys[ie] != first + (uint32_t)ie;
-      bad |= lbad;
-      if (!covered && !lbad && !shadowed(first + (uint32_t)ie)) pb[p0 + ie] = vb[ie];
-    }
   } else {
     // a partial (or unaligned) chunk — the last one of every window: eight
     // elements per lane loaded together, then checked and stored, so the
     // chunk costs one dependent round trip per eight elements per lane rather
-    // than one per element (a window's 576-key tail took three in a row).
-    // It verifies and stores [s_lo, s_hi), each element on its own key.
-    for (uint64_t i0 = s_lo + tid; i0 < s_hi; i0 += 8ull * kBlock) {
+    // than one per element (a window's 576-key tail took three in a row)
+    for (uint64_t i0 = base + tid; i0 < end; i0 += 8ull * kBlock) {
       uint32_t kk[8];
       VT vv[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const uint64_t i = i0 + (uint64_t)q * kBlock;
-        kk[q] = i < s_hi ? keys[i] : first + (uint32_t)i;
-        vv[q] = i < s_hi && !covered ? vals[i] : VT(0);
+        kk[q] = i < end ? keys[i] : first + (uint32_t)i;
+        vv[q] = i < end && !covered ? vals[i] : VT(0);
       }
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const uint64_t i = i0 + (uint64_t)q * kBlock;
         const bool ebad = kk[q] != first + (uint32_t)i;
         bad |= ebad;
-        if (i < s_hi && !covered && !ebad && !shadowed(first + (uint32_t)i)) param[p0 + i] = vv[q];
+        if (i < end && !covered && !ebad && !shadowed(first + (uint32_t)i)) param[p0 + i] = vv[q];
       }
     }
   }
   return bad;
 }
 
-// Early mode (4-byte values, 16-byte aligned batches; chosen per launch by the
-// host, option EARLY): every chunk verifies and stores its OWN elements
-// [base, end) — no phase shift — so a whole chunk's keys and values are plain
-// aligned loads that depend on nothing and can be issued before the
-// workgroup's prologue (the first and last key of every batch) has come back;
-// the price is a dword-aligned 16-byte parameter store for a window off the
-// 16-byte slots, and no skipping of the values of a chunk a later window
-// covers (the values are already in flight).  It pays where a launch is small
-// (a rank's ~8 windows at N = 8: the prologue's round trip is then a visible
-// part of the launch) and windows rarely overlap.  PRE: k / v already hold
-// the chunk (a whole one); else this loads them.  Verification and stores
-// cover the same elements, each stored only if its own key verified (above).
+// 4-byte values in 16-byte aligned batches (dense_chunk_own): every chunk
+// loads its own keys and values with aligned 16-byte loads and stores them
+// where they land, a dword-aligned 16-byte store when the window starts off
+// the 16-byte parameter slots (cfg 4's producer windows start at any key).
+// Against the round-3 form that shifted each chunk down by the window's phase
+// so the stores were slot-aligned (and the loads dword-aligned), this is as
+// fast at phase 0 and 3-4 % faster at phases 1-3 (K2g 107.3-109.2 against
+// 111.0-112.8 us per 64 x 1M keys, `profiles/r03_probes/align_own/`), and it
+// has no head or tail special case.  Early mode (option EARLY, chosen per
+// launch by the host) issues a workgroup's whole-chunk loads before its
+// prologue (the first and last key of every batch) has come back; it cannot
+// skip the values of a chunk a later window covers (they are already in
+// flight), so it is for small launches whose windows rarely overlap (a rank's
+// ~8 windows at N = 8).  PRE: k / v already hold the (whole) chunk.
 template <int U, bool NT, bool NTP, bool PRE>
 __device__ __forceinline__ bool dense_chunk_own(const GroupArgs& ga, const DenseView& d, uint32_t c,
                                                 const uint32_t* s_first, const uint32_t* s_last,
@@ -855,7 +782,8 @@ template <typename VT, bool VEC, int U, bool NT, bool NTP, bool EARLY = false>
 __global__ __launch_bounds__(kBlock) void k_assign_group(GroupArgs ga, DenseView d,
                                                          uint32_t tile_shift, uint64_t ntiles,
                                                          uint32_t* flag, uint32_t epoch) {
-  static_assert(!EARLY || (sizeof(VT) == 4 && VEC), "early mode: 4-byte values, aligned batches");
+  constexpr bool OWN = sizeof(VT) == 4 && VEC;  // dense_chunk_own
+  static_assert(!EARLY || OWN, "early loads: 4-byte values, aligned batches");
   constexpr int CH = kBlock * 4 * U;
   __shared__ uint64_t s_seg_s[kMaxBatches];
   __shared__ uint64_t s_seg_e[kMaxBatches];
@@ -867,7 +795,7 @@ __global__ __launch_bounds__(kBlock) void k_assign_group(GroupArgs ga, DenseView
   const int jb = tid & 63;
   // early mode: this workgroup's first chunk, when whole, is requested now,
   // before the prologue below (its loads need no batch endpoint)
-  uint32_t ek[EARLY ? U : 1][4], ev[EARLY ? U : 1][4];
+  uint32_t ek[OWN ? U : 1][4], ev[OWN ? U : 1][4];
   bool pre = false;
   if constexpr (EARLY) {
     if (blockIdx.x < ga.wg_prefix[ga.nb]) {
@@ -916,7 +844,7 @@ __global__ __launch_bounds__(kBlock) void k_assign_group(GroupArgs ga, DenseView
   bool bad = false;
   if (s_dense) {
     const uint32_t nchunks = ga.wg_prefix[ga.nb];
-    if constexpr (EARLY) {
+    if constexpr (OWN) {
       uint32_t c = blockIdx.x;
       if (pre) {
         bad |= dense_chunk_own<U, NT, NTP, true>(ga, d, c, s_first, s_last, ek, ev);

@@ -22,6 +22,7 @@
 #   emu_early    ranks 0 and 1 of N = 8 emulated with early mode off / auto
 #   bench_early  the cfg-2 headline with early mode auto (off there) and forced on, twice
 #   fuzz2        1500 more fuzz seeds from 5000 and 8 concurrent groups (the EARLY knob and look-alikes in play)
+#   align_own    tools/align_probe.py with K2g slot-aligned chunks (EARLY=0) vs own-range chunks (EARLY=3), twice
 #   e2e          tools/e2e_probe.py (host-buffer Add / Get against raw PCIe copy rates)
 #   bench        bench.py --steps 20 (the driver's command line)
 #   zipf         tools/zipf_probe.py kernel times on cfg 3
@@ -87,6 +88,9 @@ for step in "$@"; do
     bench_early) for r in 1 2; do for e in 2 1; do
           PSKV_EARLY=$e timeout -k 10 200 python3 "$R/bench.py" --steps 50 --no-zipf --no-cpu-baseline --no-extra \
             > "$OUT/bench_early${e}_$r.json" 2> "$OUT/bench_early${e}_$r.err" || exit 1
+        done; done ;;
+    align_own) for r in 1 2; do for e in 0 3; do
+          PSKV_EARLY=$e timeout -k 10 200 python3 "$R/tools/align_probe.py" 0,1,2,3 20 > "$OUT/align_early${e}_$r.log" 2>&1 || exit 1
         done; done ;;
     e2e) timeout -k 10 200 python3 "$R/tools/e2e_probe.py" > "$OUT/e2e.log" 2>&1 ;;
     bench) timeout -k 10 400 python3 "$R/bench.py" --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
