@@ -217,31 +217,24 @@ __device__ __forceinline__ VT load_one(const DenseView& d, const Ovf& o, uint32_
 // ------------------------------------------------------------- K1 gather
 
 // Four keys of one lane: when they are four consecutive in-range keys (dense
-// pulls), 16-byte parameter loads serve them — one when the run starts on a
-// 16-byte parameter slot, else the two slots it straddles (the second one is
-// the neighbouring lane's first, so the lines are fetched once) and a select;
-// otherwise four scalar gathers.  A pulled window may start at any key (cfg 4's
-// producer windows do); per-element loads there cost K1 ~6 % (align_probe).
+// pulls), ONE 16-byte parameter load serves them, from a dword-aligned address
+// when the run starts off a 16-byte slot (a pulled window may start at any
+// key; cfg 4's producer windows do); otherwise four scalar gathers.  (Round 3
+// loaded the two slots such a run straddles and selected: K1 ran 4-6 % slower
+// at phases 1-3 than at phase 0, `profiles/r03_probes/align_probe_own_range.log`.)
 template <typename VT>
 __device__ __forceinline__ void gather4(const DenseView& d, const Ovf& o, const uint32_t (&k)[4],
                                         VT (&v)[4]) {
   const uint32_t off0 = k[0] - d.key_begin;
   const bool run = (k[1] == k[0] + 1u) & (k[2] == k[0] + 2u) & (k[3] == k[0] + 3u) &
                    ((uint64_t)off0 + 3u < d.range);
-  const uint32_t ph = off0 & 3u;
-  if (run && ph == 0u) {
+  if (run && (off0 & 3u) == 0u) {
     Vec4<VT>::load(reinterpret_cast<const VT*>(d.param) + off0, v);
   } else if (sizeof(VT) == 4 && run) {
-    // both slots start inside the array (off0 - ph >= 0; off0 - ph + 4 <= off0 + 3),
-    // and a 16-byte slot that starts inside the allocation lies inside it
-    const VT* pa = reinterpret_cast<const VT*>(d.param) + (off0 - ph);
-    VT a[4], b[4];
-    Vec4<VT>::load(pa, a);
-    Vec4<VT>::load(pa + 4, b);
-    v[0] = ph == 1u ? a[1] : ph == 2u ? a[2] : a[3];
-    v[1] = ph == 1u ? a[2] : ph == 2u ? a[3] : b[0];
-    v[2] = ph == 1u ? a[3] : ph == 2u ? b[0] : b[1];
-    v[3] = ph == 1u ? b[0] : ph == 2u ? b[1] : b[2];
+    uint32_t t[4];
+    ld16a4<false>(reinterpret_cast<const uint32_t*>(d.param) + off0, t);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = (VT)t[e];
   } else {
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = load_one<VT>(d, o, k[e]);
@@ -249,8 +242,7 @@ __device__ __forceinline__ void gather4(const DenseView& d, const Ovf& o, const 
 }
 
 // Two keys of one lane, 8-byte values: one 16-byte load when they are two
-// consecutive in-range keys on an even offset; on an odd offset the two
-// 16-byte slots they straddle.
+// consecutive in-range keys, from a dword-aligned address on an odd offset.
 __device__ __forceinline__ void gather2(const DenseView& d, const Ovf& o, const uint32_t (&k)[2],
                                         unsigned long long (&v)[2]) {
   using T = unsigned long long;
@@ -259,11 +251,10 @@ __device__ __forceinline__ void gather2(const DenseView& d, const Ovf& o, const 
   if (run && (off0 & 1u) == 0u) {
     Vec2x8::load(reinterpret_cast<const T*>(d.param) + off0, v);
   } else if (run) {
-    T a[2], b[2];
-    Vec2x8::load(reinterpret_cast<const T*>(d.param) + (off0 - 1u), a);
-    Vec2x8::load(reinterpret_cast<const T*>(d.param) + (off0 + 1u), b);
-    v[0] = a[1];
-    v[1] = b[0];
+    uint32_t t[4];
+    ld16a4<false>(reinterpret_cast<const uint32_t*>(reinterpret_cast<const T*>(d.param) + off0), t);
+    v[0] = (T)t[0] | ((T)t[1] << 32);
+    v[1] = (T)t[2] | ((T)t[3] << 32);
   } else {
     v[0] = load_one<T>(d, o, k[0]);
     v[1] = load_one<T>(d, o, k[1]);
