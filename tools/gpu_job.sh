@@ -21,6 +21,7 @@
 #   sizes_early  tools/size_probe.py with K2g early mode off / on (PSKV_EARLY=0/1), twice
 #   emu_early    ranks 0 and 1 of N = 8 emulated with early mode off / auto
 #   bench_early  the cfg-2 headline with early mode auto (off there) and forced on, twice
+#   fuzz3        1500 more fuzz seeds from 6500 and 8 concurrent groups (own-range K2g, one-load K1)
 #   fuzz2        1500 more fuzz seeds from 5000 and 8 concurrent groups (the EARLY knob and look-alikes in play)
 #   align_own    tools/align_probe.py with K2g slot-aligned chunks (EARLY=0) vs own-range chunks (EARLY=3), twice
 #   e2e          tools/e2e_probe.py (host-buffer Add / Get against raw PCIe copy rates)
@@ -69,6 +70,8 @@ for step in "$@"; do
     abz) AB_PROG=zipf timeout -k 10 900 bash "$R/tools/ab_lib.sh" "$(basename "$OUT")/abz" > "$OUT/abz.log" 2>&1 ;;
     sizes) timeout -k 10 300 python3 "$R/tools/size_probe.py" > "$OUT/size_probe.log" 2>&1 ;;
     abs) AB_PROG=sizes timeout -k 10 900 bash "$R/tools/ab_lib.sh" "$(basename "$OUT")/abs" > "$OUT/abs.log" 2>&1 ;;
+    fuzz3) FUZZ_SEED0=6500 FUZZ_SCENARIOS=1500 FUZZ_GROUPS=8 timeout -k 10 1000 python3 -u -m pytest \
+        "$R/tests/test_fuzz.py" -m gpu -q --timeout 300 --timeout-method thread > "$OUT/fuzz3.log" 2>&1 ;;
     fuzz2) FUZZ_SEED0=5000 FUZZ_SCENARIOS=1500 FUZZ_GROUPS=8 timeout -k 10 1000 python3 -u -m pytest \
         "$R/tests/test_fuzz.py" -m gpu -q --timeout 300 --timeout-method thread > "$OUT/fuzz2.log" 2>&1 ;;
     fuzz) FUZZ_SEED0=${FUZZ_SEED0:-3500} FUZZ_SCENARIOS=${FUZZ_SCENARIOS:-1500} timeout -k 10 1000 python3 -u -m pytest \
