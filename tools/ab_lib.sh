@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B two builds of libpskv.so on one box (ab/libpskv_base.so, ab/libpskv_new.so,
-# built beforehand): alternate them (swapping the in-tree library file), 3
+# built beforehand): alternate them (swapping the in-tree library file, which
+# is restored to the tree's own build on exit), 3
 # rounds each, under bench.py (default) or, with AB_PROG=zipf, under
 # tools/zipf_probe.py (the cfg-3 K5 / K1 kernel times), with AB_PROG=sizes under
 # tools/size_probe.py (K2g / K1 fixed cost per launch).
@@ -10,6 +11,10 @@ R=${GRAFT_REPO_ROOT:-$PWD}
 OUT=$R/gpurun_out/${1:-ab}
 ARGS=${2:-"--no-extra --no-cpu-baseline --no-zipf"}
 mkdir -p "$OUT"
+LIB=$R/parameter_server_amd/libpskv.so
+cp "$LIB" "$OUT/libpskv_tree.so" || exit 1   # the tree's own build, put back at the end
+restore() { cp "$OUT/libpskv_tree.so" "$LIB"; }
+trap restore EXIT
 for i in 1 2 3; do
   for v in base new; do
     cp "$R/ab/libpskv_$v.so" "$R/parameter_server_amd/libpskv.so" || exit 1
@@ -22,5 +27,4 @@ for i in 1 2 3; do
     fi
   done
 done
-cp "$R/ab/libpskv_new.so" "$R/parameter_server_amd/libpskv.so"
 echo "ab done"
