@@ -12,8 +12,8 @@ OUT=$R/gpurun_out/${1:-ab}
 ARGS=${2:-"--no-extra --no-cpu-baseline --no-zipf"}
 mkdir -p "$OUT"
 LIB=$R/parameter_server_amd/libpskv.so
-cp "$LIB" "$OUT/libpskv_tree.so" || exit 1   # the tree's own build, put back at the end
-restore() { cp "$OUT/libpskv_tree.so" "$LIB"; }
+SAVE=$(mktemp) && cp "$LIB" "$SAVE" || exit 1   # the tree's own build, put back at the end
+restore() { cp "$SAVE" "$LIB"; rm -f "$SAVE"; }
 trap restore EXIT
 for i in 1 2 3; do
   for v in base new; do
