@@ -193,7 +193,8 @@ int pskv_shard_info(pskv_shard* s, pskv_info* info);
  * GET_DEDUP, PAGEABLE_DMA, DMA_MIN_BYTES, DMA_MIN_BYTES_GET,
  * DMA_MIN_BYTES_PINNED, ZC_MAX_BYTES, FRAME_ZC_MAX_BYTES, INLINE,
  * INLINE_ADD_CHUNKS, INLINE_GET_CHUNKS, ISPIN, SERVE, SERVE_IDLE_US,
- * TILE_SHIFT, TILE_GRID, RB_WBITS, RB_NBD, RB_TB, RB_APPLY_LOG2, RB_BIN_BLOCK.  The
+ * TILE_SHIFT, TILE_GRID, RB_WBITS, RB_NBD, RB_TB, RB_APPLY_LOG2, RB_BIN_BLOCK,
+ * RB_INSERT.  The
  * environment variable PSKV_<NAME> sets a creation default.  Every option
  * changes speed only, never results.  PSKV_EINVAL for an unknown name or a
  * value out of range (the shard is unchanged). */

@@ -160,7 +160,8 @@ struct RbMap {
 // workgroups per CU, ~7 Ki entries per bucket in one pass; 14: 128 KiB, ~14 Ki).
 hipError_t launch_rb_add(int dtype, int mode, const GroupArgs& ga, uint32_t nsc,
                          const DenseView& d, const Ovf& o, const RbMap& bm,
-                         int apply_log2, int bin_block, uint16_t* loff, void* tmp, hipStream_t st);
+                         int apply_log2, int bin_block, bool lane_insert, uint16_t* loff, void* tmp,
+                         hipStream_t st);
 uint32_t rb_superchunk(int vb, int bin_block);
 constexpr size_t kRbTmpPad = 16;  // bytes past the last entry K5b may read (paired loads)
 // K8: one small host message carried in the kernarg segment (one workgroup).

@@ -1217,7 +1217,13 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t* a, uint32_t n, uint32
 // first probe of every key is issued back to back (independent LDS atomics in
 // flight); only keys that met another key probe further.  slot[q] = EMPTY for
 // invalid keys; own bit q = this lane inserted the key.
-template <int PER, int SLOTS>
+// LANE (K5a, option RB_INSERT): the keys that met another key probe on one
+// per lane per round, the lane's lowest pending key each time (selected from
+// the registers by compares, no dynamic indexing), so a round is ONE
+// compare-and-swap instruction for the whole wave and the wave pays the
+// longest per-lane sum of extra probes — not, as in the per-key loops, a
+// round of instructions per key position that any lane still probes.
+template <int PER, int SLOTS, bool LANE = false>
 __device__ __forceinline__ uint32_t lds_insert(uint32_t* hk, uint32_t* sent,
                                                const uint32_t (&key)[PER], uint32_t valid_mask,
                                                uint32_t (&slot)[PER]) {
@@ -1238,6 +1244,39 @@ __device__ __forceinline__ uint32_t lds_insert(uint32_t* hk, uint32_t* sent,
       slot[q] = fmix32(key[q]) & (SLOTS - 1);
       old[q] = atomicCAS(&hk[slot[q]], kEmpty32, key[q]);
     }
+  }
+  if constexpr (LANE) {
+    uint32_t pend = 0;  // keys that met another key: probe on
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      if (!(valid_mask >> q & 1u) || key[q] == kEmpty32) continue;
+      if (old[q] == kEmpty32)
+        own |= 1u << q;
+      else if (old[q] != key[q])
+        pend |= 1u << q;
+    }
+    while (pend) {
+      const uint32_t q = (uint32_t)__builtin_ctz(pend);
+      uint32_t kq = key[0], hq = slot[0];
+#pragma unroll
+      for (int e = 1; e < PER; ++e)
+        if (q == (uint32_t)e) {
+          kq = key[e];
+          hq = slot[e];
+        }
+      hq = (hq + 1) & (SLOTS - 1);
+      const uint32_t o = atomicCAS(&hk[hq], kEmpty32, kq);
+#pragma unroll
+      for (int e = 0; e < PER; ++e)
+        if (q == (uint32_t)e) slot[e] = hq;
+      if (o == kEmpty32) {
+        own |= 1u << q;
+        pend &= ~(1u << q);
+      } else if (o == kq) {
+        pend &= ~(1u << q);
+      }
+    }
+    return own;
   }
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
@@ -1293,7 +1332,7 @@ constexpr uint32_t rb_sc(int binb) {
   return (sizeof(BT) == 8 ? 4u : 8u) * (uint32_t)binb;
 }
 
-template <typename AT, typename BT, int MODE, int BINB>
+template <typename AT, typename BT, int MODE, int BINB, bool LANEINS = false>
 __global__ __launch_bounds__(BINB) void k_rb_bin(GroupArgs ga, DenseView d, RbMap bm,
                                                  uint32_t nbk,
                                                  uint16_t* __restrict__ loff, uint32_t nsc,
@@ -1397,7 +1436,7 @@ __global__ __launch_bounds__(BINB) void k_rb_bin(GroupArgs ga, DenseView d, RbMa
 #pragma unroll
     for (int q = 0; q < KPT; ++q) valid |= li_of(q) < cur.nvalid ? (1u << q) : 0u;
     uint32_t slot[KPT];
-    const uint32_t own = lds_insert<KPT, SLOTS>(hk, &sent, kc, valid, slot);
+    const uint32_t own = lds_insert<KPT, SLOTS, LANEINS>(hk, &sent, kc, valid, slot);
 #pragma unroll
     for (int q = 0; q < KPT; ++q) {
       if (!(valid >> q & 1u)) continue;
@@ -2619,8 +2658,8 @@ hipError_t launch_ovf_rehash(int vb, const Ovf& from, uint64_t from_cap, const O
 
 template <typename AT, typename BT, int MODE>
 static hipError_t rb_launch(const GroupArgs& ga, uint32_t nsc, const DenseView& d, const Ovf& o,
-                            const RbMap& bm, int apply_log2, int bin_block, uint16_t* loff, void* tmp,
-                            hipStream_t st) {
+                            const RbMap& bm, int apply_log2, int bin_block, bool lane_insert, uint16_t* loff,
+                            void* tmp, hipStream_t st) {
   const uint32_t nbk = bm.nbd + 1;
   auto* t = reinterpret_cast<RbEnt<sizeof(BT)>*>(tmp);
   // persistent grid: one 1024-thread workgroup per CU (~139 KiB LDS), or two
@@ -2629,6 +2668,8 @@ static hipError_t rb_launch(const GroupArgs& ga, uint32_t nsc, const DenseView& 
   const uint32_t gb = nsc < wgs ? nsc : wgs;
   if (bin_block == 512)
     k_rb_bin<AT, BT, MODE, 512><<<gb, 512, 0, st>>>(ga, d, bm, nbk, loff, nsc, t);
+  else if (lane_insert)
+    k_rb_bin<AT, BT, MODE, 1024, true><<<gb, 1024, 0, st>>>(ga, d, bm, nbk, loff, nsc, t);
   else
     k_rb_bin<AT, BT, MODE, 1024><<<gb, 1024, 0, st>>>(ga, d, bm, nbk, loff, nsc, t);
   const uint32_t sc = rb_sc<BT>(bin_block);
@@ -2641,12 +2682,13 @@ static hipError_t rb_launch(const GroupArgs& ga, uint32_t nsc, const DenseView& 
 
 hipError_t launch_rb_add(int dtype, int mode, const GroupArgs& ga, uint32_t nsc,
                          const DenseView& d, const Ovf& o, const RbMap& bm,
-                         int apply_log2, int bin_block, uint16_t* loff, void* tmp, hipStream_t st) {
+                         int apply_log2, int bin_block, bool lane_insert, uint16_t* loff, void* tmp,
+                         hipStream_t st) {
   if (nsc == 0) return hipSuccess;
   if (bm.nbd + 1 > (uint32_t)kRbMaxBuckets || nsc > kRbMaxSc || bm.nbd == 0 ||
       (bin_block != 512 && bin_block != 1024))
     return hipErrorInvalidValue;
-#define PSKV_RB(AT, BT, M) rb_launch<AT, BT, M>(ga, nsc, d, o, bm, apply_log2, bin_block, loff, tmp, st)
+#define PSKV_RB(AT, BT, M) rb_launch<AT, BT, M>(ga, nsc, d, o, bm, apply_log2, bin_block, lane_insert, loff, tmp, st)
   if (mode == 0) {
     if (dtype == 0) return PSKV_RB(int, uint32_t, 0);
     if (dtype == 1) return PSKV_RB(float, uint32_t, 0);

@@ -303,6 +303,7 @@ struct pskv_shard {
   unsigned int ireply_seq = 0;
   int tune_rb_apply_log2 = 0; // PSKV_RB_APPLY_LOG2: 13 or 14 (0 = by bucket size)
   int tune_rb_bin_block = kRbBinBlockDefault;  // PSKV_RB_BIN_BLOCK: K5a workgroup, 512 or 1024
+  bool tune_rb_insert = false;  // PSKV_RB_INSERT: K5a probes one pending key per lane per round (1) or per key (0)
   // K9 request server (PSKV_SERVE=1): the inline-size messages go to a ring in
   // coherent page-locked memory that one resident workgroup polls
   // (PSKV_SERVE_IDLE_US: it leaves after this long without a request)
@@ -751,7 +752,7 @@ int radix_launch(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size
   if (rc) return rc;
   LaunchTimer t(s, PSKV_K_RADIX, elems);
   PSKV_HIP(launch_rb_add(s->dtype, s->mode, ga, nsc, s->dview(), s->ovf, bm, apply_log2,
-                         s->tune_rb_bin_block, s->rb_loff, s->rb_ent, s->stream));
+                         s->tune_rb_bin_block, s->tune_rb_insert, s->rb_loff, s->rb_ent, s->stream));
   t.done();
   s->n_general += 2;
   return PSKV_OK;
@@ -1774,6 +1775,7 @@ const Option kOptions[] = {
     PSKV_OPT("RB_TB", 0, 11, tune_rb_tb, uint32_t),
     PSKV_OPT("RB_APPLY_LOG2", 0, 14, tune_rb_apply_log2, int),  // 0 = by size, 13 or 14
     PSKV_OPT("RB_BIN_BLOCK", 512, 1024, tune_rb_bin_block, int),  // 512 or 1024
+    PSKV_OPT("RB_INSERT", 0, 1, tune_rb_insert, bool),
 };
 #undef PSKV_OPT
 

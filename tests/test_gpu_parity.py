@@ -1413,7 +1413,7 @@ def test_shard_options_api(cuda):
     names = ["GENERAL", "UNROLL", "NT", "NTP", "EARLY", "GET_DEDUP", "PAGEABLE_DMA", "DMA_MIN_BYTES", "DMA_MIN_BYTES_GET",
              "DMA_MIN_BYTES_PINNED", "ZC_MAX_BYTES", "FRAME_ZC_MAX_BYTES", "INLINE", "INLINE_ADD_CHUNKS",
              "INLINE_GET_CHUNKS", "ISPIN", "SERVE", "SERVE_IDLE_US", "TILE_SHIFT", "TILE_GRID", "RB_WBITS",
-             "RB_NBD", "RB_TB", "RB_APPLY_LOG2", "RB_BIN_BLOCK"]
+             "RB_NBD", "RB_TB", "RB_APPLY_LOG2", "RB_BIN_BLOCK", "RB_INSERT"]
     with ps.Shard(0, 1000, np.float32) as sh:
         for n in names:
             sh.set_option(n, sh.get_option(n))  # every default is a valid value

@@ -25,6 +25,7 @@
 #   fuzz2        1500 more fuzz seeds from 5000 and 8 concurrent groups (the EARLY knob and look-alikes in play)
 #   align_own    tools/align_probe.py with K2g slot-aligned chunks (EARLY=0) vs own-range chunks (EARLY=3), twice
 #   zwbits       K5 bucket windows of 2^11 (default) vs 2^12 keys on cfg-3 Zipf and on unhinted dense pushes
+#   rbins        K5a per-lane probe insert (RB_INSERT=1): the K5 parity tests under it, then the cfg-3 A/B
 #   e2e          tools/e2e_probe.py (host-buffer Add / Get against raw PCIe copy rates)
 #   bench        bench.py --steps 20 (the driver's command line)
 #   zipf         tools/zipf_probe.py kernel times on cfg 3
@@ -99,6 +100,10 @@ for step in "$@"; do
     zwbits) PROBE_ROUNDS=10 timeout -k 10 300 python3 "$R/tools/zipf_probe.py" "" "PSKV_RB_WBITS=12" > "$OUT/zwbits_zipf.log" 2>&1 &&
         PROBE_ROUNDS=10 PROBE_WORKLOAD=dense timeout -k 10 300 python3 "$R/tools/zipf_probe.py" "" "PSKV_RB_WBITS=12" \
           > "$OUT/zwbits_dense.log" 2>&1 ;;
+    rbins) PSKV_RB_INSERT=1 timeout -k 10 400 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread \
+          "$R/tests/test_gpu_parity.py" -k "zipf or radix or random or golden or accumulate or sentinel or ragged" \
+          > "$OUT/rbins_tests.log" 2>&1 &&
+        PROBE_ROUNDS=10 timeout -k 10 300 python3 "$R/tools/zipf_probe.py" "" "PSKV_RB_INSERT=1" > "$OUT/rbins_zipf.log" 2>&1 ;;
     e2e) timeout -k 10 200 python3 "$R/tools/e2e_probe.py" > "$OUT/e2e.log" 2>&1 ;;
     bench) timeout -k 10 400 python3 "$R/bench.py" --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     profile) bash "$R/tools/gpu_profile.sh" "$(basename "$OUT")/prof" > "$OUT/profile.log" 2>&1 ;;
