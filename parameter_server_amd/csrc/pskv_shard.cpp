@@ -303,7 +303,7 @@ struct pskv_shard {
   unsigned int ireply_seq = 0;
   int tune_rb_apply_log2 = 0; // PSKV_RB_APPLY_LOG2: 13 or 14 (0 = by bucket size)
   int tune_rb_bin_block = kRbBinBlockDefault;  // PSKV_RB_BIN_BLOCK: K5a workgroup, 512 or 1024
-  bool tune_rb_insert = false;  // PSKV_RB_INSERT: K5a probes one pending key per lane per round (1) or per key (0)
+  bool tune_rb_insert = false;  // PSKV_RB_INSERT: K5a probes one pending key per lane per round (1; measured 3 % slower) or per key (0)
   // K9 request server (PSKV_SERVE=1): the inline-size messages go to a ring in
   // coherent page-locked memory that one resident workgroup polls
   // (PSKV_SERVE_IDLE_US: it leaves after this long without a request)
