@@ -6,6 +6,7 @@
 #   align        tools/align_probe.py (window phase cost)
 #   emu          bench.py as rank 0 of 8 and of 2 (one rank's cfg-4 share alone)
 #   emu8all      bench.py as each of the 8 ranks of N = 8 in turn (every rank's cfg-4 share alone)
+#   emu_curve    every rank of N = 2 and N = 4 emulated in turn (with emu8all: the estimated scaling curve)
 #   emutrace     rocprofv3 kernel trace of rank 0 of 8 (kernel durations and gaps of a small share)
 #   emu_unroll   rank 0 of 8 at 4 x 4 keys per lane (PSKV_UNROLL=4) and at the default 8
 #   ztrace       rocprofv3 kernel trace of zipf_probe at K5a 1024 and 512 threads (K5a / K5b split)
@@ -56,6 +57,10 @@ for step in "$@"; do
           PSKV_BENCH_EMULATE=$r/8 timeout -k 10 200 python3 "$R/bench.py" --steps 50 --no-zipf --no-cpu-baseline \
             --no-extra > "$OUT/emu8_$r.json" 2> "$OUT/emu8_$r.err" || exit 1
         done ;;
+    emu_curve) for n in 2 4; do for r in $(seq 0 $((n - 1))); do
+          PSKV_BENCH_EMULATE=$r/$n timeout -k 10 200 python3 "$R/bench.py" --steps 50 --no-zipf --no-cpu-baseline \
+            --no-extra > "$OUT/emu${n}_$r.json" 2> "$OUT/emu${n}_$r.err" || exit 1
+        done; done ;;
     emutrace) PSKV_BENCH_EMULATE=0/8 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/emutrace" -o run \
           -- python3 "$R/bench.py" --steps 50 --no-zipf --no-cpu-baseline --no-extra > "$OUT/emutrace.log" 2>&1 ;;
     emu_unroll) PSKV_BENCH_EMULATE=0/8 PSKV_UNROLL=4 timeout -k 10 200 python3 "$R/bench.py" --steps 20 --no-zipf \
