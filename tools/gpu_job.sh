@@ -28,6 +28,7 @@
 #   zwbits       K5 bucket windows of 2^11 (default) vs 2^12 keys on cfg-3 Zipf and on unhinted dense pushes
 #   rbins        K5a per-lane probe insert (RB_INSERT=1): the K5 parity tests under it, then the cfg-3 A/B
 #   smoke        __graft_entry__.smoke() (what the driver runs before the bench)
+#   shardsize    tools/shard_size_probe.py: K2g / K1 per key on 1e8 / 5e8 / 1e9-key shards (same windows)
 #   e2e          tools/e2e_probe.py (host-buffer Add / Get against raw PCIe copy rates)
 #   bench        bench.py --steps 20 (the driver's command line)
 #   zipf         tools/zipf_probe.py kernel times on cfg 3
@@ -112,6 +113,8 @@ for step in "$@"; do
         PROBE_ROUNDS=10 timeout -k 10 300 python3 "$R/tools/zipf_probe.py" "" "PSKV_RB_INSERT=1" > "$OUT/rbins_zipf.log" 2>&1 ;;
     smoke) timeout -k 10 300 python3 -c "import sys; sys.path.insert(0, '$R'); import __graft_entry__ as g; g.smoke()" \
         > "$OUT/smoke.log" 2>&1 ;;
+    shardsize) timeout -k 10 400 python3 "$R/tools/shard_size_probe.py" > "$OUT/shard_size.log" 2>&1 &&
+        FLUSH=1 timeout -k 10 400 python3 "$R/tools/shard_size_probe.py" > "$OUT/shard_size_flush.log" 2>&1 ;;
     e2e) timeout -k 10 200 python3 "$R/tools/e2e_probe.py" > "$OUT/e2e.log" 2>&1 ;;
     bench) timeout -k 10 400 python3 "$R/bench.py" --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     profile) bash "$R/tools/gpu_profile.sh" "$(basename "$OUT")/prof" > "$OUT/profile.log" 2>&1 ;;
