@@ -114,8 +114,8 @@ struct Ovf {
 // nt: non-temporal loads/stores of the streamed push/pull buffers.
 // dedup: 4-byte values, scattered pull keys gathered once per distinct key per
 // workgroup chunk (an LDS table; dense chunks skip it)
-hipError_t launch_gather(int vb, bool vec, int unroll, bool nt, bool dedup, const GroupArgs& ga, uint32_t nwg,
-                         const DenseView& d, const Ovf& o, hipStream_t st);
+hipError_t launch_gather(int vb, bool vec, int unroll, bool nt, bool dedup, bool ntp, const GroupArgs& ga,
+                         uint32_t nwg, const DenseView& d, const Ovf& o, hipStream_t st);
 hipError_t launch_assign_sorted(int vb, bool vec, const uint32_t* keys, const void* vals,
                                 uint64_t n, const DenseView& d, uint32_t* flag, uint32_t epoch,
                                 hipStream_t st);

@@ -222,17 +222,17 @@ __device__ __forceinline__ VT load_one(const DenseView& d, const Ovf& o, uint32_
 // key; cfg 4's producer windows do); otherwise four scalar gathers.  (Round 3
 // loaded the two slots such a run straddles and selected: K1 ran 4-6 % slower
 // at phases 1-3 than at phase 0, `profiles/r03_probes/align_probe_own_range.log`.)
-template <typename VT>
+template <typename VT, bool NTP = false>
 __device__ __forceinline__ void gather4(const DenseView& d, const Ovf& o, const uint32_t (&k)[4],
                                         VT (&v)[4]) {
   const uint32_t off0 = k[0] - d.key_begin;
   const bool run = (k[1] == k[0] + 1u) & (k[2] == k[0] + 2u) & (k[3] == k[0] + 3u) &
                    ((uint64_t)off0 + 3u < d.range);
   if (run && (off0 & 3u) == 0u) {
-    Vec4<VT>::load(reinterpret_cast<const VT*>(d.param) + off0, v);
+    Vec4<VT>::template load<NTP>(reinterpret_cast<const VT*>(d.param) + off0, v);
   } else if (sizeof(VT) == 4 && run) {
     uint32_t t[4];
-    ld16a4<false>(reinterpret_cast<const uint32_t*>(d.param) + off0, t);
+    ld16a4<NTP>(reinterpret_cast<const uint32_t*>(d.param) + off0, t);
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = (VT)t[e];
   } else {
@@ -276,7 +276,7 @@ __device__ __forceinline__ uint32_t dedup_slot(uint32_t key) {
   return __umulhi(fmix32(key), kDedupSlots);
 }
 
-template <typename VT, bool VEC, int U, bool NT, bool DEDUP>
+template <typename VT, bool VEC, int U, bool NT, bool DEDUP, bool NTP = false>
 __global__ __launch_bounds__(kBlock) void k_gather(GroupArgs ga, DenseView d, Ovf o) {
   constexpr int CH = kBlock * 4 * U;
   __shared__ unsigned long long s_ent[DEDUP ? kDedupSlots : 1];  // key | element id << 32
@@ -340,7 +340,7 @@ __global__ __launch_bounds__(kBlock) void k_gather(GroupArgs ga, DenseView d, Ov
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           if (runs >> u & 1u) {
-            gather4<VT>(d, o, k[u], v[u]);
+            gather4<VT, NTP>(d, o, k[u], v[u]);
             continue;
           }
 #pragma unroll
@@ -369,7 +369,7 @@ __global__ __launch_bounds__(kBlock) void k_gather(GroupArgs ga, DenseView d, Ov
     }
     if (!dedup) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) gather4<VT>(d, o, k[u], v[u]);
+      for (int u = 0; u < U; ++u) gather4<VT, NTP>(d, o, k[u], v[u]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -2493,11 +2493,13 @@ static void gather_dispatch(int unroll, bool nt, uint32_t nwg, const GroupArgs& 
   }
 }
 
-hipError_t launch_gather(int vb, bool vec, int unroll, bool nt, bool dedup, const GroupArgs& ga, uint32_t nwg,
-                         const DenseView& d, const Ovf& o, hipStream_t st) {
+hipError_t launch_gather(int vb, bool vec, int unroll, bool nt, bool dedup, bool ntp, const GroupArgs& ga,
+                         uint32_t nwg, const DenseView& d, const Ovf& o, hipStream_t st) {
   if (nwg == 0) return hipSuccess;
   if (vb == 4) {
-    if (vec && dedup)
+    if (vec && ntp && !dedup && unroll == 8 && nt)  // option GET_NTP: non-temporal parameter loads
+      k_gather<uint32_t, true, 8, true, false, true><<<nwg, kBlock, 0, st>>>(ga, d, o);
+    else if (vec && dedup)
       gather_dispatch<uint32_t, true, true>(unroll, nt, nwg, ga, d, o, st);
     else if (vec)
       gather_dispatch<uint32_t, true>(unroll, nt, nwg, ga, d, o, st);

@@ -257,6 +257,7 @@ struct pskv_shard {
   int tune_unroll = 8;   // PSKV_UNROLL: 4 or 8 (8: measured +5 % on the dense Add)
   bool tune_nt = true;   // PSKV_NT: non-temporal streams (measured +12-15 % on K1 / K2g)
   bool tune_ntp = false; // PSKV_NTP: non-temporal parameter stores (dense Add)
+  bool tune_get_ntp = false;  // PSKV_GET_NTP: non-temporal parameter loads in K1 (4-byte values, 16-byte aligned runs)
   int tune_early = 2;    // PSKV_EARLY: K2g early loads (0 never, 1 always, 2 when the group's keys cover < 1/4 of the range)
   bool tune_get_dedup = false;  // GET_DEDUP: K1 gathers each distinct scattered pull key once per chunk
   // PSKV_PAGEABLE_DMA: DMA pageable host buffers directly (the runtime moves
@@ -1488,7 +1489,7 @@ int zero_copy_get_views(pskv_shard* s, const std::vector<pskv_batch>& hv) {
     uint64_t elems = 0;
     for (size_t i = g.first; i < g.second; ++i) elems += hv[i].n;
     LaunchTimer t(s, PSKV_K_GATHER, elems);
-    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, s->tune_get_dedup, ga, nwg, s->dview(), s->ovf, s->stream));
+    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, s->tune_get_dedup, s->tune_get_ntp, ga, nwg, s->dview(), s->ovf, s->stream));
     t.done();
   }
   PSKV_HIP(hipStreamSynchronize(s->stream));
@@ -1519,7 +1520,7 @@ int zero_copy_get(pskv_shard* s, const std::vector<pskv_batch>& v, bool vec) {
     uint64_t elems = 0;
     for (size_t i = g.first; i < g.second; ++i) elems += hv[i].n;
     LaunchTimer t(s, PSKV_K_GATHER, elems);
-    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, s->tune_get_dedup, ga, nwg, s->dview(), s->ovf, s->stream));
+    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, s->tune_get_dedup, s->tune_get_ntp, ga, nwg, s->dview(), s->ovf, s->stream));
     t.done();
   }
   PSKV_HIP(hipStreamSynchronize(s->stream));
@@ -1584,7 +1585,7 @@ int pinned_get(pskv_shard* s, const std::vector<pskv_batch>& v) {
     uint64_t elems = 0;
     for (size_t i = b; i < e; ++i) elems += dv[i].n;
     LaunchTimer t(s, PSKV_K_GATHER, elems);
-    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, s->tune_get_dedup, ga, nwg, s->dview(),
+    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, s->tune_get_dedup, s->tune_get_ntp, ga, nwg, s->dview(),
                            s->ovf, s->stream));
     t.done();
     PSKV_HIP(hipEventRecord(s->out_events[w], s->stream));
@@ -1678,7 +1679,7 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
     uint64_t elems = 0;
     for (size_t i = g.first; i < g.second; ++i) elems += dv[i].n;
     LaunchTimer t(s, PSKV_K_GATHER, elems);
-    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, s->tune_get_dedup, ga, nwg, s->dview(), s->ovf,
+    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, s->tune_get_dedup, s->tune_get_ntp, ga, nwg, s->dview(), s->ovf,
                            s->stream));
     t.done();
   }
@@ -1756,6 +1757,7 @@ const Option kOptions[] = {
     PSKV_OPT("NTP", 0, 1, tune_ntp, bool),
     PSKV_OPT("EARLY", 0, 2, tune_early, int),
     PSKV_OPT("GET_DEDUP", 0, 1, tune_get_dedup, bool),
+    PSKV_OPT("GET_NTP", 0, 1, tune_get_ntp, bool),
     PSKV_OPT("PAGEABLE_DMA", 0, 1, tune_pageable_dma, bool),
     PSKV_OPT("DMA_MIN_BYTES", 0, INT64_MAX, tune_dma_min_bytes, size_t),
     PSKV_OPT("DMA_MIN_BYTES_GET", 0, INT64_MAX, tune_dma_min_bytes_get, size_t),

@@ -1410,7 +1410,7 @@ def test_shard_options_api(cuda):
     import parameter_server_amd as ps
     from parameter_server_amd import PskvError, _lib
 
-    names = ["GENERAL", "UNROLL", "NT", "NTP", "EARLY", "GET_DEDUP", "PAGEABLE_DMA", "DMA_MIN_BYTES", "DMA_MIN_BYTES_GET",
+    names = ["GENERAL", "UNROLL", "NT", "NTP", "EARLY", "GET_DEDUP", "GET_NTP", "PAGEABLE_DMA", "DMA_MIN_BYTES", "DMA_MIN_BYTES_GET",
              "DMA_MIN_BYTES_PINNED", "ZC_MAX_BYTES", "FRAME_ZC_MAX_BYTES", "INLINE", "INLINE_ADD_CHUNKS",
              "INLINE_GET_CHUNKS", "ISPIN", "SERVE", "SERVE_IDLE_US", "TILE_SHIFT", "TILE_GRID", "RB_WBITS",
              "RB_NBD", "RB_TB", "RB_APPLY_LOG2", "RB_BIN_BLOCK", "RB_INSERT"]

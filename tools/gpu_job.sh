@@ -29,6 +29,7 @@
 #   rbins        K5a per-lane probe insert (RB_INSERT=1): the K5 parity tests under it, then the cfg-3 A/B
 #   smoke        __graft_entry__.smoke() (what the driver runs before the bench)
 #   shardsize    tools/shard_size_probe.py: K2g / K1 per key on 1e8 / 5e8 / 1e9-key shards (same windows)
+#   getntp       tools/shard_size_probe.py with K1 parameter loads cached / non-temporal (GET_NTP=0/1), twice
 #   e2e          tools/e2e_probe.py (host-buffer Add / Get against raw PCIe copy rates)
 #   bench        bench.py --steps 20 (the driver's command line)
 #   zipf         tools/zipf_probe.py kernel times on cfg 3
@@ -115,6 +116,9 @@ for step in "$@"; do
         > "$OUT/smoke.log" 2>&1 ;;
     shardsize) timeout -k 10 400 python3 "$R/tools/shard_size_probe.py" > "$OUT/shard_size.log" 2>&1 &&
         FLUSH=1 timeout -k 10 400 python3 "$R/tools/shard_size_probe.py" > "$OUT/shard_size_flush.log" 2>&1 ;;
+    getntp) for r in 1 2; do for e in 0 1; do
+          PSKV_GET_NTP=$e timeout -k 10 400 python3 "$R/tools/shard_size_probe.py" > "$OUT/getntp${e}_$r.log" 2>&1 || exit 1
+        done; done ;;
     e2e) timeout -k 10 200 python3 "$R/tools/e2e_probe.py" > "$OUT/e2e.log" 2>&1 ;;
     bench) timeout -k 10 400 python3 "$R/bench.py" --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     profile) bash "$R/tools/gpu_profile.sh" "$(basename "$OUT")/prof" > "$OUT/profile.log" 2>&1 ;;
