@@ -1,32 +1,34 @@
 """bench.py — device-resident KV Add+Get throughput (BASELINE.json metric).
 
 One step = one pass of the hot path over one push set and one pull set: a
-grouped Add of the step's push batches, then a grouped Get of the batches the
-NEXT step will push — the parameter-server worker loop, pipelined: push this
-round's parameters, pull the ones the next round updates.  Consecutive steps
-rotate over R window sets (--sets, default 16; set r drawn with seed
-set_seed(r), set 0 being the config's own seed).  The Get therefore reads
-parameters the step did not just write (the windows both sets share aside), and
-a step touches more than 256 MB of parameters (push set ∪ pull set, reported as
-config.param_bytes_touched_per_step), so the Infinity Cache cannot hold them
-from the Add to the Get.  The round-2 form (the Get pulls the windows it just
-pushed: 192 MB of parameters, Infinity-Cache warm) is kept as
-extra.cache_warm_step.  Inputs are resident in HBM before timing.
+grouped Add of the step's push batches, then a grouped Get of windows the push
+did NOT touch (zero push/pull overlap, config.push_pull_overlap_keys = 0;
+round 4).  Consecutive steps rotate over R window sets (--sets, default 16;
+set r drawn with seed set_seed(r), set 0 being the config's own seed).  The
+round-2 form (the Get pulls the windows it just pushed, Infinity-Cache warm)
+is kept as extra.cache_warm_step.  Inputs are resident in HBM before timing.
 
   N = 1: configs[1] (cfg 2) — 1e8-key float shard, J x 1M contiguous-key
          windows at uniform 1M-aligned bases (seed 42 for set 0), vals U(-1,1),
-         assign mode.
+         assign mode; the pull is every window slot of the shard's 100 that the
+         push set left free (~52), in a seeded order.  The 1e8-key shard is
+         400 MB against the 256 MB Infinity Cache, so part of the array stays
+         cached across steps whatever the step does: roofline.cold runs the same
+         step on a 1e9-key shard (4 GB, cfg 4's whole key space; a window
+         recurs every ~8 steps), where HBM serves every byte.
   N > 1: configs[3] (cfg 4) — 1e9 keys range-partitioned over N GPUs (one
          shard per rank, base/range_partition_manager.hpp's map).  J = 64
          producer streams; stream s pushes a contiguous 1M window at a uniformly
          random base in [0, 1e9 - 1M] (seed 1000 + s for set 0), which the range
-         map slices — a window straddling a boundary splits in two.  Each rank
-         applies the slices routed to it, in producer order, as one grouped
-         Add (the server's grouped flush), and pulls likewise.  The total work
-         per step is fixed (64 windows): "scaling": "strong".  The weak-scaled
-         form (64 windows inside every rank's own range) is extra.weak_scaled.
-         No collective on the data path; torch.distributed (RCCL) only for the
-         barrier and the max-time / sum-bytes reductions.
+         map slices — a window straddling a boundary splits in two.  The pull
+         is J windows at random bases meeting no pushed window and no other
+         pulled one, sliced the same way.  Each rank applies the slices routed
+         to it, in producer order, as one grouped Add (the server's grouped
+         flush), and pulls likewise.  The total work per step is fixed:
+         "scaling": "strong".  The weak-scaled form (64 windows inside every
+         rank's own range) is extra.weak_scaled.  No collective on the data
+         path; torch.distributed (RCCL) only for the barrier and the max-time /
+         sum-bytes reductions.
 
 Bytes per step (counting what the step must move):
   Add (assign)  n*4 keys + u*V values + u*V parameter writes, u = distinct keys
@@ -34,9 +36,10 @@ Bytes per step (counting what the step must move):
                 window shadowed by a later one in the step costs its keys only)
   Get           q*(4+2V) (key read + parameter read + value write)
 
-Prints ONE JSON line on rank 0 with roofline (dominant kernel, HIP events on
-the launch stream) and cpu_baseline (the oracle restatement of the reference
-storages timed on this host, N = 1 only).
+Prints ONE JSON line on rank 0 with roofline (per-kernel rates from HIP events
+on the launch stream, the dominant kernel's as `frac`, and the cold form's) and
+cpu_baseline (the oracle restatement of the reference storages timed on this
+host, N = 1 only).
 """
 from __future__ import annotations
 
@@ -76,6 +79,10 @@ def parse(argv=None):
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extra", action="store_true", help="skip the side measurements (e2e, f64, accumulate)")
     p.add_argument("--no-zipf", action="store_true", help="skip the cfg-3 sparse (Zipf) measurement")
+    p.add_argument("--no-cold", action="store_true", help="skip the cold (HBM-served) form on a 1e9-key shard")
+    p.add_argument("--cold-only", action="store_true",
+                   help="run only the cold form (N = 1) and print its record (rocprof summaries of that form)")
+    p.add_argument("--cold-keys", type=float, default=1e9, help="shard size of the cold form")
     p.add_argument("--cpu-batches", type=int, default=64,
                    help="1M-key windows in the 1-thread CPU baseline sample (~10 s)")
     p.add_argument("--vector-sizes", default="100000,200000,300000",
@@ -150,21 +157,22 @@ def sum_over_ranks(x, world, dev):
 # ------------------------------------------------------------------ planning
 
 
-def plan_rank(rank, world, J, B, r=0, weak=False, bases=None):
-    """Key range and window slices (window set r) of one rank — pure host logic,
+def plan_rank(rank, world, J, B, r=0, weak=False, bases=None, space=None):
+    """Key range and push slices (window set r) of one rank — pure host logic,
     tested on CPU (tests/test_oracle.py, tests/test_dist.py with gloo).
 
     Returns (key_space, lo, hi, slices, bases): slices = [(window w, first key,
     length)] routed to this rank, in producer order; bases = the set's window
-    bases (every rank's).  N = 1: cfg 2.  N > 1: cfg 4 (global producer windows
-    through the range map), or with weak=True the weak-scaled form (J aligned
-    windows inside this rank's range).  `bases` (N > 1) replaces the drawn
-    producer windows (tests)."""
+    bases (every rank's).  N = 1: cfg 2 (or, with `space`, the same draw on a
+    shard of `space` keys: the cold form).  N > 1: cfg 4 (global producer
+    windows through the range map), or with weak=True the weak-scaled form (J
+    aligned windows inside this rank's range).  `bases` (N > 1) replaces the
+    drawn producer windows (tests)."""
     from parameter_server_amd import workload
 
     seed = workload.set_seed(r, world)
     if world == 1:
-        key_space = 100_000_000
+        key_space = space or 100_000_000
         lo, hi = 0, key_space
         bases = workload.dense_bases(J, key_space, B, seed=seed)
         slices = [(j, int(b), B) for j, b in enumerate(bases)]
@@ -186,6 +194,32 @@ def plan_rank(rank, world, J, B, r=0, weak=False, bases=None):
     return key_space, lo, hi, slices, bases
 
 
+def plan_pull(rank, world, J, B, r, push_bases, weak=False, space=None, n_pull=None):
+    """Pull slices of window set r's step: windows DISJOINT from the step's push
+    set (zero push/pull overlap), each pulled once.  N = 1 and the weak-scaled
+    form: every aligned window slot the push set left free (cfg 2: ~52 of the
+    shard's 100), in a seeded order, at most n_pull of them.  N > 1 (cfg 4): J
+    windows at uniformly random bases that meet no pushed window and no other
+    pulled one, sliced by the range map like the pushes.  Returns (slices,
+    bases) as plan_rank."""
+    from parameter_server_amd import workload
+
+    seed = workload.set_seed(r, world) + 7
+    if world == 1:
+        key_space = space or 100_000_000
+        bases = workload.complement_windows(push_bases, 0, key_space, B, seed=seed, n_max=n_pull)
+        return [(j, int(b), B) for j, b in enumerate(bases)], bases
+    key_space = 1_000_000_000
+    ranges = workload.rank_ranges(key_space, world)
+    if weak:
+        lo, hi = ranges[rank]
+        bases = workload.complement_windows(push_bases, lo, hi, B, seed=seed + 1000 * rank, n_max=J)
+        return [(j, int(b), B) for j, b in enumerate(bases)], bases
+    bases = workload.disjoint_windows(push_bases, J, key_space, B, seed=seed * 100)
+    routed = workload.route_windows(bases, B, ranges)
+    return [(w, int(bases[w]) + off, n) for w, off, n in routed[rank]], bases
+
+
 def window_vals(w, r, B, dev, rank=0, weak=False, dtype=None):
     """The value stream of producer w in window set r: U(-1, 1), seed
     42 + w + 100000 r (+ 1000 rank in the weak-scaled form, whose producers
@@ -198,76 +232,91 @@ def window_vals(w, r, B, dev, rank=0, weak=False, dtype=None):
     return torch.rand(B, generator=g, device=dev, dtype=dtype or torch.float32) * 2 - 1
 
 
-def make_set(rank, world, J, B, dev, r=0, weak=False, dtype=None, bases=None):
-    """Window set r of this rank in HBM: (slices, [(keys, vals)], distinct keys)."""
+def make_set(rank, world, J, B, dev, r=0, weak=False, dtype=None, bases=None, space=None, n_pull=None):
+    """Window set r of this rank in HBM: the push slices with their (keys, vals)
+    batches and distinct-key count, and the step's pull slices with their keys."""
     import torch
 
-    _, lo, hi, slices, bases = plan_rank(rank, world, J, B, r, weak, bases)
+    from parameter_server_amd import workload
+
+    _, lo, hi, slices, bases = plan_rank(rank, world, J, B, r, weak, bases, space)
     batches = []
     for w, first, n in slices:
         keys = torch.arange(first, first + n, dtype=torch.int64, device=dev).to(torch.int32)
         off = first - int(bases[w])
         vals = window_vals(w, r, B, dev, rank, weak, dtype)[off:off + n].clone()  # own, aligned buffer
         batches.append((keys, vals))
+    pull, pull_bases = plan_pull(rank, world, J, B, r, bases, weak, space, n_pull)
+    pull_keys = [torch.arange(first, first + n, dtype=torch.int64, device=dev).to(torch.int32)
+                 for _, first, n in pull]
+    u = workload.interval_union([(f, n) for _, f, n in slices])
+    return {"slices": slices, "batches": batches, "u": u, "r": r, "bases": bases,
+            "pull": pull, "pull_keys": pull_keys, "pull_bases": pull_bases}
+
+
+def overlap_keys(s):
+    """Keys a set's pull shares with its own push (0 by construction)."""
     from parameter_server_amd import workload
 
-    u = workload.interval_union([(f, n) for _, f, n in slices])
-    return {"slices": slices, "batches": batches, "u": u, "r": r}
+    push = workload.interval_union([(f, n) for _, f, n in s["slices"]])
+    pull = workload.interval_union([(f, n) for _, f, n in s["pull"]])
+    both = workload.interval_union([(f, n) for _, f, n in s["slices"] + s["pull"]])
+    return push + pull - both
 
 
 class Form:
     """One way of running the step over R window sets on a shard: step i pushes
-    set i % R and pulls set (i + shift) % R (shift 1: the headline; 0: the
-    cache-warm round-2 form)."""
+    set i % R, then pulls set i % R's pull windows (pull="disjoint": the
+    headline, no pulled key pushed in the step) or the windows it just pushed
+    (pull="same": the cache-warm round-2 form)."""
 
-    def __init__(self, shard, sets, shift, dev, vb=V, sorted_hint=True):
+    def __init__(self, shard, sets, dev, vb=V, sorted_hint=True, pull="disjoint"):
         import torch
 
-        self.shard, self.sets, self.shift, self.R, self.vb = shard, sets, shift, len(sets), vb
-        self.hint = sorted_hint
+        self.shard, self.sets, self.R, self.vb = shard, sets, len(sets), vb
+        self.hint, self.mode = sorted_hint, pull
         tdt = {4: torch.float32, 8: torch.float64}[vb]
-        self.outs = [[torch.empty(k.numel(), dtype=tdt, device=dev) for k, _ in s["batches"]] for s in sets]
+        self.pull_slices = [s["pull"] if pull == "disjoint" else s["slices"] for s in sets]
+        pull_keys = [s["pull_keys"] if pull == "disjoint" else [k for k, _ in s["batches"]] for s in sets]
+        self.outs = [[torch.empty(k.numel(), dtype=tdt, device=dev) for k in pk] for pk in pull_keys]
         self.adds = [shard.prepare(s["batches"]) for s in sets]
-        self.gets = [shard.prepare([(k, o) for (k, _), o in zip(s["batches"], outs)], is_get=True)
-                     for s, outs in zip(sets, self.outs)]
+        self.gets = [shard.prepare(list(zip(pk, outs)), is_get=True) for pk, outs in zip(pull_keys, self.outs)]
         self.add_b = [step_bytes(sum(n for _, _, n in s["slices"]), s["u"], 0, vb)[0] for s in sets]
-        self.get_b = [step_bytes(0, 0, sum(n for _, _, n in s["slices"]), vb)[1] for s in sets]
-
-    def pull_of(self, i):
-        return (i + self.shift) % self.R
+        self.get_b = [step_bytes(0, 0, sum(n for _, _, n in p), vb)[1] for p in self.pull_slices]
 
     def step(self, i):
         self.shard.add_grouped(self.adds[i % self.R], sorted_hint=self.hint)
-        self.shard.get_grouped(self.gets[self.pull_of(i)])
+        self.shard.get_grouped(self.gets[i % self.R])
 
     def bytes(self, steps):
         """(add bytes, get bytes) of steps 0..steps-1."""
         a = sum(self.add_b[i % self.R] for i in range(steps))
-        g = sum(self.get_b[self.pull_of(i)] for i in range(steps))
+        g = sum(self.get_b[i % self.R] for i in range(steps))
         return a, g
 
     def touched(self, i):
         """Distinct parameter bytes step i reads or writes (push set ∪ pull set)."""
         from parameter_server_amd import workload
 
-        iv = [(f, n) for s in (self.sets[i % self.R], self.sets[self.pull_of(i)]) for _, f, n in s["slices"]]
+        iv = [(f, n) for _, f, n in self.sets[i % self.R]["slices"] + self.pull_slices[i % self.R]]
         return workload.interval_union(iv) * self.vb
 
-    def self_check(self, lo, hi, dev):
-        """From a cleared shard, run one rotation and compare every pull with a
-        torch model of the shard (sequential last-write-wins slice assigns,
-        map_storage.hpp:22-23) — the benchmarked state is the reference's."""
+    def self_check(self, lo, hi, dev, rotations=1):
+        """From a cleared shard, run `rotations` rotations and compare every pull
+        with a torch model of the shard (sequential last-write-wins slice
+        assigns, map_storage.hpp:22-23; never-written keys read 0,
+        map_storage.hpp:33-37) — the benchmarked state is the reference's."""
         import torch
 
         self.shard.clear()
         ref = torch.zeros(hi - lo, dtype={4: torch.float32, 8: torch.float64}[self.vb], device=dev)
-        for i in range(self.R):
-            for (_, first, n), (_, v) in zip(self.sets[i % self.R]["slices"], self.sets[i % self.R]["batches"]):
+        for i in range(self.R * rotations):
+            t = i % self.R
+            for (_, first, n), (_, v) in zip(self.sets[t]["slices"], self.sets[t]["batches"]):
                 ref[first - lo:first - lo + n] = v
             self.step(i)
             torch.cuda.synchronize()
-            t = self.pull_of(i)
-            for (_, first, n), o in zip(self.sets[t]["slices"], self.outs[t]):
+            for (_, first, n), o in zip(self.pull_slices[t], self.outs[t]):
                 if not torch.equal(o, ref[first - lo:first - lo + n]):
                     raise AssertionError(f"bench self-check failed: step {i}, pull of set {t}, key {first}")
         del ref
@@ -794,11 +843,12 @@ def variant_f64(rank, world, J, B, dev, R, steps, lo, hi):
     sets = [make_set(rank, world, J, B, dev, r, dtype=torch.float64) for r in range(R)]
     with ps.Shard(lo, hi, np.float64, device=dev.index) as sh:
         sh.set_stream(torch.cuda.current_stream().cuda_stream)
-        f = Form(sh, sets, 1, dev, vb=8)
+        f = Form(sh, sets, dev, vb=8)
         f.self_check(lo, hi, dev)
         res = run_form(f, steps, 2, world, dev)
         sh.set_stream(None)
-    return {"workload": f"the headline step with float64 values ({J} x {B} windows, pull of the next set, assign)",
+    return {"workload": f"the headline step with float64 values ({J} x {B} windows pushed, the free window slots "
+                        "pulled, assign)",
             "GB/s": res["GB/s"], "ms_per_step": res["ms_per_step"]}
 
 
@@ -814,7 +864,7 @@ def variant_accumulate(rank, world, J, B, dev, sets, steps, lo, hi):
 
     with ps.Shard(lo, hi, np.float32, mode="accumulate", device=dev.index) as sh:
         sh.set_stream(torch.cuda.current_stream().cuda_stream)
-        f = Form(sh, sets, 1, dev)
+        f = Form(sh, sets, dev)
         # accumulate bytes: every pushed value is read
         f.add_b = [sum(n for _, _, n in s["slices"]) * (4 + V) + 2 * s["u"] * V for s in sets]
         ref = torch.zeros(hi - lo, dtype=torch.float32, device=dev)
@@ -823,15 +873,53 @@ def variant_accumulate(rank, world, J, B, dev, sets, steps, lo, hi):
                 ref[first - lo:first - lo + n] += v
             f.step(i)
             torch.cuda.synchronize()
-            t = f.pull_of(i)
-            for (_, first, n), o in zip(sets[t]["slices"], f.outs[t]):
+            for (_, first, n), o in zip(f.pull_slices[i], f.outs[i]):
                 assert torch.equal(o, ref[first - lo:first - lo + n]), "accumulate self-check failed"
         del ref
         res = run_form(f, steps, 2, world, dev)
         sh.set_stream(None)
-    return {"workload": f"the headline step in accumulate mode (gradient push += then pull of the next set), "
+    return {"workload": f"the headline step in accumulate mode (gradient push +=, then pull of the free window "
+                        f"slots), "
                         f"{J} x {B} windows (K6 + K7 + K1)",
             "GB/s": res["GB/s"], "ms_per_step": res["ms_per_step"]}
+
+
+def kernel_fracs(ktimes):
+    """Per-kernel fraction of the HBM peak (algorithmic bytes / avg duration)."""
+    return {n: dict(k, frac=k["GB/s"] / HBM_PEAK_GBS) for n, k in ktimes.items()}
+
+
+def cold_form(dev, J, B, R, steps, warmup, space, n_pulls):
+    """The headline step on a shard of `space` keys (default 1e9 = cfg 4's whole
+    key space: 4 GB of parameters against the 256 MB Infinity Cache): push set r
+    = J windows at uniform 1M-aligned bases (seed set_seed(r)), pull = n_pulls[r]
+    free window slots (as many as cfg 2's set r pulls).  With 1000 window slots
+    a window recurs only every ~8 steps, after ~4 GB of other traffic, so both
+    kernels are served by HBM — the rate a cold rank sees, and the roofline's
+    cold figure.  N = 1 only (one process; the 1e9-key shard alone)."""
+    import torch
+
+    import parameter_server_amd as ps
+
+    sets = [make_set(0, 1, J, B, dev, r, space=space, n_pull=n_pulls[r % len(n_pulls)]) for r in range(R)]
+    assert all(overlap_keys(s) == 0 for s in sets)
+    with ps.Shard(0, space, np.float32, device=dev.index) as sh:
+        sh.set_stream(torch.cuda.current_stream().cuda_stream)
+        f = Form(sh, sets, dev)
+        f.self_check(0, space, dev)
+        res = run_form(f, steps, max(warmup, R), 1, dev)
+        kt, ev_s = evented(f, steps, 1, dev)
+        sh.set_stream(None)
+    a, g = f.bytes(steps)
+    del f, sets
+    torch.cuda.empty_cache()
+    return {"workload": f"the headline step on a {space:.3g}-key float shard ({space * 4 / 1e9:.0f} GB of parameters): "
+                        f"{J} x {B} windows at 1M-aligned bases pushed, then free window slots pulled (as many as "
+                        "cfg 2 pulls), zero push/pull overlap, a window recurring only every ~8 steps: every "
+                        "parameter read and write is served by HBM",
+            "shard_keys": int(space), "GB/s": res["GB/s"], "ms_per_step": res["ms_per_step"],
+            "bytes_per_step": (a + g) / steps, "ms_per_step_evented": ev_s / steps * 1e3,
+            "kernels": kernel_fracs(kt)}
 
 
 def main(argv=None):
@@ -866,11 +954,19 @@ def main(argv=None):
     if os.environ.get("PSKV_BENCH_EMULATE") and world == 1:
         prank, pworld = (int(x) for x in os.environ["PSKV_BENCH_EMULATE"].split("/"))
     sets = [make_set(prank, pworld, J, B, dev, r) for r in range(R)]
+    assert all(overlap_keys(s) == 0 for s in sets), "a pull set overlaps its push set"
+    n_pulls = [len(s["pull"]) for s in sets]
+    if args.cold_only:
+        del sets
+        rec = cold_form(dev, J, B, R, args.steps, args.warmup, int(args.cold_keys), n_pulls)
+        json_out.write(json.dumps({"cold": rec}) + "\n")
+        json_out.flush()
+        return
     key_space, lo, hi = plan_rank(prank, pworld, J, B)[:3]
     stream = torch.cuda.current_stream()
     shard = ps.Shard(lo, hi, np.float32, device=local)
     shard.set_stream(stream.cuda_stream)  # torch events and the kernels share one stream
-    form = Form(shard, sets, 1, dev)
+    form = Form(shard, sets, dev)
     # correctness guard on the benchmarked state: one rotation from a cleared
     # shard, every pull against a model of the shard
     form.self_check(lo, hi, dev)
@@ -889,11 +985,16 @@ def main(argv=None):
     zipf_res = None
     if not args.no_zipf:
         zipf_res, zb = zipf_sparse(prank, world, dev, lo, hi, B, args.steps)
+    cold = None
+    if pworld == 1 and not args.no_cold:
+        shard.set_stream(None)  # the cold shard takes the stream meanwhile
+        cold = cold_form(dev, J, B, R, args.steps, args.warmup, int(args.cold_keys), n_pulls)
+        shard.set_stream(stream.cuda_stream)
 
     # dominant kernel: the one with the most time in the evented pass
     dom = max(ktimes.items(), key=lambda kv: kv[1]["avg_ms"] * kv[1]["launches"])
     achieved = dom[1]["GB/s"]
-    cfg_key = {"n_gpus": world, "batches": J, "batch_keys": B, "sets": R, "form": "pull-next-set"}
+    cfg_key = {"n_gpus": world, "batches": J, "batch_keys": B, "sets": R, "form": "pull-free-slots"}
     traffic, traffic_src = load_pmc(dom[0], cfg_key)
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": dom[0],
@@ -904,7 +1005,9 @@ def main(argv=None):
                       "kernels, over a second pass of the same K steps run right after the "
                       "event-free timed region",
             "ms_per_step_evented": evented_s / args.steps * 1e3,
-            "kernels": ktimes}
+            "kernels": kernel_fracs(ktimes)}
+    if cold is not None:
+        roof["cold"] = cold
     if traffic_src:
         roof["traffic_source"] = traffic_src
         roof["traffic_over_algorithmic"] = traffic / dom[1]["algorithmic_bytes"]
@@ -927,8 +1030,8 @@ def main(argv=None):
                          if pworld == 1 else
                          f"cfg 4 ranges: 1e9 keys over {pworld} range shards, {J} producer streams each pushing one "
                          f"{B}-key contiguous window at a uniformly random base, sliced by the range map ") +
-                        "pushed, then the windows of the next set pulled, per step; assign (last-write-wins) mode, "
-                        f"grouped launches, {R} window sets rotated over the steps",
+                        "pushed, then windows the push did not touch pulled (zero push/pull overlap), per step; "
+                        f"assign (last-write-wins) mode, grouped launches, {R} window sets rotated over the steps",
             "key_space": key_space,
             "shard_keys_per_gpu": hi - lo,
             "windows_per_step": J,
@@ -936,6 +1039,8 @@ def main(argv=None):
             "window_sets": R,
             "window_set_seeds": [workload.set_seed(r, pworld) for r in range(R)],
             "keys_pushed_per_step_per_gpu": n_push,
+            "keys_pulled_per_step_per_gpu": sum(n for s in sets for _, _, n in s["pull"]) / R,
+            "push_pull_overlap_keys": max(overlap_keys(s) for s in sets),
             "distinct_pushed_keys_per_step_per_gpu": sum(s["u"] for s in sets) / R,
             "bytes_per_step_per_gpu": own_bytes / args.steps,
             "param_bytes_touched_per_step_per_gpu": touched,
@@ -952,7 +1057,7 @@ def main(argv=None):
         result["zipf_sparse"] = zipf_res
     extra = {}
     if not args.no_extra:
-        warm = Form(shard, sets, 0, dev)
+        warm = Form(shard, sets, dev, pull="same")
         w = run_form(warm, args.steps, 2, world, dev)
         extra["cache_warm_step"] = {
             "workload": "the round-2 headline form: the Get pulls the windows the step just pushed (their "
@@ -961,12 +1066,12 @@ def main(argv=None):
         del warm
         if pworld > 1:
             wsets = [make_set(prank, pworld, J, B, dev, r, weak=True) for r in range(R)]
-            wf = Form(shard, wsets, 1, dev)
+            wf = Form(shard, wsets, dev)
             wf.self_check(lo, hi, dev)
             wr = run_form(wf, args.steps, 2, world, dev)
             extra["weak_scaled"] = {
                 "workload": f"weak scaling: every rank's own {J} producers push 1M-aligned windows inside its "
-                            "range (per-GPU work fixed), pull of the next set", "GB/s": wr["GB/s"],
+                            "range (per-GPU work fixed), pull of free window slots of the range", "GB/s": wr["GB/s"],
                 "ms_per_step": wr["ms_per_step"],
                 "per_gpu_min_GB/s": -max_over_ranks(-wr["own_GB/s"], world, dev)}
             del wf, wsets

@@ -43,7 +43,7 @@ def _stale(out, deps):
 
 def build_lib(force=False):
     srcs = [os.path.join(CSRC, s) for s in LIB_SOURCES]
-    deps = srcs + [os.path.join(CSRC, h) for h in ("pskv_internal.h", "pskv_frames.h")] + [os.path.join(INCLUDE, "pskv.h")]
+    deps = srcs + [os.path.join(CSRC, h) for h in ("pskv_internal.h", "pskv_frames.h", "pskv_queues.h")] + [os.path.join(INCLUDE, "pskv.h")]
     if force or _stale(LIB_OUT, deps):
         _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
               "-I", INCLUDE, "-I", CSRC, *srcs, "-o", LIB_OUT])

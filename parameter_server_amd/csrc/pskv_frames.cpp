@@ -90,7 +90,13 @@ class Arena {
         (void)hipHostFree(p);
         return set(err, PSKV_EHIP, "pskv_host_alloc: hipHostGetDevicePointer failed");
       }
-      f = new Frame{static_cast<char*>(p), static_cast<char*>(dev), cap, cls, {}};
+      // The frame is portable (every device may map it), but a kernel reads it
+      // in place only through ONE address for all devices: ROCm's unified
+      // address space maps page-locked memory at its host address on every
+      // device.  Should a device view ever differ from the host address, the
+      // frame keeps no view and calls on it take the DMA path (device_view
+      // returns null), which is correct for any device.
+      f = new Frame{static_cast<char*>(p), dev == p ? static_cast<char*>(dev) : nullptr, cap, cls, {}};
     }
     {
       std::lock_guard<std::mutex> g(mu_);
@@ -127,7 +133,7 @@ class Arena {
   void* device_view(const void* p, size_t bytes) {
     std::lock_guard<std::mutex> g(mu_);
     Frame* f = find(p);
-    if (!f) return nullptr;
+    if (!f || !f->dev) return nullptr;
     const size_t off = static_cast<size_t>(static_cast<const char*>(p) - f->base);
     if (bytes > f->cap - off) return nullptr;
     return f->dev + off;

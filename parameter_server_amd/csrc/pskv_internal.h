@@ -112,9 +112,8 @@ struct Ovf {
 // pointers 16-byte aligned so 16 B vector accesses are legal.
 // unroll: 4 or 8 groups of 4 keys per lane (chunk = 256*4*unroll keys);
 // nt: non-temporal loads/stores of the streamed push/pull buffers.
-// dedup: 4-byte values, scattered pull keys gathered once per distinct key per
-// workgroup chunk (an LDS table; dense chunks skip it)
-hipError_t launch_gather(int vb, bool vec, int unroll, bool nt, bool dedup, bool ntp, const GroupArgs& ga,
+// ntp: non-temporal parameter loads (option GET_NTP; 4-byte values, unroll 8, nt)
+hipError_t launch_gather(int vb, bool vec, int unroll, bool nt, bool ntp, const GroupArgs& ga,
                          uint32_t nwg, const DenseView& d, const Ovf& o, hipStream_t st);
 hipError_t launch_assign_sorted(int vb, bool vec, const uint32_t* keys, const void* vals,
                                 uint64_t n, const DenseView& d, uint32_t* flag, uint32_t epoch,
@@ -160,7 +159,7 @@ struct RbMap {
 // workgroups per CU, ~7 Ki entries per bucket in one pass; 14: 128 KiB, ~14 Ki).
 hipError_t launch_rb_add(int dtype, int mode, const GroupArgs& ga, uint32_t nsc,
                          const DenseView& d, const Ovf& o, const RbMap& bm,
-                         int apply_log2, int bin_block, bool lane_insert, uint16_t* loff, void* tmp,
+                         int apply_log2, int bin_block, uint16_t* loff, void* tmp,
                          hipStream_t st);
 uint32_t rb_superchunk(int vb, int bin_block);
 constexpr size_t kRbTmpPad = 16;  // bytes past the last entry K5b may read (paired loads)

@@ -261,26 +261,9 @@ __device__ __forceinline__ void gather2(const DenseView& d, const Ovf& o, const 
   }
 }
 
-// Pull-key dedup (K1, 4-byte values, DEDUP): a chunk of scattered keys — a
-// Zipf pull repeats its hot keys many times (cfg 3: ~30 % of an 8 Ki-key
-// chunk's keys are repeats) — gathers each distinct key once.  Every scattered
-// key claims a slot of a direct-mapped LDS table, (key, element id) written as
-// one 8-byte store (the last writer of a slot owns it); the owners gather and
-// publish their values in LDS; the other elements with the owner's key read
-// the value from LDS; keys whose slot another key took gather themselves.
-// No atomics, no clearing (a slot is read only by the elements that wrote it),
-// two workgroup barriers.  Chunks whose groups are all runs (dense pulls)
-// skip it after one barrier.  18 KiB of LDS keeps 8 workgroups per CU.
-constexpr uint32_t kDedupSlots = 1536;
-__device__ __forceinline__ uint32_t dedup_slot(uint32_t key) {
-  return __umulhi(fmix32(key), kDedupSlots);
-}
-
-template <typename VT, bool VEC, int U, bool NT, bool DEDUP, bool NTP = false>
+template <typename VT, bool VEC, int U, bool NT, bool NTP = false>
 __global__ __launch_bounds__(kBlock) void k_gather(GroupArgs ga, DenseView d, Ovf o) {
   constexpr int CH = kBlock * 4 * U;
-  __shared__ unsigned long long s_ent[DEDUP ? kDedupSlots : 1];  // key | element id << 32
-  __shared__ VT s_val[DEDUP ? kDedupSlots : 1];
   const uint32_t wg = blockIdx.x;
   const int j = batch_of(ga, wg);
   const uint32_t* __restrict__ keys = ga.b[j].keys;
@@ -312,65 +295,8 @@ __global__ __launch_bounds__(kBlock) void k_gather(GroupArgs ga, DenseView d, Ov
     for (int u = 0; u < U; ++u)
       Vec4<uint32_t>::load<NT>(keys + base + (uint64_t)(u * kBlock + tid) * 4, k[u]);
     VT v[U][4];
-    bool dedup = false;
-    if constexpr (DEDUP && sizeof(VT) == 4) {
-      static_assert(U * 4 <= 32, "one mask bit per element of a lane");
-      uint32_t runs = 0;  // bit u: group u is four consecutive in-range keys
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t off0 = k[u][0] - d.key_begin;
-        const bool run = (k[u][1] == k[u][0] + 1u) & (k[u][2] == k[u][0] + 2u) &
-                         (k[u][3] == k[u][0] + 3u) & ((uint64_t)off0 + 3u < d.range);
-        runs |= run ? (1u << u) : 0u;
-      }
-      dedup = __syncthreads_or(runs != (1u << U) - 1u) != 0;
-      if (dedup) {
-        // claim: every scattered element writes (key, its id) into its slot
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if (runs >> u & 1u) continue;
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            s_ent[dedup_slot(k[u][e])] =
-                (unsigned long long)k[u][e] | ((unsigned long long)(tid * 32 + u * 4 + e) << 32);
-        }
-        __syncthreads();
-        // owners and slot losers gather; the other holders of an owned key wait
-        uint32_t waits = 0, owns = 0;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if (runs >> u & 1u) {
-            gather4<VT, NTP>(d, o, k[u], v[u]);
-            continue;
-          }
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const unsigned long long ent = s_ent[dedup_slot(k[u][e])];
-            const bool same = (uint32_t)ent == k[u][e];
-            const bool own = same && (uint32_t)(ent >> 32) == (uint32_t)(tid * 32 + u * 4 + e);
-            const uint32_t bit = 1u << (u * 4 + e);
-            waits |= same && !own ? bit : 0u;
-            owns |= own ? bit : 0u;
-            v[u][e] = same && !own ? VT(0) : load_one<VT>(d, o, k[u][e]);
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (owns >> (u * 4 + e) & 1u) s_val[dedup_slot(k[u][e])] = v[u][e];
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (waits >> (u * 4 + e) & 1u) v[u][e] = s_val[dedup_slot(k[u][e])];
-      }
-    }
-    if (!dedup) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) gather4<VT, NTP>(d, o, k[u], v[u]);
-    }
+    for (int u = 0; u < U; ++u) gather4<VT, NTP>(d, o, k[u], v[u]);
 #pragma unroll
     for (int u = 0; u < U; ++u)
       Vec4<VT>::template store<NT>(out + base + (uint64_t)(u * kBlock + tid) * 4, v[u]);
@@ -1217,13 +1143,7 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t* a, uint32_t n, uint32
 // first probe of every key is issued back to back (independent LDS atomics in
 // flight); only keys that met another key probe further.  slot[q] = EMPTY for
 // invalid keys; own bit q = this lane inserted the key.
-// LANE (K5a, option RB_INSERT): the keys that met another key probe on one
-// per lane per round, the lane's lowest pending key each time (selected from
-// the registers by compares, no dynamic indexing), so a round is ONE
-// compare-and-swap instruction for the whole wave and the wave pays the
-// longest per-lane sum of extra probes — not, as in the per-key loops, a
-// round of instructions per key position that any lane still probes.
-template <int PER, int SLOTS, bool LANE = false>
+template <int PER, int SLOTS>
 __device__ __forceinline__ uint32_t lds_insert(uint32_t* hk, uint32_t* sent,
                                                const uint32_t (&key)[PER], uint32_t valid_mask,
                                                uint32_t (&slot)[PER]) {
@@ -1244,39 +1164,6 @@ __device__ __forceinline__ uint32_t lds_insert(uint32_t* hk, uint32_t* sent,
       slot[q] = fmix32(key[q]) & (SLOTS - 1);
       old[q] = atomicCAS(&hk[slot[q]], kEmpty32, key[q]);
     }
-  }
-  if constexpr (LANE) {
-    uint32_t pend = 0;  // keys that met another key: probe on
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-      if (!(valid_mask >> q & 1u) || key[q] == kEmpty32) continue;
-      if (old[q] == kEmpty32)
-        own |= 1u << q;
-      else if (old[q] != key[q])
-        pend |= 1u << q;
-    }
-    while (pend) {
-      const uint32_t q = (uint32_t)__builtin_ctz(pend);
-      uint32_t kq = key[0], hq = slot[0];
-#pragma unroll
-      for (int e = 1; e < PER; ++e)
-        if (q == (uint32_t)e) {
-          kq = key[e];
-          hq = slot[e];
-        }
-      hq = (hq + 1) & (SLOTS - 1);
-      const uint32_t o = atomicCAS(&hk[hq], kEmpty32, kq);
-#pragma unroll
-      for (int e = 0; e < PER; ++e)
-        if (q == (uint32_t)e) slot[e] = hq;
-      if (o == kEmpty32) {
-        own |= 1u << q;
-        pend &= ~(1u << q);
-      } else if (o == kq) {
-        pend &= ~(1u << q);
-      }
-    }
-    return own;
   }
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
@@ -1332,7 +1219,7 @@ constexpr uint32_t rb_sc(int binb) {
   return (sizeof(BT) == 8 ? 4u : 8u) * (uint32_t)binb;
 }
 
-template <typename AT, typename BT, int MODE, int BINB, bool LANEINS = false>
+template <typename AT, typename BT, int MODE, int BINB>
 __global__ __launch_bounds__(BINB) void k_rb_bin(GroupArgs ga, DenseView d, RbMap bm,
                                                  uint32_t nbk,
                                                  uint16_t* __restrict__ loff, uint32_t nsc,
@@ -1436,7 +1323,7 @@ __global__ __launch_bounds__(BINB) void k_rb_bin(GroupArgs ga, DenseView d, RbMa
 #pragma unroll
     for (int q = 0; q < KPT; ++q) valid |= li_of(q) < cur.nvalid ? (1u << q) : 0u;
     uint32_t slot[KPT];
-    const uint32_t own = lds_insert<KPT, SLOTS, LANEINS>(hk, &sent, kc, valid, slot);
+    const uint32_t own = lds_insert<KPT, SLOTS>(hk, &sent, kc, valid, slot);
 #pragma unroll
     for (int q = 0; q < KPT; ++q) {
       if (!(valid >> q & 1u)) continue;
@@ -2477,30 +2364,28 @@ __global__ __launch_bounds__(kInlineMax) void k_serve(SrvRing* ring, DenseView d
 
 // ------------------------------------------------------- launch wrappers
 
-template <typename VT, bool VEC, bool DEDUP = false>
+template <typename VT, bool VEC>
 static void gather_dispatch(int unroll, bool nt, uint32_t nwg, const GroupArgs& ga,
                             const DenseView& d, const Ovf& o, hipStream_t st) {
   if (unroll == 8) {
     if (nt)
-      k_gather<VT, VEC, 8, true, DEDUP><<<nwg, kBlock, 0, st>>>(ga, d, o);
+      k_gather<VT, VEC, 8, true><<<nwg, kBlock, 0, st>>>(ga, d, o);
     else
-      k_gather<VT, VEC, 8, false, DEDUP><<<nwg, kBlock, 0, st>>>(ga, d, o);
+      k_gather<VT, VEC, 8, false><<<nwg, kBlock, 0, st>>>(ga, d, o);
   } else {
     if (nt)
-      k_gather<VT, VEC, 4, true, DEDUP><<<nwg, kBlock, 0, st>>>(ga, d, o);
+      k_gather<VT, VEC, 4, true><<<nwg, kBlock, 0, st>>>(ga, d, o);
     else
-      k_gather<VT, VEC, 4, false, DEDUP><<<nwg, kBlock, 0, st>>>(ga, d, o);
+      k_gather<VT, VEC, 4, false><<<nwg, kBlock, 0, st>>>(ga, d, o);
   }
 }
 
-hipError_t launch_gather(int vb, bool vec, int unroll, bool nt, bool dedup, bool ntp, const GroupArgs& ga,
+hipError_t launch_gather(int vb, bool vec, int unroll, bool nt, bool ntp, const GroupArgs& ga,
                          uint32_t nwg, const DenseView& d, const Ovf& o, hipStream_t st) {
   if (nwg == 0) return hipSuccess;
   if (vb == 4) {
-    if (vec && ntp && !dedup && unroll == 8 && nt)  // option GET_NTP: non-temporal parameter loads
-      k_gather<uint32_t, true, 8, true, false, true><<<nwg, kBlock, 0, st>>>(ga, d, o);
-    else if (vec && dedup)
-      gather_dispatch<uint32_t, true, true>(unroll, nt, nwg, ga, d, o, st);
+    if (vec && ntp && unroll == 8 && nt)  // option GET_NTP: non-temporal parameter loads
+      k_gather<uint32_t, true, 8, true, true><<<nwg, kBlock, 0, st>>>(ga, d, o);
     else if (vec)
       gather_dispatch<uint32_t, true>(unroll, nt, nwg, ga, d, o, st);
     else
@@ -2660,7 +2545,7 @@ hipError_t launch_ovf_rehash(int vb, const Ovf& from, uint64_t from_cap, const O
 
 template <typename AT, typename BT, int MODE>
 static hipError_t rb_launch(const GroupArgs& ga, uint32_t nsc, const DenseView& d, const Ovf& o,
-                            const RbMap& bm, int apply_log2, int bin_block, bool lane_insert, uint16_t* loff,
+                            const RbMap& bm, int apply_log2, int bin_block, uint16_t* loff,
                             void* tmp, hipStream_t st) {
   const uint32_t nbk = bm.nbd + 1;
   auto* t = reinterpret_cast<RbEnt<sizeof(BT)>*>(tmp);
@@ -2670,8 +2555,6 @@ static hipError_t rb_launch(const GroupArgs& ga, uint32_t nsc, const DenseView& 
   const uint32_t gb = nsc < wgs ? nsc : wgs;
   if (bin_block == 512)
     k_rb_bin<AT, BT, MODE, 512><<<gb, 512, 0, st>>>(ga, d, bm, nbk, loff, nsc, t);
-  else if (lane_insert)
-    k_rb_bin<AT, BT, MODE, 1024, true><<<gb, 1024, 0, st>>>(ga, d, bm, nbk, loff, nsc, t);
   else
     k_rb_bin<AT, BT, MODE, 1024><<<gb, 1024, 0, st>>>(ga, d, bm, nbk, loff, nsc, t);
   const uint32_t sc = rb_sc<BT>(bin_block);
@@ -2684,13 +2567,13 @@ static hipError_t rb_launch(const GroupArgs& ga, uint32_t nsc, const DenseView& 
 
 hipError_t launch_rb_add(int dtype, int mode, const GroupArgs& ga, uint32_t nsc,
                          const DenseView& d, const Ovf& o, const RbMap& bm,
-                         int apply_log2, int bin_block, bool lane_insert, uint16_t* loff, void* tmp,
+                         int apply_log2, int bin_block, uint16_t* loff, void* tmp,
                          hipStream_t st) {
   if (nsc == 0) return hipSuccess;
   if (bm.nbd + 1 > (uint32_t)kRbMaxBuckets || nsc > kRbMaxSc || bm.nbd == 0 ||
       (bin_block != 512 && bin_block != 1024))
     return hipErrorInvalidValue;
-#define PSKV_RB(AT, BT, M) rb_launch<AT, BT, M>(ga, nsc, d, o, bm, apply_log2, bin_block, lane_insert, loff, tmp, st)
+#define PSKV_RB(AT, BT, M) rb_launch<AT, BT, M>(ga, nsc, d, o, bm, apply_log2, bin_block, loff, tmp, st)
   if (mode == 0) {
     if (dtype == 0) return PSKV_RB(int, uint32_t, 0);
     if (dtype == 1) return PSKV_RB(float, uint32_t, 0);

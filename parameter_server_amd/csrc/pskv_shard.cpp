@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <cctype>
+#include <cerrno>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -37,6 +38,7 @@
 #include "pskv.h"
 #include "pskv_frames.h"
 #include "pskv_internal.h"
+#include "pskv_queues.h"
 
 using namespace pskv;
 
@@ -259,7 +261,6 @@ struct pskv_shard {
   bool tune_ntp = false; // PSKV_NTP: non-temporal parameter stores (dense Add)
   bool tune_get_ntp = false;  // PSKV_GET_NTP: non-temporal parameter loads in K1 (4-byte values, 16-byte aligned runs)
   int tune_early = 2;    // PSKV_EARLY: K2g early loads (0 never, 1 always, 2 when the group's keys cover < 1/4 of the range)
-  bool tune_get_dedup = false;  // GET_DEDUP: K1 gathers each distinct scattered pull key once per chunk
   // PSKV_PAGEABLE_DMA: DMA pageable host buffers directly (the runtime moves
   // them at the PCIe rate, measured 55 GB/s) instead of copying them into
   // pinned staging first; 0 selects the staging path.  cfg-2-shaped Add of
@@ -304,7 +305,6 @@ struct pskv_shard {
   unsigned int ireply_seq = 0;
   int tune_rb_apply_log2 = 0; // PSKV_RB_APPLY_LOG2: 13 or 14 (0 = by bucket size)
   int tune_rb_bin_block = kRbBinBlockDefault;  // PSKV_RB_BIN_BLOCK: K5a workgroup, 512 or 1024
-  bool tune_rb_insert = false;  // PSKV_RB_INSERT: K5a probes one pending key per lane per round (1; measured 3 % slower) or per key (0)
   // K9 request server (PSKV_SERVE=1): the inline-size messages go to a ring in
   // coherent page-locked memory that one resident workgroup polls
   // (PSKV_SERVE_IDLE_US: it leaves after this long without a request)
@@ -317,7 +317,7 @@ struct pskv_shard {
   bool srv_running = false;
   uint32_t srv_posted = 0;
   unsigned long long srv_idle_ticks = 0;
-  bool counted = false;  // in g_device_shards
+  bool counted = false;  // in g_queues (pskv_queues.h)
   bool add_chunks_set = false;  // INLINE_ADD_CHUNKS chosen explicitly
   int wall_khz = 0;             // device wall-clock rate (the server's idle timer)
 
@@ -326,9 +326,7 @@ struct pskv_shard {
 
 namespace {
 
-// K1's keys per lane group: the pull-key dedup variant runs 4 groups per lane
-// (its LDS barriers hold every group's keys and values: 8 groups took 126 VGPRs)
-int gather_unroll(const pskv_shard* s) { return s->tune_get_dedup && s->vb == 4 ? 4 : s->tune_unroll; }
+int gather_unroll(const pskv_shard* s) { return s->tune_unroll; }
 
 int use_device(pskv_shard* s) {
   PSKV_HIP(hipSetDevice(s->device));
@@ -396,30 +394,20 @@ int drain_timing(pskv_shard* s) {
 // (srv_launch: stream wait on an event), so stream order is kept both ways.
 // A kernel that left on its idle timer is restarted from done_seq (srv_wait).
 
-// A resident server holds the hardware queue its stream maps to: work of any
-// other stream on that queue waits behind it until it idles out.  The process
-// has GPU_MAX_HW_QUEUES queues per device (HIP's default 4); HIP deals streams
-// to them round-robin.  Every shard on the device holds a stream and a served
-// one a second (the server's), and the null stream takes one more, so the
-// server engages only while 2 * shards + 1 streams fit the queues (one shard
-// at the default 4) — it then holds a queue of its own, provided the process
-// creates no further streams on the device (torch's default stream is the null
-// stream).  Beyond that the K8 launches serve.  A launch that is nevertheless
-// queued behind other work does not hang its caller: srv_wait bounds the wait
-// for it to start (kSrvStartTimeoutMs) and fails the call.
-std::atomic<int> g_device_shards[64];
-std::atomic<int> g_device_extra_streams[64];  // pinned-Get output streams
+// A resident server holds the hardware queue its stream maps to (the
+// accounting per device, pskv_queues.h): the server engages on a device only
+// while 2 * shards + 1 + extra streams fit its GPU_MAX_HW_QUEUES queues (one
+// shard at the default 4) — it then holds a queue of its own, provided the
+// process creates no further streams on the device (torch's default stream is
+// the null stream).  Beyond that the K8 launches serve.  A launch that is
+// nevertheless queued behind other work does not hang its caller: srv_wait
+// bounds the wait for it to start (kSrvStartTimeoutMs) and fails the call.
+DeviceQueues g_queues;
 
 bool serve_on(const pskv_shard* s) {
-  if (!s->tune_serve || s->device < 0 || s->device >= 64) return false;
-  static const int queues = [] {
-    const char* e = std::getenv("GPU_MAX_HW_QUEUES");
-    const int q = e ? std::atoi(e) : 4;
-    return q > 0 ? q : 4;
-  }();
-  return 2 * g_device_shards[s->device].load(std::memory_order_relaxed) + 1 +
-             g_device_extra_streams[s->device].load(std::memory_order_relaxed) <=
-         queues;
+  if (!s->tune_serve) return false;
+  static const int queues = hw_queues_from_env(std::getenv("GPU_MAX_HW_QUEUES"));
+  return g_queues.serve_fits(s->device, queues);
 }
 
 constexpr int kSrvStartTimeoutMs = 2000;
@@ -468,7 +456,12 @@ int srv_reap(pskv_shard* s) {
 // Wait until request `seq` has been applied.
 int srv_wait(pskv_shard* s, uint32_t seq) {
   SrvRing* r = s->srv;
-  auto t_start = std::chrono::steady_clock::now();  // since the current launch was seen queued
+  // The start clock runs only once the server's own dependency (everything
+  // queued on the shard's stream before its launch, srv_dep) has completed: a
+  // launch still waiting for that work -- e.g. a long replay of a broken sorted
+  // hint -- is not stuck, however long the work takes.
+  auto t_start = std::chrono::steady_clock::now();
+  bool dep_done = false;
   for (uint32_t it = 1;; ++it) {
     if ((int32_t)(__atomic_load_n(&r->done_seq, __ATOMIC_ACQUIRE) - seq) >= 0) return PSKV_OK;
     if ((it & 255u) == 0 && __atomic_load_n(&r->alive, __ATOMIC_ACQUIRE) == 0u) {
@@ -476,13 +469,22 @@ int srv_wait(pskv_shard* s, uint32_t seq) {
       if (int rc = srv_reap(s)) return rc;
       if ((int32_t)(__atomic_load_n(&r->done_seq, __ATOMIC_ACQUIRE) - seq) >= 0) return PSKV_OK;
       if (int rc = srv_launch(s)) return rc;
+      dep_done = false;
       t_start = std::chrono::steady_clock::now();
     }
     if ((it & 65535u) == 0) {  // a faulted kernel never publishes: surface the error
       const hipError_t e = hipStreamQuery(s->srv_stream);
       if (e != hipSuccess && e != hipErrorNotReady) PSKV_HIP(e);
-      // a launch that has not started is queued behind other work on its
-      // hardware queue: fail the call rather than wait without bound
+      if (!dep_done) {
+        const hipError_t d = hipEventQuery(s->srv_dep);
+        if (d != hipSuccess && d != hipErrorNotReady) PSKV_HIP(d);
+        dep_done = d == hipSuccess;
+        t_start = std::chrono::steady_clock::now();  // re-armed while the dependency runs
+        continue;
+      }
+      // the dependency is done and the launch has still not started: it is
+      // queued behind other work on its hardware queue -- fail the call rather
+      // than wait without bound
       if (__atomic_load_n(&r->started, __ATOMIC_ACQUIRE) != s->srv_gen &&
           std::chrono::steady_clock::now() - t_start > std::chrono::milliseconds(kSrvStartTimeoutMs))
         return fail(PSKV_ESTATE,
@@ -753,7 +755,7 @@ int radix_launch(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size
   if (rc) return rc;
   LaunchTimer t(s, PSKV_K_RADIX, elems);
   PSKV_HIP(launch_rb_add(s->dtype, s->mode, ga, nsc, s->dview(), s->ovf, bm, apply_log2,
-                         s->tune_rb_bin_block, s->tune_rb_insert, s->rb_loff, s->rb_ent, s->stream));
+                         s->tune_rb_bin_block, s->rb_loff, s->rb_ent, s->stream));
   t.done();
   s->n_general += 2;
   return PSKV_OK;
@@ -1044,6 +1046,10 @@ void* pinned_range_view(const void* p, size_t bytes) {
   }
   const uintptr_t b = reinterpret_cast<uintptr_t>(base), d = reinterpret_cast<uintptr_t>(dev);
   if (d < b || d + bytes > b + size) return nullptr;
+  // in place only through the unified address (valid on every device; see
+  // pskv_frames.cpp): a device-specific view would tie the buffer to the
+  // device that was current when the attributes were read
+  if (dev != p) return nullptr;
   return dev;
 }
 
@@ -1489,7 +1495,7 @@ int zero_copy_get_views(pskv_shard* s, const std::vector<pskv_batch>& hv) {
     uint64_t elems = 0;
     for (size_t i = g.first; i < g.second; ++i) elems += hv[i].n;
     LaunchTimer t(s, PSKV_K_GATHER, elems);
-    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, s->tune_get_dedup, s->tune_get_ntp, ga, nwg, s->dview(), s->ovf, s->stream));
+    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, s->tune_get_ntp, ga, nwg, s->dview(), s->ovf, s->stream));
     t.done();
   }
   PSKV_HIP(hipStreamSynchronize(s->stream));
@@ -1520,7 +1526,7 @@ int zero_copy_get(pskv_shard* s, const std::vector<pskv_batch>& v, bool vec) {
     uint64_t elems = 0;
     for (size_t i = g.first; i < g.second; ++i) elems += hv[i].n;
     LaunchTimer t(s, PSKV_K_GATHER, elems);
-    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, s->tune_get_dedup, s->tune_get_ntp, ga, nwg, s->dview(), s->ovf, s->stream));
+    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, s->tune_get_ntp, ga, nwg, s->dview(), s->ovf, s->stream));
     t.done();
   }
   PSKV_HIP(hipStreamSynchronize(s->stream));
@@ -1542,7 +1548,7 @@ int pinned_get(pskv_shard* s, const std::vector<pskv_batch>& v) {
   if (rc) return rc;
   if (!s->out_stream) {
     PSKV_HIP(hipStreamCreateWithFlags(&s->out_stream, hipStreamNonBlocking));
-    g_device_extra_streams[s->device].fetch_add(1, std::memory_order_relaxed);
+    g_queues.add_stream(s->device, 1);
   }
   std::vector<pskv_batch> dv = v;
   char* d = static_cast<char*>(s->dstage);
@@ -1585,7 +1591,7 @@ int pinned_get(pskv_shard* s, const std::vector<pskv_batch>& v) {
     uint64_t elems = 0;
     for (size_t i = b; i < e; ++i) elems += dv[i].n;
     LaunchTimer t(s, PSKV_K_GATHER, elems);
-    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, s->tune_get_dedup, s->tune_get_ntp, ga, nwg, s->dview(),
+    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, s->tune_get_ntp, ga, nwg, s->dview(),
                            s->ovf, s->stream));
     t.done();
     PSKV_HIP(hipEventRecord(s->out_events[w], s->stream));
@@ -1679,7 +1685,7 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
     uint64_t elems = 0;
     for (size_t i = g.first; i < g.second; ++i) elems += dv[i].n;
     LaunchTimer t(s, PSKV_K_GATHER, elems);
-    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, s->tune_get_dedup, s->tune_get_ntp, ga, nwg, s->dview(), s->ovf,
+    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, s->tune_get_ntp, ga, nwg, s->dview(), s->ovf,
                            s->stream));
     t.done();
   }
@@ -1756,7 +1762,6 @@ const Option kOptions[] = {
     PSKV_OPT("NT", 0, 1, tune_nt, bool),
     PSKV_OPT("NTP", 0, 1, tune_ntp, bool),
     PSKV_OPT("EARLY", 0, 2, tune_early, int),
-    PSKV_OPT("GET_DEDUP", 0, 1, tune_get_dedup, bool),
     PSKV_OPT("GET_NTP", 0, 1, tune_get_ntp, bool),
     PSKV_OPT("PAGEABLE_DMA", 0, 1, tune_pageable_dma, bool),
     PSKV_OPT("DMA_MIN_BYTES", 0, INT64_MAX, tune_dma_min_bytes, size_t),
@@ -1777,7 +1782,6 @@ const Option kOptions[] = {
     PSKV_OPT("RB_TB", 0, 11, tune_rb_tb, uint32_t),
     PSKV_OPT("RB_APPLY_LOG2", 0, 14, tune_rb_apply_log2, int),  // 0 = by size, 13 or 14
     PSKV_OPT("RB_BIN_BLOCK", 512, 1024, tune_rb_bin_block, int),  // 512 or 1024
-    PSKV_OPT("RB_INSERT", 0, 1, tune_rb_insert, bool),
 };
 #undef PSKV_OPT
 
@@ -1807,17 +1811,45 @@ int set_option(pskv_shard* s, const Option& o, int64_t v) {
   return PSKV_OK;
 }
 
+// The environment only sets creation defaults: a value that does not parse or
+// that pskv_set_option would reject is reported on stderr (once per variable
+// and process) and ignored -- the option keeps its built-in default, and the
+// shard is created as without the variable.  pskv_set_option itself stays
+// strict (PSKV_EINVAL).
 int apply_env_options(pskv_shard* s) {
+  static std::mutex warn_mu;
+  static std::vector<std::string> warned;
   for (const auto& o : kOptions) {
     const std::string var = std::string("PSKV_") + o.name;
     const char* e = std::getenv(var.c_str());
     if (!e || !*e) continue;
-    int64_t v;
-    if (std::strcmp(o.name, "GENERAL") == 0 && (std::isalpha((unsigned char)e[0]) != 0))
-      v = std::strcmp(e, "stamps") == 0 ? 0 : std::strcmp(e, "radix") == 0 ? 2 : 1;
-    else
-      v = std::atoll(e);
-    if (int rc = set_option(s, o, v)) return fail(rc, "environment " + var + ": " + g_last_error);
+    int64_t v = 0;
+    bool ok = true;
+    if (std::strcmp(o.name, "GENERAL") == 0 && std::isalpha((unsigned char)e[0]) != 0) {
+      if (std::strcmp(e, "stamps") == 0)
+        v = 0;
+      else if (std::strcmp(e, "auto") == 0)
+        v = 1;
+      else if (std::strcmp(e, "radix") == 0)
+        v = 2;
+      else
+        ok = false;
+    } else {
+      char* end = nullptr;
+      errno = 0;
+      v = std::strtoll(e, &end, 10);
+      ok = end != e && *end == '\0' && errno == 0;
+    }
+    const std::string saved = g_last_error;
+    if (ok && set_option(s, o, v) == PSKV_OK) continue;
+    const std::string why = ok ? g_last_error : std::string("not a valid value");
+    g_last_error = saved;
+    std::lock_guard<std::mutex> g(warn_mu);
+    if (std::find(warned.begin(), warned.end(), var) == warned.end()) {
+      warned.push_back(var);
+      std::fprintf(stderr, "pskv: ignoring environment %s=%s (%s); the option keeps its default\n", var.c_str(), e,
+                   why.c_str());
+    }
   }
   return PSKV_OK;
 }
@@ -1889,8 +1921,7 @@ int pskv_shard_create_ex(int device, uint32_t key_begin, uint64_t key_end, int d
   if (rc) return bail(rc);
   if (hipStreamSynchronize(s->stream) != hipSuccess)
     return bail(fail(PSKV_EHIP, "hipStreamSynchronize failed"));
-  if (device < 64) g_device_shards[device].fetch_add(1, std::memory_order_relaxed);
-  s->counted = true;
+  s->counted = g_queues.add_shard(device, 1);
   *out = s;
   return PSKV_OK;
 }
@@ -1911,13 +1942,13 @@ int pskv_shard_destroy(pskv_shard* s) {
     }
     (void)hipHostFree(s->srv);
   }
-  if (s->counted) g_device_shards[s->device].fetch_sub(1, std::memory_order_relaxed);
+  if (s->counted) g_queues.add_shard(s->device, -1);
   if (s->srv_stream) (void)hipStreamDestroy(s->srv_stream);
   if (s->srv_dep) (void)hipEventDestroy(s->srv_dep);
   if (s->out_stream) {
     (void)hipStreamSynchronize(s->out_stream);
     (void)hipStreamDestroy(s->out_stream);
-    g_device_extra_streams[s->device].fetch_sub(1, std::memory_order_relaxed);
+    g_queues.add_stream(s->device, -1);
   }
   for (auto e : s->out_events) (void)hipEventDestroy(e);
   if (s->own_stream) (void)hipStreamSynchronize(s->own_stream);

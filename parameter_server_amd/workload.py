@@ -106,6 +106,40 @@ def global_windows(n_producers: int, key_space: int, batch: int = MILLION, seed:
                        for s in range(n_producers)], dtype=np.int64)
 
 
+def complement_windows(push_bases, lo: int, hi: int, batch: int = MILLION, seed: int = 0,
+                       n_max: int | None = None) -> np.ndarray:
+    """The pull windows of a step on an aligned shard (cfg 2; the cold form; the
+    weak-scaled cfg 4): every `batch`-aligned window slot of [lo, hi) that the
+    step's push set does not touch, in a seeded random order, at most n_max of
+    them.  The pull then reads only parameters the step did not write, and reads
+    each once (no repeated window inside one Get)."""
+    slots = (hi - lo) // batch
+    pushed = {(int(b) - lo) // batch for b in push_bases}
+    free = np.array([s for s in range(slots) if s not in pushed], dtype=np.int64)
+    free = free[np.random.default_rng(seed).permutation(free.size)]
+    if n_max is not None:
+        free = free[:n_max]
+    return lo + free * batch
+
+
+def disjoint_windows(push_bases, n: int, key_space: int, batch: int = MILLION, seed: int = 0) -> np.ndarray:
+    """The pull windows of a cfg-4 step: n windows at uniformly random bases in
+    [0, key_space - batch] (any alignment), drawn in turn with seed `seed` + s and
+    redrawn until the window meets neither a pushed window nor an earlier pull
+    window — zero push/pull overlap, no key pulled twice."""
+    taken = sorted((int(b), int(b) + batch) for b in push_bases)
+    out = []
+    for s in range(n):
+        rng = np.random.default_rng(seed + s)
+        while True:
+            b = int(rng.integers(0, key_space - batch + 1))
+            if all(e <= b or b + batch <= a for a, e in taken):
+                break
+        taken.append((b, b + batch))
+        out.append(b)
+    return np.asarray(out, dtype=np.int64)
+
+
 def interval_union(intervals) -> int:
     """Number of distinct keys covered by half-open [a, a + n) intervals."""
     tot, end = 0, -1

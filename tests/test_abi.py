@@ -254,3 +254,22 @@ def test_python_range_partition_manager_mirror():
     pm2 = RangePartitionManager([0, 1, 2], [(2, 4), (4, 7), (7, 10)])
     sl2 = pm2.Slice(np.array([2, 8, 9], np.uint32))
     assert [(s, list(k)) for s, k in sl2] == [(0, [2]), (2, [8, 9])]
+
+
+def test_queue_accounting_per_device(tmp_path):
+    """The request server's hardware-queue accounting per device
+    (parameter_server_amd/csrc/pskv_queues.h), as a host-only C++
+    program built with g++ here: 2 * shards + 1 + extra streams <= GPU_MAX_HW_QUEUES
+    on EACH device, with CreateTable's i % ndev binding of 8 server threads
+    (driver/engine.hpp:98-110, include/ps/storage_factory.hpp)."""
+    import subprocess
+
+    src = os.path.join(ROOT, "tests", "cpp", "queue_accounting_test.cpp")
+    exe = str(tmp_path / "queue_accounting_test")
+    r = subprocess.run(["g++", "-O1", "-std=c++17", "-Wall", "-Werror",
+                        "-I", os.path.join(ROOT, "parameter_server_amd", "csrc"), src, "-o", exe],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert " 0 failed" in r.stdout

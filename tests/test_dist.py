@@ -63,10 +63,25 @@ def _worker(rank, world, port, q):
                 ref = oracle.range_slice_ref(ranges, np.array(keys, dtype=np.uint32))
                 want = [(q_, [k for k in keys if f <= k < f + n]) for f, n, q_ in ps_]
                 assert ref == want, (w, ref, want)
+            # the step's pull: J windows meeting no pushed window and no other
+            # pull, routed by the same map; every rank draws the same ones
+            pull, pbases = bench.plan_pull(rank, world, J, B, r, bases)
+            pp = [None] * world
+            dist.all_gather_object(pp, (pull, [int(b) for b in pbases]))
+            assert all(x[1] == pp[0][1] for x in pp)
+            assert sum(n for sl, _ in pp for _, _, n in sl) == J * B
+            for q_, (sl, _) in enumerate(pp):
+                a, b, _, _ = rr[q_]
+                assert all(a <= f and f + n <= b for _, f, n in sl)
+            assert bench.overlap_keys({"slices": slices, "pull": pull}) == 0
             # weak-scaled form: this rank's windows stay inside its range, whole
             _, lo_w, hi_w, sl_w, _ = bench.plan_rank(rank, world, J, B, r, weak=True)
             assert (lo_w, hi_w) == (lo, hi) and len(sl_w) == J
             assert all(lo <= f and f + n <= hi and n == B for _, f, n in sl_w)
+            _, b_w = bench.plan_rank(rank, world, J, B, r, weak=True)[3:]
+            pw, _ = bench.plan_pull(rank, world, J, B, r, b_w, weak=True)
+            assert pw and all(lo <= f and f + n <= hi for _, f, n in pw)
+            assert bench.overlap_keys({"slices": sl_w, "pull": pw}) == 0
         # reductions as bench.py does them (device = cpu under gloo)
         t = bench.max_over_ranks(float(rank + 1), world, torch.device("cpu"))
         u = bench.sum_over_ranks(10.0, world, torch.device("cpu"))

@@ -3,7 +3,7 @@ bench.py's PSKV_BENCH_SHARE_GPU rehearsal setup) each own one 5e8-key range
 shard of the 1e9-key space (base/range_partition_manager.hpp's map) and run
 bench.py's own step — 64 producer windows at uniformly random bases, sliced by
 the range map (straddling windows split), pushed as one grouped Add per rank,
-then the next set's windows pulled — through the timed region (barrier,
+then windows no push of the step touched pulled — through the timed region (barrier,
 synchronize, max over ranks).  Every pull, and at the end every rank's WHOLE
 dense array, is compared bit for bit with the oracle's sequential
 last-write-wins restatement (map_storage.hpp:17-27) of the slices that rank
@@ -59,7 +59,7 @@ def _rank(rank, world, port, q):
         host = [[(f, v.cpu().numpy()) for (_, f, _), (_, v) in zip(s["slices"], s["batches"])] for s in sets]
         with ps.Shard(lo, hi, np.float32, device=0) as sh:
             sh.set_stream(torch.cuda.current_stream().cuda_stream)
-            form = bench.Form(sh, sets, 1, dev)
+            form = bench.Form(sh, sets, dev)
             steps = 2 * R
             # stepwise: every pull against the oracle state after the step's Add
             for i in range(steps):
@@ -67,8 +67,9 @@ def _rank(rank, world, port, q):
                     oracle.dense_last_wins(ref, lo, np.arange(f, f + v.size, dtype=np.uint32), v)
                 form.step(i)
                 torch.cuda.synchronize()
-                t = form.pull_of(i)
-                for (_, f, n), o in zip(sets[t]["slices"], form.outs[t]):
+                t = i % R
+                assert bench.overlap_keys(sets[t]) == 0
+                for (_, f, n), o in zip(form.pull_slices[t], form.outs[t]):
                     got = o.cpu().numpy()
                     if not np.array_equal(got.view(np.uint32), ref[f - lo:f - lo + n].view(np.uint32)):
                         raise AssertionError(f"rank {rank} step {i}: pull of key {f} differs from the oracle")

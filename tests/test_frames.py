@@ -209,3 +209,28 @@ def test_frame_pool_reuses_and_trims(cuda):
     b.free()
     ps.host_pool_trim()
     assert ps.host_pool_stats()["cached_bytes"] == 0
+
+
+def test_page_locked_memory_has_one_address_on_every_device(cuda):
+    """The multi-device assumption behind in-place frame access:
+    page-locked host memory is mapped at its host address on every device, so
+    one frame pointer serves a kernel on any device (pskv_frames.cpp keeps a
+    frame's view only when hipHostGetDevicePointer returns the host address).
+    Checked on every visible device through the HIP runtime itself."""
+    import ctypes
+
+    import torch
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    p = ctypes.c_void_p()
+    assert hip.hipHostMalloc(ctypes.byref(p), ctypes.c_size_t(1 << 16),
+                             ctypes.c_uint(0x1 | 0x2)) == 0  # Portable | Mapped
+    try:
+        for d in range(torch.cuda.device_count()):
+            assert hip.hipSetDevice(d) == 0
+            dv = ctypes.c_void_p()
+            assert hip.hipHostGetDevicePointer(ctypes.byref(dv), p, ctypes.c_uint(0)) == 0
+            assert dv.value == p.value, f"device {d}: view {dv.value:#x} != host {p.value:#x}"
+    finally:
+        hip.hipSetDevice(0)
+        hip.hipHostFree(p)

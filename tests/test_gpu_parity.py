@@ -391,9 +391,57 @@ def test_baseline_size_dense_roundtrip(cuda):
         sh.sync()
 
 
+@pytest.mark.parametrize("space,R,steps", [(100_000_000, 16, 20), (1_000_000_000, 4, 6)],
+                         ids=["cfg2_1e8", "cold_1e9"])
+def test_bench_headline_form_bit_exact(cuda, oracle_mod, space, R, steps):
+    """The benchmarked state itself: bench.py's own sets and
+    Form — 64 x 1M windows at seed-42-family 1M-aligned bases per set, R sets
+    rotated, the sorted-hint grouped Add (K2g dense mode + verification + K4r),
+    then the grouped Get (K1) of the window slots the push left free (zero
+    push/pull overlap).  Every pull of every step is compared bit for bit with
+    the oracle's sequential last-write-wins restatement (map_storage.hpp:22-23;
+    never-written keys read 0, :33-37), and at the end the whole dense array.
+    cfg2_1e8 is the headline (N = 1, cfg 2); cold_1e9 is roofline.cold's form."""
+    import sys
+
+    import torch
+
+    import parameter_server_amd as ps
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    dev = torch.device(cuda)
+    J, B = 64, 1_000_000
+    n_pulls = [len(bench.plan_pull(0, 1, J, B, r, bench.plan_rank(0, 1, J, B, r)[4])[0]) for r in range(R)]
+    sp = None if space == 100_000_000 else space
+    sets = [bench.make_set(0, 1, J, B, dev, r, space=sp, n_pull=None if sp is None else n_pulls[r])
+            for r in range(R)]
+    assert all(bench.overlap_keys(s) == 0 for s in sets)
+    ref = np.zeros(space, np.float32)
+    host = [[(f, v.cpu().numpy()) for (_, f, _), (_, v) in zip(s["slices"], s["batches"])] for s in sets]
+    with ps.Shard(0, space, np.float32) as sh:
+        sh.set_stream(torch.cuda.current_stream().cuda_stream)
+        form = bench.Form(sh, sets, dev)
+        for i in range(steps):
+            t = i % R
+            for f, v in host[t]:
+                oracle_mod.dense_last_wins(ref, 0, np.arange(f, f + v.size, dtype=np.uint32), v)
+            form.step(i)
+            torch.cuda.synchronize()
+            for (_, f, n), o in zip(form.pull_slices[t], form.outs[t]):
+                assert_bits_equal(o.cpu().numpy(), ref[f:f + n], f"step {i}: pull of window {f}")
+        dense = sh.dense_view().cpu().numpy()
+        sh.set_stream(None)
+        sh.sync()
+    assert_bits_equal(dense, ref, "whole shard after the steps")
+    assert np.count_nonzero(ref) > 0
+
+
 def test_zipf_batches_parity(cuda, oracle_mod):
     """cfg 3 shape at reduced key space: unsorted Zipf(0.99) pushes with heavy
-    duplicates go through K4 (LDS dedup + stamps) and match the oracle."""
+    duplicates go through the default unhinted path (K5: LDS super-chunk dedup,
+    key buckets, bucket-owned resolve) and match the oracle."""
     import torch
 
     import parameter_server_amd as ps
@@ -414,12 +462,14 @@ def test_zipf_batches_parity(cuda, oracle_mod):
     assert_bits_equal(got, dense, "zipf")
 
 
-@pytest.mark.parametrize("dedup", [0, 1])
-def test_zipf_pulls_dedup(cuda, oracle_mod, dedup):
-    """K1 with and without the per-chunk pull-key dedup (option GET_DEDUP):
-    Zipf pulls (hot keys repeated hundreds of times per chunk), out-of-range
-    keys, the sentinel 0xFFFFFFFF, never-written keys, and chunks that mix dense
-    runs with scattered keys — bit-exact against the oracle."""
+@pytest.mark.parametrize("get_ntp", [0, 1])
+def test_zipf_pulls(cuda, oracle_mod, get_ntp):
+    """K1 on Zipf pulls (hot keys repeated hundreds of times per chunk),
+    out-of-range keys, the sentinel 0xFFFFFFFF, never-written keys, and chunks
+    that mix dense runs at every phase with scattered keys — bit-exact against
+    the oracle, with cached and non-temporal (option GET_NTP) parameter loads.
+    (Round 3's pull-key dedup variant, GET_DEDUP, measured no gain and was
+    removed in round 4.)"""
     import torch
 
     import parameter_server_amd as ps
@@ -428,7 +478,7 @@ def test_zipf_pulls_dedup(cuda, oracle_mod, dedup):
     space = 2_000_000
     zb = workload.zipf_batches(3, space, batch=300_000, device=cuda)
     ref = oracle_mod.MapStorageRef(np.float32)
-    with ps.Shard(0, space, np.float32, overflow_slots=1 << 12, options={"GET_DEDUP": dedup}) as sh:
+    with ps.Shard(0, space, np.float32, overflow_slots=1 << 12, options={"GET_NTP": get_ntp}) as sh:
         for k, v in zb:
             sh.add(k, v)
             ref.add(k.cpu().numpy().view(np.uint32), v.cpu().numpy())
@@ -438,6 +488,8 @@ def test_zipf_pulls_dedup(cuda, oracle_mod, dedup):
         ref.add(extra, xv)
         q = zb[0][0].cpu().numpy().view(np.uint32).copy()
         q[1000:1000 + 64] = np.arange(5000, 5064, dtype=np.uint32)       # dense runs inside scattered chunks
+        q[4096:4096 + 8192] = np.arange(7001, 7001 + 8192, dtype=np.uint32)  # a whole chunk run, phase 1
+        q[20480:20480 + 8192] = np.arange(9003, 9003 + 8192, dtype=np.uint32)  # phase 3
         q[7:40] = 0xFFFFFFFF
         q[50:60] = space + 5
         q[-9:] = np.arange(space + 100, space + 109, dtype=np.uint32)     # never written: 0
@@ -446,8 +498,8 @@ def test_zipf_pulls_dedup(cuda, oracle_mod, dedup):
         parts = [tdev(q[:q.size // 2], cuda), tdev(q[q.size // 2:], cuda)]
         sh.get_grouped(list(zip(parts, outs)))
         got = torch.cat(outs).cpu().numpy()
-        assert sh.get_option("GET_DEDUP") == dedup
-    assert_bits_equal(got, ref.get(q), f"zipf pulls, dedup {dedup}")
+        assert sh.get_option("GET_NTP") == get_ntp
+    assert_bits_equal(got, ref.get(q), f"zipf pulls, GET_NTP {get_ntp}")
 
 
 @pytest.mark.parametrize("mode", ["assign", "accumulate"])
@@ -1403,17 +1455,20 @@ def test_c_abi_error_paths_leave_the_shard_usable(cuda, oracle_mod):
     ref.close()
 
 
-def test_shard_options_api(cuda):
+def test_shard_options_api(cuda, monkeypatch, capfd):
     """pskv_set_option / pskv_get_option: every option by name, round trip,
     unknown names and out-of-range values rejected with PSKV_EINVAL (the shard
-    unchanged), the environment as the creation default."""
+    unchanged), the environment as the creation default -- where an invalid
+    value is reported on stderr and ignored, never a failed creation (ADVICE r3);
+    the options removed in round 4 (GET_DEDUP, RB_INSERT: measured losers) are
+    unknown names now."""
     import parameter_server_amd as ps
     from parameter_server_amd import PskvError, _lib
 
-    names = ["GENERAL", "UNROLL", "NT", "NTP", "EARLY", "GET_DEDUP", "GET_NTP", "PAGEABLE_DMA", "DMA_MIN_BYTES", "DMA_MIN_BYTES_GET",
+    names = ["GENERAL", "UNROLL", "NT", "NTP", "EARLY", "GET_NTP", "PAGEABLE_DMA", "DMA_MIN_BYTES", "DMA_MIN_BYTES_GET",
              "DMA_MIN_BYTES_PINNED", "ZC_MAX_BYTES", "FRAME_ZC_MAX_BYTES", "INLINE", "INLINE_ADD_CHUNKS",
              "INLINE_GET_CHUNKS", "ISPIN", "SERVE", "SERVE_IDLE_US", "TILE_SHIFT", "TILE_GRID", "RB_WBITS",
-             "RB_NBD", "RB_TB", "RB_APPLY_LOG2", "RB_BIN_BLOCK", "RB_INSERT"]
+             "RB_NBD", "RB_TB", "RB_APPLY_LOG2", "RB_BIN_BLOCK"]
     with ps.Shard(0, 1000, np.float32) as sh:
         for n in names:
             sh.set_option(n, sh.get_option(n))  # every default is a valid value
@@ -1424,8 +1479,8 @@ def test_shard_options_api(cuda):
         sh.set_option("ZC_MAX_BYTES", 12345)
         assert sh.get_option("ZC_MAX_BYTES") == 12345
         for n, bad in (("UNROLL", 5), ("RB_APPLY_LOG2", 12), ("TILE_SHIFT", 3), ("INLINE", 2),
-                        ("RB_BIN_BLOCK", 768), ("NOPE", 1)):
-            before = sh.get_option(n) if n != "NOPE" else None
+                        ("RB_BIN_BLOCK", 768), ("NOPE", 1), ("GET_DEDUP", 1), ("RB_INSERT", 1)):
+            before = sh.get_option(n) if n in names else None
             with pytest.raises(PskvError) as ei:
                 sh.set_option(n, bad)
             assert ei.value.code == _lib.PSKV_EINVAL
@@ -1436,3 +1491,22 @@ def test_shard_options_api(cuda):
         assert np.array_equal(sh.get(k), k.astype(np.float32))
     with ps.Shard(0, 1000, np.float32, options={"SERVE": 1}) as sh:
         assert sh.get_option("INLINE_ADD_CHUNKS") == 2  # the server's small-Add default
+    # the environment: valid values become creation defaults, invalid ones are
+    # reported and ignored (the shard is created with the built-in default)
+    monkeypatch.setenv("PSKV_UNROLL", "4")
+    monkeypatch.setenv("PSKV_TILE_SHIFT", "5")      # out of range
+    monkeypatch.setenv("PSKV_GENERAL", "bogus")     # unknown name
+    monkeypatch.setenv("PSKV_RB_BIN_BLOCK", "1024x")  # not a number
+    capfd.readouterr()
+    with ps.Shard(0, 1000, np.float32) as sh:
+        assert sh.get_option("UNROLL") == 4
+        assert sh.get_option("TILE_SHIFT") == 0
+        assert sh.get_option("GENERAL") == 1
+        assert sh.get_option("RB_BIN_BLOCK") == 1024
+        k = np.arange(100, dtype=np.uint32)
+        sh.add(k, k.astype(np.float32) + 1)
+        assert np.array_equal(sh.get(k), k.astype(np.float32) + 1)
+    err = capfd.readouterr().err
+    for var in ("PSKV_TILE_SHIFT", "PSKV_GENERAL", "PSKV_RB_BIN_BLOCK"):
+        assert f"ignoring environment {var}=" in err, err
+    assert "PSKV_UNROLL" not in err

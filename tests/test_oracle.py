@@ -108,9 +108,10 @@ def test_bench_step_bytes_and_single_gpu_sets():
     """bench.py's algorithmic byte accounting (counting what a step
     must move: Add n*4 keys + u*V last values + u*V parameter writes, Get
     q*(4+2V)) and the N = 1 window sets: 1M-aligned bases inside the 1e8-key
-    shard, set 0 on the config's seed 42, the other sets on distinct seeds, and
-    a push set plus the next pull set touching more than the 256 MB Infinity
-    Cache."""
+    shard, set 0 on the config's seed 42, the other sets on distinct seeds; the
+    pull of each step is every window slot its push left free, each once — zero
+    push/pull overlap (the Get must read parameters the step did not
+    write) — so a step touches the whole 400 MB shard."""
     import sys
 
     sys.path.insert(0, ROOT)
@@ -127,11 +128,40 @@ def test_bench_step_bytes_and_single_gpu_sets():
         assert all(b % 1_000_000 == 0 and 0 <= b <= 99_000_000 for b in bases)
         assert [(w, f, n) for w, f, n in slices] == [(j, int(b), 1_000_000) for j, b in enumerate(bases)]
         seen.append(tuple(int(b) for b in bases))
+        pull, pbases = bench.plan_pull(0, 1, 64, 1_000_000, r, bases)
+        pushed = set(int(b) for b in bases)
+        assert len(pull) == 100 - len(pushed) and len(set(int(b) for b in pbases)) == len(pull)
+        assert not pushed & set(int(b) for b in pbases)
+        assert sorted(pushed | set(int(b) for b in pbases)) == list(range(0, 100_000_000, 1_000_000))
+        s = {"slices": slices, "pull": pull}
+        assert bench.overlap_keys(s) == 0
+        # the cold form: the same draw on a 1e9-key shard, as many pulls
+        _, _, hi9, sl9, b9 = bench.plan_rank(0, 1, 64, 1_000_000, r, space=1_000_000_000)
+        p9, pb9 = bench.plan_pull(0, 1, 64, 1_000_000, r, b9, space=1_000_000_000, n_pull=len(pull))
+        assert hi9 == 1_000_000_000 and len(p9) == len(pull)
+        assert bench.overlap_keys({"slices": sl9, "pull": p9}) == 0
     assert len(set(seen)) == 4
     assert seen[0] == tuple(int(b) for b in workload.dense_bases(64, 100_000_000, 1_000_000, seed=42))
-    for r in range(4):  # parameters touched by step r: push set r and pull set r+1
-        touched = workload.interval_union([(b, 1_000_000) for b in seen[r] + seen[(r + 1) % 4]]) * 4
-        assert touched > 256 << 20, (r, touched)
+    # an overlapping pull is detected
+    assert bench.overlap_keys({"slices": [(0, 5, 10)], "pull": [(0, 12, 10)]}) == 3
+
+
+def test_disjoint_and_complement_windows():
+    from parameter_server_amd import workload
+
+    push = workload.global_windows(64, 1_000_000_000, 1_000_000, seed=1000)
+    pull = workload.disjoint_windows(push, 64, 1_000_000_000, 1_000_000, seed=7)
+    assert pull.shape == (64,) and int(pull.min()) >= 0 and int(pull.max()) <= 999_000_000
+    iv = sorted([(int(b), int(b) + 1_000_000) for b in pull])
+    assert all(iv[i][1] <= iv[i + 1][0] for i in range(len(iv) - 1))  # pulls pairwise disjoint
+    assert all(e <= int(p) or int(p) + 1_000_000 <= int(b)
+               for p in pull for b, e in ((int(x), int(x) + 1_000_000) for x in push))
+    assert list(workload.disjoint_windows(push, 64, 1_000_000_000, 1_000_000, seed=7)) == list(pull)
+    c = workload.complement_windows([0, 20, 20, 60], 0, 100, 20, seed=3)
+    assert sorted(int(x) for x in c) == [40, 80]
+    assert len(workload.complement_windows([0], 0, 100, 20, seed=3, n_max=2)) == 2
+    c2 = workload.complement_windows([1000, 1040], 1000, 1100, 20, seed=1)
+    assert sorted(int(x) for x in c2) == [1020, 1060, 1080]
 
 
 def test_interval_union_and_global_windows():

@@ -161,3 +161,43 @@ def test_serve_several_shards_one_device(cuda, oracle_mod, serve, nshards):
     finally:
         for sh in shards:
             sh.close()
+
+
+def test_serve_start_waits_for_slow_stream_work(cuda, oracle_mod, serve):
+    """A server launch queued behind > 2 s of earlier work on the shard's stream
+    (here a spin kernel on the legacy default stream, which the shard's blocking
+    stream orders behind) is not "stuck": srv_wait starts its start-timeout
+    clock only once that dependency has completed (a long replay of a
+    broken sorted hint followed by a small served Get used to fail with
+    PSKV_ESTATE after 2 s)."""
+    import torch
+
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(31)
+    ref = oracle_mod.MapStorageRef(np.float32)
+    # calibrate the spin kernel (it counts shader clocks)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    torch.cuda._sleep(100_000_000)
+    e1.record()
+    torch.cuda.synchronize()
+    cycles_per_ms = 100_000_000 / max(e0.elapsed_time(e1), 1e-3)
+    with ps.Shard(0, 10_000, np.float32, options=dict(serve, SERVE_IDLE_US=1000)) as sh:
+        k = rng.integers(0, 10_000, size=100).astype(np.uint32)
+        v = rng.standard_normal(k.size).astype(np.float32)
+        sh.add(k, v)
+        ref.add(k, v)
+        assert_bits_equal(sh.get(k), ref.get(k), "before")
+        time.sleep(0.05)  # the server idles out
+        torch.cuda._sleep(int(4000 * cycles_per_ms))  # ~4 s of earlier work
+        t0 = time.perf_counter()
+        k2 = rng.integers(0, 10_000, size=100).astype(np.uint32)
+        v2 = rng.standard_normal(k2.size).astype(np.float32)
+        sh.add(k2, v2)  # relaunches the server behind the spin kernel
+        ref.add(k2, v2)
+        q = rng.integers(0, 10_000, size=300).astype(np.uint32)
+        got = sh.get(q)
+        waited = time.perf_counter() - t0
+    assert_bits_equal(got, ref.get(q), "after the slow dependency")
+    assert waited > 2.0, f"the dependency did not delay the served calls ({waited:.2f} s): the test lost its point"

@@ -27,6 +27,9 @@
 #   align_own    tools/align_probe.py with K2g slot-aligned chunks (EARLY=0) vs own-range chunks (EARLY=3), twice
 #   zwbits       K5 bucket windows of 2^11 (default) vs 2^12 keys on cfg-3 Zipf and on unhinted dense pushes
 #   rbins        K5a per-lane probe insert (RB_INSERT=1): the K5 parity tests under it, then the cfg-3 A/B
+#   coldmicro    tools/micro/cold_stream: HBM ceilings of the dense step's access shapes, every byte cold
+#   coldbench    bench.py --cold-only (the headline step on a 1e9-key shard: roofline.cold's form)
+#   coldopts     the cold form under cache-policy options (GET_NTP, NTP, both, NT=0)
 #   smoke        __graft_entry__.smoke() (what the driver runs before the bench)
 #   shardsize    tools/shard_size_probe.py: K2g / K1 per key on 1e8 / 5e8 / 1e9-key shards (same windows)
 #   getntp       tools/shard_size_probe.py with K1 parameter loads cached / non-temporal (GET_NTP=0/1), twice
@@ -112,6 +115,12 @@ for step in "$@"; do
           "$R/tests/test_gpu_parity.py" -k "zipf or radix or random or golden or accumulate or sentinel or ragged" \
           > "$OUT/rbins_tests.log" 2>&1 &&
         PROBE_ROUNDS=10 timeout -k 10 300 python3 "$R/tools/zipf_probe.py" "" "PSKV_RB_INSERT=1" > "$OUT/rbins_zipf.log" 2>&1 ;;
+    coldmicro) timeout -k 10 200 "$R/tools/micro/cold_stream" > "$OUT/cold_stream.log" 2>&1 ;;
+    coldbench) timeout -k 10 300 python3 "$R/bench.py" --cold-only --steps 50 > "$OUT/cold.json" 2> "$OUT/cold.err" ;;
+    coldopts) for o in "" "PSKV_GET_NTP=1" "PSKV_NTP=1" "PSKV_GET_NTP=1 PSKV_NTP=1" "PSKV_NT=0"; do
+          tag=$(echo "x$o" | tr ' =' '__')
+          env $o timeout -k 10 300 python3 "$R/bench.py" --cold-only --steps 50 > "$OUT/cold$tag.json" 2> "$OUT/cold$tag.err" || exit 1
+        done ;;
     smoke) timeout -k 10 300 python3 -c "import sys; sys.path.insert(0, '$R'); import __graft_entry__ as g; g.smoke()" \
         > "$OUT/smoke.log" 2>&1 ;;
     shardsize) timeout -k 10 400 python3 "$R/tools/shard_size_probe.py" > "$OUT/shard_size.log" 2>&1 &&
