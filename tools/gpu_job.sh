@@ -30,6 +30,8 @@
 #   coldmicro    tools/micro/cold_stream: HBM ceilings of the dense step's access shapes, every byte cold
 #   coldbench    bench.py --cold-only (the headline step on a 1e9-key shard: roofline.cold's form)
 #   coldopts     the cold form under cache-policy options (GET_NTP, NTP, both, NT=0)
+#   ntp_ab       the headline (and its cold form) with K2g parameter stores cached / non-temporal, twice
+#   emu_ntp      every rank of N = 8 emulated, K2g parameter stores cached / non-temporal
 #   smoke        __graft_entry__.smoke() (what the driver runs before the bench)
 #   shardsize    tools/shard_size_probe.py: K2g / K1 per key on 1e8 / 5e8 / 1e9-key shards (same windows)
 #   getntp       tools/shard_size_probe.py with K1 parameter loads cached / non-temporal (GET_NTP=0/1), twice
@@ -121,6 +123,14 @@ for step in "$@"; do
           tag=$(echo "x$o" | tr ' =' '__')
           env $o timeout -k 10 300 python3 "$R/bench.py" --cold-only --steps 50 > "$OUT/cold$tag.json" 2> "$OUT/cold$tag.err" || exit 1
         done ;;
+    ntp_ab) for r in 1 2; do for e in 0 1; do
+          PSKV_NTP=$e timeout -k 10 300 python3 "$R/bench.py" --steps 50 --no-zipf --no-extra --no-cpu-baseline \
+            > "$OUT/ntp${e}_$r.json" 2> "$OUT/ntp${e}_$r.err" || exit 1
+        done; done ;;
+    emu_ntp) for r in 0 1 2 3 4 5 6 7; do for e in 0 1; do
+          PSKV_NTP=$e PSKV_BENCH_EMULATE=$r/8 timeout -k 10 200 python3 "$R/bench.py" --steps 50 --no-zipf \
+            --no-cpu-baseline --no-extra > "$OUT/emu8_${r}_ntp$e.json" 2> "$OUT/emu8_${r}_ntp$e.err" || exit 1
+        done; done ;;
     smoke) timeout -k 10 300 python3 -c "import sys; sys.path.insert(0, '$R'); import __graft_entry__ as g; g.smoke()" \
         > "$OUT/smoke.log" 2>&1 ;;
     shardsize) timeout -k 10 400 python3 "$R/tools/shard_size_probe.py" > "$OUT/shard_size.log" 2>&1 &&
