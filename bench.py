@@ -285,8 +285,10 @@ class Form:
         self.get_b = [step_bytes(0, 0, sum(n for _, _, n in p), vb)[1] for p in self.pull_slices]
 
     def step(self, i):
-        self.shard.add_grouped(self.adds[i % self.R], sorted_hint=self.hint)
-        self.shard.get_grouped(self.gets[i % self.R])
+        # the grouped Add then the grouped Get, in one call
+        # (pskv_add_get_grouped: one fused launch for hinted device windows,
+        # option FUSE; PSKV_FUSE=0 runs them as the two separate calls)
+        self.shard.add_get_grouped(self.adds[i % self.R], self.gets[i % self.R], sorted_hint=self.hint)
 
     def bytes(self, steps):
         """(add bytes, get bytes) of steps 0..steps-1."""
@@ -338,17 +340,22 @@ def timed(form, steps, world, dev):
     return max_over_ranks(own, world, dev), own
 
 
-def evented(form, steps, world, dev):
-    """The same steps again with HIP events around the two streaming kernels on
+def evented(form, steps, world, dev, fuse=None):
+    """The same steps again with HIP events around the streaming kernels on
     their launch stream: per-kernel launches and average duration, and the
-    algorithmic bytes per launch (this rank's)."""
+    algorithmic bytes per launch (this rank's).  The fused Add + Get launch
+    (K10) moves both halves' bytes; fuse=0 runs the step as the separate K2g /
+    K1 launches for their own rates (the shard's FUSE option, restored after)."""
     import torch
 
     from parameter_server_amd import _lib
 
     sh = form.shard
+    old = sh.get_option("FUSE")
+    if fuse is not None:
+        sh.set_option("FUSE", fuse)
     sh.reset_timing()
-    sh.set_timing(True, kernels=[_lib.PSKV_K_GATHER, _lib.PSKV_K_ASSIGN_TILES])
+    sh.set_timing(True, kernels=[_lib.PSKV_K_GATHER, _lib.PSKV_K_ASSIGN_TILES, _lib.PSKV_K_ADD_GET])
     torch.cuda.synchronize()
     t2 = time.perf_counter()
     for i in range(steps):
@@ -356,12 +363,13 @@ def evented(form, steps, world, dev):
     torch.cuda.synchronize()
     t3 = time.perf_counter()
     sh.set_timing(False)
+    sh.set_option("FUSE", old)
     add_b, get_b = form.bytes(steps)
     ktimes = {}
     for k, name in _lib.KERNEL_NAMES.items():
         t = sh.kernel_time(k)
         if t["launches"]:
-            b = get_b if k == _lib.PSKV_K_GATHER else add_b
+            b = {_lib.PSKV_K_GATHER: get_b, _lib.PSKV_K_ADD_GET: add_b + get_b}.get(k, add_b)
             rec = {"launches": t["launches"], "avg_ms": t["total_ms"] / t["launches"],
                    "keys_per_launch": t["elements"] / t["launches"],
                    "algorithmic_bytes": b / t["launches"]}
@@ -371,14 +379,19 @@ def evented(form, steps, world, dev):
     return ktimes, max_over_ranks(t3 - t2, world, dev)
 
 
-def run_form(form, steps, warmup, world, dev):
-    """Warm up, time, and sum the bytes over ranks: the aggregate GB/s of a form."""
+def run_form(form, steps, warmup, world, dev, fuse=None):
+    """Warm up, time, and sum the bytes over ranks: the aggregate GB/s of a form
+    (fuse: the shard's FUSE option for this measurement, restored after)."""
     import torch
 
+    old = form.shard.get_option("FUSE")
+    if fuse is not None:
+        form.shard.set_option("FUSE", fuse)
     for i in range(warmup):
         form.step(i)
     torch.cuda.synchronize()
     elapsed, own = timed(form, steps, world, dev)
+    form.shard.set_option("FUSE", old)
     a, g = form.bytes(steps)
     total = sum_over_ranks(float(a + g), world, dev)
     return {"GB/s": total / elapsed / 1e9, "ms_per_step": elapsed / steps * 1e3, "elapsed": elapsed,
@@ -909,6 +922,8 @@ def cold_form(dev, J, B, R, steps, warmup, space, n_pulls):
         f.self_check(0, space, dev)
         res = run_form(f, steps, max(warmup, R), 1, dev)
         kt, ev_s = evented(f, steps, 1, dev)
+        kt_sep, _ = evented(f, steps, 1, dev, fuse=0)
+        sep = run_form(f, steps, 2, 1, dev, fuse=0)
         sh.set_stream(None)
     a, g = f.bytes(steps)
     del f, sets
@@ -919,7 +934,9 @@ def cold_form(dev, J, B, R, steps, warmup, space, n_pulls):
                         "parameter read and write is served by HBM",
             "shard_keys": int(space), "GB/s": res["GB/s"], "ms_per_step": res["ms_per_step"],
             "bytes_per_step": (a + g) / steps, "ms_per_step_evented": ev_s / steps * 1e3,
-            "kernels": kernel_fracs(kt)}
+            "kernels": kernel_fracs(kt),
+            "separate_launches": {"GB/s": sep["GB/s"], "ms_per_step": sep["ms_per_step"],
+                                  "kernels": kernel_fracs(kt_sep)}}
 
 
 def main(argv=None):
@@ -972,6 +989,10 @@ def main(argv=None):
     form.self_check(lo, hi, dev)
     head = run_form(form, args.steps, max(args.warmup, R), world, dev)
     ktimes, evented_s = evented(form, args.steps, world, dev)
+    # the same step as the separate K2g / K1 launches (FUSE = 0): each kernel's
+    # own rate, and the step without the fused launch
+    ktimes_sep, _ = evented(form, args.steps, world, dev, fuse=0)
+    sep = run_form(form, args.steps, 2, world, dev, fuse=0)
     touched = min(form.touched(i) for i in range(R))
     a_b, g_b = form.bytes(args.steps)
     own_bytes = a_b + g_b
@@ -1005,7 +1026,9 @@ def main(argv=None):
                       "kernels, over a second pass of the same K steps run right after the "
                       "event-free timed region",
             "ms_per_step_evented": evented_s / args.steps * 1e3,
-            "kernels": kernel_fracs(ktimes)}
+            "kernels": kernel_fracs(ktimes),
+            "separate_launches": {"GB/s": sep["GB/s"], "ms_per_step": sep["ms_per_step"],
+                                  "kernels": kernel_fracs(ktimes_sep)}}
     if cold is not None:
         roof["cold"] = cold
     if traffic_src:

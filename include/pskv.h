@@ -137,8 +137,9 @@ enum pskv_kernel {
   PSKV_K_ACC_DENSE = 7,     /* K7: accumulate dense windows, one RMW per key */
   PSKV_K_INLINE_ADD = 8,    /* K8: small host Add carried in the kernel arguments */
   PSKV_K_INLINE_GET = 9,    /* K8: small host Get, reply written to page-locked memory */
-  PSKV_K_REPLAY = 10,       /* K4r: conditional replay behind a verifying sorted-path group */
-  PSKV_K_COUNT = 11
+  PSKV_K_REPLAY = 10,       /* K4r / K10r: conditional replay behind a verifying sorted-path group */
+  PSKV_K_ADD_GET = 11,      /* K10: fused grouped sorted Add + grouped Get */
+  PSKV_K_COUNT = 12
 };
 
 /* Create a shard owning keys [key_begin, key_end) on `device`.  The dense
@@ -172,6 +173,16 @@ int pskv_get(pskv_shard* s, const uint32_t* keys, uint64_t n, void* out, int fla
  * fixed number of kernel launches. */
 int pskv_add_grouped(pskv_shard* s, const pskv_batch* batches, uint64_t nb, int flags);
 int pskv_get_grouped(pskv_shard* s, const pskv_batch* batches, uint64_t nb, int flags);
+/* pskv_add_grouped(adds) then pskv_get_grouped(gets) in one call: the BSP
+ * model's flush of its deferred Adds followed by the Gets that flush releases
+ * (server/consistency/bsp_model.cpp:14-31), or one worker round's push then
+ * pull.  Identical results.  For device batches under PSKV_SORTED_HINT (4-byte
+ * values, assign mode, 16-byte-aligned batches) the Add group and the Get
+ * group run as ONE launch (option FUSE), the Get's workgroups starting as the
+ * Add's finish; a wrong hint is repaired (the Get answered again) as for
+ * pskv_add. */
+int pskv_add_get_grouped(pskv_shard* s, const pskv_batch* adds, uint64_t na, const pskv_batch* gets,
+                         uint64_t ng, int flags);
 
 /* Wait for the shard's stream, grow the overflow table if needed, report
  * sticky device errors. */

@@ -35,7 +35,8 @@ PSKV_K_ACC_DENSE = 7
 PSKV_K_INLINE_ADD = 8
 PSKV_K_INLINE_GET = 9
 PSKV_K_REPLAY = 10
-PSKV_K_COUNT = 11
+PSKV_K_ADD_GET = 11
+PSKV_K_COUNT = 12
 KERNEL_NAMES = {
     PSKV_K_GATHER: "k_gather",
     PSKV_K_ASSIGN_SORTED: "k_assign_sorted",
@@ -48,12 +49,13 @@ KERNEL_NAMES = {
     PSKV_K_INLINE_ADD: "k_inline_add",
     PSKV_K_INLINE_GET: "k_inline_get",
     PSKV_K_REPLAY: "k_replay",
+    PSKV_K_ADD_GET: "k_add_get",
 }
 
 # Every symbol include/pskv.h declares (checked by tests/test_abi.py).
 EXPORTED = [
     "pskv_shard_create", "pskv_shard_create_ex", "pskv_shard_destroy", "pskv_add", "pskv_get",
-    "pskv_add_grouped", "pskv_get_grouped", "pskv_sync", "pskv_clear", "pskv_set_stream",
+    "pskv_add_grouped", "pskv_get_grouped", "pskv_add_get_grouped", "pskv_sync", "pskv_clear", "pskv_set_stream",
     "pskv_get_stream", "pskv_dense_ptr", "pskv_shard_info", "pskv_set_timing", "pskv_set_timing_mask",
     "pskv_kernel_time", "pskv_reset_timing", "pskv_range_slice", "pskv_jump_hash", "pskv_last_error",
     "pskv_abi_version", "pskv_device_count", "pskv_host_alloc", "pskv_host_free",
@@ -97,6 +99,7 @@ def _load():
         "pskv_get": ([vp, vp, u64, vp, i32], i32),
         "pskv_add_grouped": ([vp, ctypes.POINTER(PskvBatch), u64, i32], i32),
         "pskv_get_grouped": ([vp, ctypes.POINTER(PskvBatch), u64, i32], i32),
+        "pskv_add_get_grouped": ([vp, ctypes.POINTER(PskvBatch), u64, ctypes.POINTER(PskvBatch), u64, i32], i32),
         "pskv_sync": ([vp], i32),
         "pskv_clear": ([vp], i32),
         "pskv_set_stream": ([vp, vp], i32),

@@ -52,9 +52,9 @@ struct DevBatch {
 struct GroupArgs {
   int nb;
   uint32_t wg_prefix[kMaxBatches + 1];  // first workgroup of each batch
-  uint64_t elem_prefix[kMaxBatches];    // group-wide index of each batch's first element
   DevBatch b[kMaxBatches];
 };
+static_assert(sizeof(GroupArgs) <= 1800, "two groups (the fused Add+Get launch) fit the 4 KiB kernarg segment");
 
 // K8: a whole small message inside the kernel arguments (<= 4 KiB kernarg).
 struct InlineAdd {
@@ -131,6 +131,16 @@ hipError_t launch_general_mark(int dtype, int mode, const GroupArgs& ga, uint32_
 hipError_t launch_general_commit(int vb, const GroupArgs& ga, uint32_t nwg, const DenseView& d,
                                  const Ovf& o, const unsigned long long* owner,
                                  const uint32_t* cond, uint32_t epoch, hipStream_t st);
+// K10 fused grouped sorted Add + grouped Get (4-byte values, aligned batches,
+// assign): persistent grid of `grid` <= add_get_max_grid() workgroups; the
+// tile mode's grid barrier waits until *bar reaches bar_target (every launch
+// adds `grid` to *bar).  K10r replays + answers the Get again on a tag.
+hipError_t launch_add_get(bool ntp, const GroupArgs& ga, const GroupArgs& gg, const DenseView& d, const Ovf& o,
+                          uint32_t tile_shift, uint64_t ntiles, uint32_t grid, uint32_t* flag, uint32_t epoch,
+                          unsigned long long* bar, unsigned long long bar_target, hipStream_t st);
+int add_get_max_grid();
+hipError_t launch_replay_get(const GroupArgs& ga, const GroupArgs& gg, const DenseView& d, const Ovf& o,
+                             const uint32_t* cond, uint32_t epoch, hipStream_t st);
 hipError_t launch_ovf_rehash(int vb, const Ovf& from, uint64_t from_cap, const Ovf& to,
                              hipStream_t st);
 // K4r: conditional replay of a group in call order by ONE workgroup (runs only

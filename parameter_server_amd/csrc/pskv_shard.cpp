@@ -259,6 +259,11 @@ struct pskv_shard {
   int tune_unroll = 8;   // PSKV_UNROLL: 4 or 8 (8: measured +5 % on the dense Add)
   bool tune_nt = true;   // PSKV_NT: non-temporal streams (measured +12-15 % on K1 / K2g)
   bool tune_ntp = false; // PSKV_NTP: non-temporal parameter stores (dense Add)
+  // PSKV_FUSE: pskv_add_get_grouped runs its last Add group and first Get group
+  // as ONE launch (K10) where it can (1), or as the separate calls (0)
+  bool tune_fuse = true;
+  int fuse_grid_max = 0;          // K10's co-resident grid (occupancy query, at first use)
+  unsigned long long bar_count = 0;  // K10's barrier counter: every launch adds its grid
   bool tune_get_ntp = false;  // PSKV_GET_NTP: non-temporal parameter loads in K1 (4-byte values, 16-byte aligned runs)
   int tune_early = 2;    // PSKV_EARLY: K2g early loads (0 never, 1 always, 2 when the group's keys cover < 1/4 of the range)
   // PSKV_PAGEABLE_DMA: DMA pageable host buffers directly (the runtime moves
@@ -631,14 +636,12 @@ uint32_t build_group(const std::vector<pskv_batch>& v, size_t b, size_t e, uint6
                      GroupArgs* ga) {
   std::memset(ga, 0, sizeof(*ga));
   ga->nb = (int)(e - b);
-  uint64_t wg = 0, el = 0;
+  uint64_t wg = 0;
   for (size_t i = b; i < e; ++i) {
     const int j = (int)(i - b);
     ga->wg_prefix[j] = (uint32_t)wg;
-    ga->elem_prefix[j] = el;
     ga->b[j] = DevBatch{v[i].keys, v[i].vals, v[i].n};
     wg += (v[i].n + chunk - 1) / chunk;
-    el += v[i].n;
   }
   ga->wg_prefix[e - b] = (uint32_t)wg;
   return (uint32_t)wg;
@@ -1736,6 +1739,102 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
   return PSKV_OK;
 }
 
+// ---------------------------------------------------- fused Add + Get (K10)
+// pskv_add_get_grouped: the same as pskv_add_grouped(adds) followed by
+// pskv_get_grouped(gets) -- BSPModel::Clock's flush of the deferred Adds
+// followed by the Gets it released (server/consistency/bsp_model.cpp:14-31), or
+// one worker round's push then pull.  Device batches under the sorted hint,
+// 4-byte values, assign mode, every pointer 16-byte aligned, the default
+// streams (UNROLL 8, NT 1) and option FUSE: the last Add launch group and the
+// first Get launch group run as ONE launch (K10) followed by the conditional
+// K10r; every other case, and every other group, takes the separate paths.
+int add_get_impl(pskv_shard* s, const std::vector<pskv_batch>& adds, const std::vector<pskv_batch>& gets,
+                 int flags) {
+  std::vector<pskv_batch> va, vg;
+  for (auto& b : adds) {
+    if (b.n == 0) continue;
+    if (!b.keys || !b.vals) return fail(PSKV_EINVAL, "pskv_add: null keys/vals with n > 0");
+    push_pieces(va, b, (size_t)s->vb);
+  }
+  for (auto& b : gets) {
+    if (b.n == 0) continue;
+    if (!b.keys || !b.vals) return fail(PSKV_EINVAL, "pskv_get: null keys/out with n > 0");
+    push_pieces(vg, b, (size_t)s->vb);
+  }
+  bool vec = true;
+  for (auto& b : va) vec &= aligned16(b.keys) & aligned16(b.vals);
+  for (auto& b : vg) vec &= aligned16(b.keys) & aligned16(b.vals);
+  const bool fuse = s->tune_fuse && (flags & PSKV_DEVICE) && (flags & PSKV_SORTED_HINT) &&
+                    s->mode == PSKV_ASSIGN && s->vb == 4 && s->tune_unroll == 8 && s->tune_nt && vec &&
+                    !va.empty() && !vg.empty();
+  if (!fuse) {
+    int rc = add_impl(s, adds, flags);
+    if (rc) return rc;
+    return get_impl(s, gets, flags & ~PSKV_SORTED_HINT);
+  }
+  s->n_add++;
+  s->n_get++;
+  int rc = use_device(s);
+  if (rc) return rc;
+  rc = srv_stop(s);
+  if (rc) return rc;
+  if (!s->fuse_grid_max) {
+    s->fuse_grid_max = add_get_max_grid();
+    if (s->fuse_grid_max <= 0) return fail(PSKV_EHIP, "fused Add+Get: occupancy query failed");
+  }
+  const auto ag = split_groups(va);
+  const auto gg = split_groups(vg);
+  for (size_t i = 0; i + 1 < ag.size(); ++i) {  // all Add groups but the last: the sorted path
+    rc = sorted_add(s, va, ag[i].first, ag[i].second, true, next_epoch(s), /*repair=*/true, /*maybe_windows=*/true);
+    if (rc) return rc;
+  }
+  {
+    const uint32_t epoch = next_epoch(s);
+    const auto& a = ag.back();
+    const auto& g = gg.front();
+    GroupArgs gaa, gga;
+    const uint32_t nadd = build_group(va, a.first, a.second, stream_chunk(8), &gaa);
+    const uint32_t nget = build_group(vg, g.first, g.second, stream_chunk(8), &gga);
+    uint64_t elems = 0;
+    for (size_t i = a.first; i < a.second; ++i) elems += va[i].n;
+    for (size_t i = g.first; i < g.second; ++i) elems += vg[i].n;
+    uint64_t add_elems = 0;
+    for (size_t i = a.first; i < a.second; ++i) add_elems += va[i].n;
+    uint32_t shift = 16;  // the tile mode's tiles, as sorted_add
+    while (shift > 12 && (add_elems >> shift) < 2048) --shift;
+    if (s->tune_tile_shift) shift = s->tune_tile_shift;
+    const uint64_t ntiles = (s->range + (1ull << shift) - 1) >> shift;
+    const uint64_t want = std::max<uint64_t>({(uint64_t)nadd, (uint64_t)nget, std::min<uint64_t>(ntiles, 1024)});
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(want, (uint64_t)s->fuse_grid_max);
+    s->bar_count += grid;
+    unsigned long long* bar = reinterpret_cast<unsigned long long*>(s->flag + 2);
+    {
+      LaunchTimer t(s, PSKV_K_ADD_GET, elems);
+      PSKV_HIP(launch_add_get(s->tune_ntp, gaa, gga, s->dview(), s->ovf, shift, ntiles, grid, s->flag, epoch, bar,
+                              s->bar_count, s->stream));
+      t.done();
+    }
+    {
+      LaunchTimer t(s, PSKV_K_REPLAY, add_elems);
+      PSKV_HIP(launch_replay_get(gaa, gga, s->dview(), s->ovf, s->flag, epoch, s->stream));
+      t.done();
+    }
+    s->n_sorted++;
+    s->n_general++;
+  }
+  for (size_t i = 1; i < gg.size(); ++i) {  // the other Get groups: K1
+    GroupArgs ga;
+    const uint32_t nwg = build_group(vg, gg[i].first, gg[i].second, stream_chunk(gather_unroll(s)), &ga);
+    uint64_t elems = 0;
+    for (size_t k = gg[i].first; k < gg[i].second; ++k) elems += vg[k].n;
+    LaunchTimer t(s, PSKV_K_GATHER, elems);
+    PSKV_HIP(launch_gather(s->vb, true, gather_unroll(s), s->tune_nt, s->tune_get_ntp, ga, nwg, s->dview(), s->ovf,
+                           s->stream));
+    t.done();
+  }
+  return PSKV_OK;
+}
+
 // ------------------------------------------------------------- options
 // Every tuning knob and path selector of a shard, by name: pskv_set_option /
 // pskv_get_option, and the environment variable PSKV_<NAME> as the creation
@@ -1761,6 +1860,7 @@ const Option kOptions[] = {
     PSKV_OPT("UNROLL", 4, 8, tune_unroll, int),              // 4 or 8 (others: 8)
     PSKV_OPT("NT", 0, 1, tune_nt, bool),
     PSKV_OPT("NTP", 0, 1, tune_ntp, bool),
+    PSKV_OPT("FUSE", 0, 1, tune_fuse, bool),
     PSKV_OPT("EARLY", 0, 2, tune_early, int),
     PSKV_OPT("GET_NTP", 0, 1, tune_get_ntp, bool),
     PSKV_OPT("PAGEABLE_DMA", 0, 1, tune_pageable_dma, bool),
@@ -1913,8 +2013,10 @@ int pskv_shard_create_ex(int device, uint32_t key_begin, uint64_t key_end, int d
     return bail(fail(PSKV_ENOMEM, "dense parameter allocation failed"));
   if (hipMemsetAsync(s->dense, 0, s->range * (size_t)vb, s->stream) != hipSuccess)
     return bail(fail(PSKV_EHIP, "hipMemsetAsync failed"));
-  if (hipMalloc(&s->flag, 16) != hipSuccess) return bail(fail(PSKV_ENOMEM, "flag allocation failed"));
-  if (hipMemsetAsync(s->flag, 0, 16, s->stream) != hipSuccess)
+  // flag[0]: the sorted path's verification tag; flag[2..3]: K10's barrier
+  // counter (u64, monotonic)
+  if (hipMalloc(&s->flag, 64) != hipSuccess) return bail(fail(PSKV_ENOMEM, "flag allocation failed"));
+  if (hipMemsetAsync(s->flag, 0, 64, s->stream) != hipSuccess)
     return bail(fail(PSKV_EHIP, "hipMemsetAsync failed"));
   s->ocap = next_pow2(std::max<uint64_t>(overflow_slots ? overflow_slots : kDefaultOverflowSlots, 64));
   rc = alloc_overflow(&s->ovf, s->ocap, vb, s->stream);
@@ -2001,6 +2103,14 @@ int pskv_add_grouped(pskv_shard* s, const pskv_batch* batches, uint64_t nb, int 
   if (nb && !batches) return fail(PSKV_EINVAL, "pskv_add_grouped: null batches");
   if (bad_flags(flags)) return fail(PSKV_EINVAL, "pskv_add_grouped: unknown flags");
   return add_impl(s, std::vector<pskv_batch>(batches, batches + nb), flags);
+}
+
+int pskv_add_get_grouped(pskv_shard* s, const pskv_batch* adds, uint64_t na, const pskv_batch* gets, uint64_t ng,
+                         int flags) {
+  if (!s) return fail(PSKV_EINVAL, "pskv_add_get_grouped: null shard");
+  if ((na && !adds) || (ng && !gets)) return fail(PSKV_EINVAL, "pskv_add_get_grouped: null batches");
+  if (bad_flags(flags)) return fail(PSKV_EINVAL, "pskv_add_get_grouped: unknown flags");
+  return add_get_impl(s, std::vector<pskv_batch>(adds, adds + na), std::vector<pskv_batch>(gets, gets + ng), flags);
 }
 
 int pskv_get_grouped(pskv_shard* s, const pskv_batch* batches, uint64_t nb, int flags) {

@@ -147,6 +147,20 @@ class Shard:
             flags |= _lib.PSKV_HOST_FRAME
         check(lib.pskv_get_grouped(self._h, bs.arr, bs.n, flags))
 
+    def add_get_grouped(self, adds, gets, sorted_hint: bool = False):
+        """add_grouped(adds) then get_grouped(gets) in ONE call (pskv_add_get_grouped:
+        the BSP model's flush then the Gets it releases, or a worker round's push
+        then pull).  Device batches under the sorted hint run as one fused
+        launch (option FUSE).  adds / gets: batch lists or BatchSets."""
+        ba = adds if isinstance(adds, BatchSet) else self.prepare(adds)
+        bg = gets if isinstance(gets, BatchSet) else self.prepare(gets, is_get=True)
+        if (ba.flags ^ bg.flags) & _lib.PSKV_DEVICE and ba.n and bg.n:
+            raise ValueError("add_get_grouped: adds and gets must both be device or both host batches")
+        flags = ba.flags if ba.n else bg.flags
+        if sorted_hint and flags & _lib.PSKV_DEVICE:
+            flags |= _lib.PSKV_SORTED_HINT
+        check(lib.pskv_add_get_grouped(self._h, ba.arr, ba.n, bg.arr, bg.n, flags))
+
     def _batch_array(self, batches, is_get):
         arr = (_lib.PskvBatch * max(1, len(batches)))()
         keep = []

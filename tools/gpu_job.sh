@@ -3,6 +3,7 @@
 # first failure (gpurun runs it as: bash tools/gpu_job.sh OUTDIR STEP...).
 #   tests_focus  the parity tests of the dense / repair / golden / replay paths
 #   tests_all    pytest -m gpu (everything)
+#   tests_fused  the fused Add + Get tests, the bench-form and two-rank cfg-4 tests, options
 #   align        tools/align_probe.py (window phase cost)
 #   emu          bench.py as rank 0 of 8 and of 2 (one rank's cfg-4 share alone)
 #   emu8all      bench.py as each of the 8 ranks of N = 8 in turn (every rank's cfg-4 share alone)
@@ -30,7 +31,7 @@
 #   coldmicro    tools/micro/cold_stream: HBM ceilings of the dense step's access shapes, every byte cold
 #   coldbench    bench.py --cold-only (the headline step on a 1e9-key shard: roofline.cold's form)
 #   coldopts     the cold form under cache-policy options (GET_NTP, NTP, both, NT=0)
-#   ntp_ab       the headline (and its cold form) with K2g parameter stores cached / non-temporal, twice
+#   ntp_ab       the headline (and its cold form) with K2g parameter stores and K1 parameter loads cached / nt, twice
 #   emu_ntp      every rank of N = 8 emulated, K2g parameter stores cached / non-temporal
 #   smoke        __graft_entry__.smoke() (what the driver runs before the bench)
 #   shardsize    tools/shard_size_probe.py: K2g / K1 per key on 1e8 / 5e8 / 1e9-key shards (same windows)
@@ -53,6 +54,9 @@ for step in "$@"; do
     tests_focus) timeout -k 10 300 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread \
         "$R/tests/test_gpu_parity.py" "$R/tests/test_replay.py" \
         -k "phase or dense or lookalike or repaired or hint or golden or replay or options or dedup or zipf or radix or sentinel or random" > "$OUT/tests_focus.log" 2>&1 ;;
+    tests_fused) timeout -k 10 400 python3 -u -m pytest -x -v --timeout 200 --timeout-method thread \
+        "$R/tests/test_fused.py" "$R/tests/test_dist_gpu.py" "$R/tests/test_gpu_parity.py" \
+        -k "fused or cfg4 or headline or options or zipf_pulls" > "$OUT/tests_fused.log" 2>&1 ;;
     tests_all) timeout -k 10 900 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread "$R/tests" -m gpu \
         > "$OUT/tests_all.log" 2>&1 ;;
     align) timeout -k 10 200 python3 "$R/tools/align_probe.py" 0,1,2,3 20 > "$OUT/align.log" 2>&1 ;;
@@ -123,10 +127,10 @@ for step in "$@"; do
           tag=$(echo "x$o" | tr ' =' '__')
           env $o timeout -k 10 300 python3 "$R/bench.py" --cold-only --steps 50 > "$OUT/cold$tag.json" 2> "$OUT/cold$tag.err" || exit 1
         done ;;
-    ntp_ab) for r in 1 2; do for e in 0 1; do
-          PSKV_NTP=$e timeout -k 10 300 python3 "$R/bench.py" --steps 50 --no-zipf --no-extra --no-cpu-baseline \
-            > "$OUT/ntp${e}_$r.json" 2> "$OUT/ntp${e}_$r.err" || exit 1
-        done; done ;;
+    ntp_ab) for r in 1 2; do for e in 0 1; do for g in 0 1; do
+          PSKV_NTP=$e PSKV_GET_NTP=$g timeout -k 10 300 python3 "$R/bench.py" --steps 50 --no-zipf --no-extra \
+            --no-cpu-baseline > "$OUT/ntp${e}_getntp${g}_$r.json" 2> "$OUT/ntp${e}_getntp${g}_$r.err" || exit 1
+        done; done; done ;;
     emu_ntp) for r in 0 1 2 3 4 5 6 7; do for e in 0 1; do
           PSKV_NTP=$e PSKV_BENCH_EMULATE=$r/8 timeout -k 10 200 python3 "$R/bench.py" --steps 50 --no-zipf \
             --no-cpu-baseline --no-extra > "$OUT/emu8_${r}_ntp$e.json" 2> "$OUT/emu8_${r}_ntp$e.err" || exit 1
