@@ -519,10 +519,11 @@ def _cpu_model():
     return "unknown"
 
 
-def load_pmc(kernel_substr, config):
+def load_pmc(kernel_substr, config, name="pmc_latest.json"):
     """HBM traffic per dispatch from the committed rocprofv3 --pmc summary, if it
-    was collected on this same bench configuration."""
-    path = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    was collected on this same bench configuration (profiles/pmc_latest.json:
+    the headline; pmc_cold_latest.json: the cold form)."""
+    path = os.path.join(ROOT, "profiles", name)
     if not os.path.exists(path):
         return None, None
     with open(path) as f:
@@ -928,6 +929,9 @@ def cold_form(dev, J, B, R, steps, warmup, space, n_pulls):
     a, g = f.bytes(steps)
     del f, sets
     torch.cuda.empty_cache()
+    dom = max(kt.items(), key=lambda kv: kv[1]["avg_ms"] * kv[1]["launches"])
+    traffic, src = load_pmc(dom[0], {"n_gpus": 1, "batches": J, "batch_keys": B, "sets": R, "form": "cold",
+                                     "shard_keys": int(space)}, "pmc_cold_latest.json")
     return {"workload": f"the headline step on a {space:.3g}-key float shard ({space * 4 / 1e9:.0f} GB of parameters): "
                         f"{J} x {B} windows at 1M-aligned bases pushed, then free window slots pulled (as many as "
                         "cfg 2 pulls), zero push/pull overlap, a window recurring only every ~8 steps: every "
@@ -935,6 +939,9 @@ def cold_form(dev, J, B, R, steps, warmup, space, n_pulls):
             "shard_keys": int(space), "GB/s": res["GB/s"], "ms_per_step": res["ms_per_step"],
             "bytes_per_step": (a + g) / steps, "ms_per_step_evented": ev_s / steps * 1e3,
             "kernels": kernel_fracs(kt),
+            "kernel": dom[0], "frac": dom[1]["GB/s"] / HBM_PEAK_GBS, "traffic": traffic,
+            "traffic_over_algorithmic": traffic / dom[1]["algorithmic_bytes"] if traffic else None,
+            "traffic_source": src,
             "separate_launches": {"GB/s": sep["GB/s"], "ms_per_step": sep["ms_per_step"],
                                   "kernels": kernel_fracs(kt_sep)}}
 

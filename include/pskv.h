@@ -88,7 +88,9 @@ enum pskv_mode {
 #define PSKV_SORTED_HINT 0x2 /* caller believes keys are non-decreasing: take the sorted path.
                                 The kernel verifies the claim and repairs the result on the
                                 device if it was wrong, so a wrong hint costs time, never
-                                correctness. */
+                                correctness.  What it costs: the group is replayed in call
+                                order by ONE workgroup (K4r), ~1 GB/s of keys and values --
+                                64 M 4-byte keys take ~0.3 s -- on top of the sorted pass. */
 #define PSKV_HOST_FRAME 0x4  /* host keys/vals/out that lie in pskv_host_alloc frames are
                                 BORROWED until pskv_host_free: the call reads and writes them
                                 in place (no staging copy) and an Add returns once its work
@@ -200,15 +202,25 @@ int pskv_shard_info(pskv_shard* s, pskv_info* info);
 
 /* Tuning and path options of one shard, by name (DESIGN.md §5 lists them and
  * what each selects): GENERAL (0 = K4 stamps, 1 = auto, 2 = K5 always),
- * UNROLL, NT, NTP, EARLY (K2g early loads: 0 never, 1 always, 2 auto),
- * GET_DEDUP, GET_NTP, PAGEABLE_DMA, DMA_MIN_BYTES, DMA_MIN_BYTES_GET,
+ * UNROLL, NT, NTP, FUSE, EARLY (K2g early loads: 0 never, 1 always, 2 auto),
+ * GET_NTP, PAGEABLE_DMA, DMA_MIN_BYTES, DMA_MIN_BYTES_GET,
  * DMA_MIN_BYTES_PINNED, ZC_MAX_BYTES, FRAME_ZC_MAX_BYTES, INLINE,
  * INLINE_ADD_CHUNKS, INLINE_GET_CHUNKS, ISPIN, SERVE, SERVE_IDLE_US,
- * TILE_SHIFT, TILE_GRID, RB_WBITS, RB_NBD, RB_TB, RB_APPLY_LOG2, RB_BIN_BLOCK,
- * RB_INSERT.  The
- * environment variable PSKV_<NAME> sets a creation default.  Every option
- * changes speed only, never results.  PSKV_EINVAL for an unknown name or a
- * value out of range (the shard is unchanged). */
+ * TILE_SHIFT, TILE_GRID, RB_WBITS, RB_NBD, RB_TB, RB_APPLY_LOG2, RB_BIN_BLOCK.
+ * Every option changes speed only, never results.  Some apply only together
+ * with others (a value is accepted and echoed either way):
+ *   EARLY = 1     K2g with UNROLL 8 and NT 1 (otherwise the default loads)
+ *   GET_NTP = 1   K1 with UNROLL 8, NT 1, 4-byte values, 16-byte-aligned batches
+ *   FUSE = 1      pskv_add_get_grouped with device batches, PSKV_SORTED_HINT,
+ *                 4-byte values, assign mode, 16-byte-aligned batches, UNROLL 8
+ *                 and NT 1 (otherwise the separate Add and Get paths)
+ *   SERVE = 1     only while the device's hardware queues hold the server
+ *                 (DESIGN.md §8); INLINE_*_CHUNKS and ISPIN only on the K8 path
+ *   RB_* options  only on the K5 path (unhinted Adds)
+ * pskv_set_option returns PSKV_EINVAL for an unknown name or a value out of
+ * range (the shard is unchanged).  The environment variable PSKV_<NAME> sets a
+ * creation default; an invalid value there is reported on stderr and ignored
+ * (the built-in default stays; creation does not fail). */
 int pskv_set_option(pskv_shard* s, const char* name, int64_t value);
 int pskv_get_option(pskv_shard* s, const char* name, int64_t* value);
 

@@ -1049,8 +1049,17 @@ __global__ __launch_bounds__(kBlock) void k_add_get(GroupArgs ga, GroupArgs gg, 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < bar_target)
+    // bounded: a barrier that has not filled within ~1 s (100 MHz wall clock)
+    // is abandoned, and the group tagged -- K10r then replays the Add and
+    // answers the Get again, so the result is right either way
+    const unsigned long long t0 = wall_clock64();
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < bar_target) {
       __builtin_amdgcn_s_sleep(4);
+      if (wall_clock64() - t0 > 100000000ull) {
+        *flag = epoch;
+        break;
+      }
+    }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }

@@ -31,8 +31,8 @@ def per_dispatch(path, counter):
 
 
 def short(name):
-    for k in ("k_gather", "k_assign_group", "k_assign_sorted", "k_general_mark", "k_general_commit", "k_replay",
-              "k_rb_bin", "k_rb_resolve"):
+    for k in ("k_add_get", "k_replay_get", "k_gather", "k_assign_group", "k_assign_sorted", "k_general_mark",
+              "k_general_commit", "k_replay", "k_rb_bin", "k_rb_resolve"):
         if k in name:
             return k + name[name.index(k) + len(k):].split("(")[0]
     return None
@@ -42,7 +42,7 @@ def main():
     fetch_csv, write_csv, out = sys.argv[1:4]
     # the bench configuration profiled (bench.py uses the traffic only for the same one)
     config = json.loads(sys.argv[4]) if len(sys.argv) > 4 else {"n_gpus": 1, "batches": 64, "batch_keys": 1000000,
-                                                                "sets": 16, "form": "pull-next-set"}
+                                                                "sets": 16, "form": "pull-free-slots"}
     fe = per_dispatch(fetch_csv, "FETCH_SIZE")
     wr = per_dispatch(write_csv, "WRITE_SIZE")
     res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of bench.py; "

@@ -40,7 +40,8 @@
 #   bench        bench.py --steps 20 (the driver's command line)
 #   zipf         tools/zipf_probe.py kernel times on cfg 3
 #   zipf_bin     the same for K5a at 1024- and 512-thread workgroups
-#   profile      tools/gpu_profile.sh: rocprofv3 kernel trace + stats, FETCH / WRITE PMC passes
+#   profile      tools/gpu_profile.sh: rocprofv3 kernel trace + stats, FETCH / WRITE PMC passes (headline)
+#   profile_cold the same for the cold form (bench.py --cold-only)
 #   vector       bench.py --vector-only at 1e6 keys (config 1's VectorStorage restatement, CPU, once)
 #   asan         tools/asan_build.sh (host ASan + UBSan) and the C++ boundary programs under it
 set -o pipefail
@@ -145,6 +146,7 @@ for step in "$@"; do
     e2e) timeout -k 10 200 python3 "$R/tools/e2e_probe.py" > "$OUT/e2e.log" 2>&1 ;;
     bench) timeout -k 10 400 python3 "$R/bench.py" --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     profile) bash "$R/tools/gpu_profile.sh" "$(basename "$OUT")/prof" > "$OUT/profile.log" 2>&1 ;;
+    profile_cold) MODE=cold bash "$R/tools/gpu_profile.sh" "$(basename "$OUT")/prof_cold" > "$OUT/profile_cold.log" 2>&1 ;;
     zipf) timeout -k 10 300 python3 "$R/tools/zipf_probe.py" "" "PSKV_GET_DEDUP=1" > "$OUT/zipf.log" 2>&1 ;;
     zipf_bin) timeout -k 10 300 python3 "$R/tools/zipf_probe.py" "" "PSKV_RB_BIN_BLOCK=1024" "PSKV_RB_BIN_BLOCK=512" \
         > "$OUT/zipf_bin.log" 2>&1 ;;

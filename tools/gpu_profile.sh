@@ -8,7 +8,15 @@ export TMPDIR=/tmp
 OUT=$R/gpurun_out/${1:-prof}
 shift || true
 mkdir -p "$OUT"
-ARGS="--steps 20 --warmup 2 --no-cpu-baseline --no-extra --no-zipf $*"
+# MODE=cold: the cold form alone (bench.py --cold-only, roofline.cold);
+# otherwise the headline step alone (no cold form, Zipf or side measurements)
+if [ "${MODE:-headline}" = cold ]; then
+  ARGS="--steps 20 --warmup 2 --cold-only $*"
+  CONFIG='{"n_gpus": 1, "batches": 64, "batch_keys": 1000000, "sets": 16, "form": "cold", "shard_keys": 1000000000}'
+else
+  ARGS="--steps 20 --warmup 2 --no-cpu-baseline --no-extra --no-zipf --no-cold $*"
+  CONFIG='{"n_gpus": 1, "batches": 64, "batch_keys": 1000000, "sets": 16, "form": "pull-free-slots"}'
+fi
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT" -o trace -- \
   python3 "$R/bench.py" $ARGS > "$OUT/trace.log" 2>&1 || exit 1
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT" -o fetch -- \
@@ -16,5 +24,5 @@ timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT" -o fe
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT" -o write -- \
   python3 "$R/bench.py" $ARGS > "$OUT/write.log" 2>&1 || exit 3
 python3 "$R/tools/collect_pmc.py" "$OUT/fetch_counter_collection.csv" \
-  "$OUT/write_counter_collection.csv" "$OUT/pmc.json" > /dev/null || exit 4
+  "$OUT/write_counter_collection.csv" "$OUT/pmc.json" "$CONFIG" > /dev/null || exit 4
 echo "profile done: $OUT"
