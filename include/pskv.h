@@ -203,14 +203,13 @@ int pskv_shard_info(pskv_shard* s, pskv_info* info);
 /* Tuning and path options of one shard, by name (DESIGN.md §5 lists them and
  * what each selects): GENERAL (0 = K4 stamps, 1 = auto, 2 = K5 always),
  * UNROLL, NT, NTP, FUSE, EARLY (K2g early loads: 0 never, 1 always, 2 auto),
- * GET_NTP, PAGEABLE_DMA, DMA_MIN_BYTES, DMA_MIN_BYTES_GET,
+ * PAGEABLE_DMA, DMA_MIN_BYTES, DMA_MIN_BYTES_GET,
  * DMA_MIN_BYTES_PINNED, ZC_MAX_BYTES, FRAME_ZC_MAX_BYTES, INLINE,
  * INLINE_ADD_CHUNKS, INLINE_GET_CHUNKS, ISPIN, SERVE, SERVE_IDLE_US,
  * TILE_SHIFT, TILE_GRID, RB_WBITS, RB_NBD, RB_TB, RB_APPLY_LOG2, RB_BIN_BLOCK.
  * Every option changes speed only, never results.  Some apply only together
  * with others (a value is accepted and echoed either way):
  *   EARLY = 1     K2g with UNROLL 8 and NT 1 (otherwise the default loads)
- *   GET_NTP = 1   K1 with UNROLL 8, NT 1, 4-byte values, 16-byte-aligned batches
  *   FUSE = 1      pskv_add_get_grouped with device batches, PSKV_SORTED_HINT,
  *                 4-byte values, assign mode, 16-byte-aligned batches, UNROLL 8
  *                 and NT 1 (otherwise the separate Add and Get paths)

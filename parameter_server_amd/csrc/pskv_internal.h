@@ -112,8 +112,7 @@ struct Ovf {
 // pointers 16-byte aligned so 16 B vector accesses are legal.
 // unroll: 4 or 8 groups of 4 keys per lane (chunk = 256*4*unroll keys);
 // nt: non-temporal loads/stores of the streamed push/pull buffers.
-// ntp: non-temporal parameter loads (option GET_NTP; 4-byte values, unroll 8, nt)
-hipError_t launch_gather(int vb, bool vec, int unroll, bool nt, bool ntp, const GroupArgs& ga,
+hipError_t launch_gather(int vb, bool vec, int unroll, bool nt, const GroupArgs& ga,
                          uint32_t nwg, const DenseView& d, const Ovf& o, hipStream_t st);
 hipError_t launch_assign_sorted(int vb, bool vec, const uint32_t* keys, const void* vals,
                                 uint64_t n, const DenseView& d, uint32_t* flag, uint32_t epoch,

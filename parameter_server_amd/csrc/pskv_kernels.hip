@@ -271,7 +271,7 @@ __device__ __forceinline__ void gather2(const DenseView& d, const Ovf& o, const 
   }
 }
 
-template <typename VT, bool VEC, int U, bool NT, bool NTP = false>
+template <typename VT, bool VEC, int U, bool NT>
 __global__ __launch_bounds__(kBlock) void k_gather(GroupArgs ga, DenseView d, Ovf o) {
   constexpr int CH = kBlock * 4 * U;
   const uint32_t wg = blockIdx.x;
@@ -306,7 +306,7 @@ __global__ __launch_bounds__(kBlock) void k_gather(GroupArgs ga, DenseView d, Ov
       Vec4<uint32_t>::load<NT>(keys + base + (uint64_t)(u * kBlock + tid) * 4, k[u]);
     VT v[U][4];
 #pragma unroll
-    for (int u = 0; u < U; ++u) gather4<VT, NTP>(d, o, k[u], v[u]);
+    for (int u = 0; u < U; ++u) gather4<VT>(d, o, k[u], v[u]);
 #pragma unroll
     for (int u = 0; u < U; ++u)
       Vec4<VT>::template store<NT>(out + base + (uint64_t)(u * kBlock + tid) * 4, v[u]);
@@ -2660,13 +2660,11 @@ static void gather_dispatch(int unroll, bool nt, uint32_t nwg, const GroupArgs& 
   }
 }
 
-hipError_t launch_gather(int vb, bool vec, int unroll, bool nt, bool ntp, const GroupArgs& ga,
+hipError_t launch_gather(int vb, bool vec, int unroll, bool nt, const GroupArgs& ga,
                          uint32_t nwg, const DenseView& d, const Ovf& o, hipStream_t st) {
   if (nwg == 0) return hipSuccess;
   if (vb == 4) {
-    if (vec && ntp && unroll == 8 && nt)  // option GET_NTP: non-temporal parameter loads
-      k_gather<uint32_t, true, 8, true, true><<<nwg, kBlock, 0, st>>>(ga, d, o);
-    else if (vec)
+    if (vec)
       gather_dispatch<uint32_t, true>(unroll, nt, nwg, ga, d, o, st);
     else
       gather_dispatch<uint32_t, false>(unroll, nt, nwg, ga, d, o, st);

@@ -258,13 +258,17 @@ struct pskv_shard {
   uint32_t tune_tile_grid = 4096;
   int tune_unroll = 8;   // PSKV_UNROLL: 4 or 8 (8: measured +5 % on the dense Add)
   bool tune_nt = true;   // PSKV_NT: non-temporal streams (measured +12-15 % on K1 / K2g)
-  bool tune_ntp = false; // PSKV_NTP: non-temporal parameter stores (dense Add)
+  // PSKV_NTP: non-temporal parameter stores in the dense Add (K2g, K10).  On
+  // since round 4: cached stores leave the Add's parameter lines dirty in the
+  // Infinity Cache, and the next Get pays their write-back; the headline step
+  // 5.74-5.86 -> 6.11-6.22 TB/s, its Get (K1) 114-116 -> 91 us
+  // (profiles/r04_probes/ntp_ab/)
+  bool tune_ntp = true;
   // PSKV_FUSE: pskv_add_get_grouped runs its last Add group and first Get group
   // as ONE launch (K10) where it can (1), or as the separate calls (0)
   bool tune_fuse = true;
   int fuse_grid_max = 0;          // K10's co-resident grid (occupancy query, at first use)
   unsigned long long bar_count = 0;  // K10's barrier counter: every launch adds its grid
-  bool tune_get_ntp = false;  // PSKV_GET_NTP: non-temporal parameter loads in K1 (4-byte values, 16-byte aligned runs)
   int tune_early = 2;    // PSKV_EARLY: K2g early loads (0 never, 1 always, 2 when the group's keys cover < 1/4 of the range)
   // PSKV_PAGEABLE_DMA: DMA pageable host buffers directly (the runtime moves
   // them at the PCIe rate, measured 55 GB/s) instead of copying them into
@@ -1498,7 +1502,7 @@ int zero_copy_get_views(pskv_shard* s, const std::vector<pskv_batch>& hv) {
     uint64_t elems = 0;
     for (size_t i = g.first; i < g.second; ++i) elems += hv[i].n;
     LaunchTimer t(s, PSKV_K_GATHER, elems);
-    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, s->tune_get_ntp, ga, nwg, s->dview(), s->ovf, s->stream));
+    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, ga, nwg, s->dview(), s->ovf, s->stream));
     t.done();
   }
   PSKV_HIP(hipStreamSynchronize(s->stream));
@@ -1529,7 +1533,7 @@ int zero_copy_get(pskv_shard* s, const std::vector<pskv_batch>& v, bool vec) {
     uint64_t elems = 0;
     for (size_t i = g.first; i < g.second; ++i) elems += hv[i].n;
     LaunchTimer t(s, PSKV_K_GATHER, elems);
-    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, s->tune_get_ntp, ga, nwg, s->dview(), s->ovf, s->stream));
+    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, ga, nwg, s->dview(), s->ovf, s->stream));
     t.done();
   }
   PSKV_HIP(hipStreamSynchronize(s->stream));
@@ -1594,7 +1598,7 @@ int pinned_get(pskv_shard* s, const std::vector<pskv_batch>& v) {
     uint64_t elems = 0;
     for (size_t i = b; i < e; ++i) elems += dv[i].n;
     LaunchTimer t(s, PSKV_K_GATHER, elems);
-    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, s->tune_get_ntp, ga, nwg, s->dview(),
+    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, ga, nwg, s->dview(),
                            s->ovf, s->stream));
     t.done();
     PSKV_HIP(hipEventRecord(s->out_events[w], s->stream));
@@ -1688,7 +1692,7 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
     uint64_t elems = 0;
     for (size_t i = g.first; i < g.second; ++i) elems += dv[i].n;
     LaunchTimer t(s, PSKV_K_GATHER, elems);
-    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, s->tune_get_ntp, ga, nwg, s->dview(), s->ovf,
+    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, ga, nwg, s->dview(), s->ovf,
                            s->stream));
     t.done();
   }
@@ -1828,7 +1832,7 @@ int add_get_impl(pskv_shard* s, const std::vector<pskv_batch>& adds, const std::
     uint64_t elems = 0;
     for (size_t k = gg[i].first; k < gg[i].second; ++k) elems += vg[k].n;
     LaunchTimer t(s, PSKV_K_GATHER, elems);
-    PSKV_HIP(launch_gather(s->vb, true, gather_unroll(s), s->tune_nt, s->tune_get_ntp, ga, nwg, s->dview(), s->ovf,
+    PSKV_HIP(launch_gather(s->vb, true, gather_unroll(s), s->tune_nt, ga, nwg, s->dview(), s->ovf,
                            s->stream));
     t.done();
   }
@@ -1862,7 +1866,6 @@ const Option kOptions[] = {
     PSKV_OPT("NTP", 0, 1, tune_ntp, bool),
     PSKV_OPT("FUSE", 0, 1, tune_fuse, bool),
     PSKV_OPT("EARLY", 0, 2, tune_early, int),
-    PSKV_OPT("GET_NTP", 0, 1, tune_get_ntp, bool),
     PSKV_OPT("PAGEABLE_DMA", 0, 1, tune_pageable_dma, bool),
     PSKV_OPT("DMA_MIN_BYTES", 0, INT64_MAX, tune_dma_min_bytes, size_t),
     PSKV_OPT("DMA_MIN_BYTES_GET", 0, INT64_MAX, tune_dma_min_bytes_get, size_t),

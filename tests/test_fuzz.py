@@ -35,8 +35,8 @@ N_GROUPS = int(os.environ.get("FUZZ_GROUPS", "4"))  # concurrent groups of 6 sha
 # kernel paths; each scenario takes one
 KNOBS = [{}, {}, {}, {"SERVE": 1}, {"GENERAL": "stamps"}, {"INLINE": 0},
          {"UNROLL": 4}, {"PAGEABLE_DMA": 1}, {"ZC_MAX_BYTES": 0},
-         {"RB_APPLY_LOG2": 13}, {"RB_BIN_BLOCK": 512}, {"EARLY": 1}, {"EARLY": 0}, {"GET_NTP": 1},
-         {"NTP": 1}]
+         {"RB_APPLY_LOG2": 13}, {"RB_BIN_BLOCK": 512}, {"EARLY": 1}, {"EARLY": 0}, {"NTP": 0},
+         {"FUSE": 0}]
 SIZES = [0, 1, 5, 100, 256, 257, 1024, 2049, 5000, 40_000, 300_000]
 U32 = 1 << 32
 
@@ -186,9 +186,9 @@ def _run(cuda, oracle_mod, seed, rng, dt, mode, kb, ke, knobs):
 
     with ps.Shard(kb, ke, dt, mode=mode, overflow_slots=1 << 14, options=knobs) as sh:
         for step in range(N_STEPS):
-            op = rng.choice(["add", "add", "add_dev", "add_grouped", "add_grouped_dev",
+            op = rng.choice(["add", "add", "add_dev", "add_grouped", "add_grouped_dev", "add_get_dev",
                              "get", "get_dev", "get_grouped", "clear"],
-                            p=[.16, .08, .16, .12, .12, .12, .1, .1, .04])
+                            p=[.15, .07, .15, .11, .11, .08, .11, .09, .09, .04])
             kind = str(rng.choice(kinds))
             if op == "clear":
                 sh.clear()
@@ -226,6 +226,37 @@ def _run(cuda, oracle_mod, seed, rng, dt, mode, kb, ke, knobs):
                     sh.sync()
                 for k, v in batches:
                     ref.add(k, v)
+            elif op == "add_get_dev":
+                # pskv_add_get_grouped: the fused launch (K10) for hinted
+                # 4-byte windows, the separate paths otherwise; the pulls see
+                # the pushes of the same call
+                nb = int(rng.choice([1, 5, 64, 67]))
+                dense = kind in ("dense", "lookalike")
+                adds = []
+                for _ in range(nb):
+                    n = int(rng.choice([0, 1, 1000, 8192, 30_000] if dense else [0, 1, 33, 8192, 20_001]))
+                    k = _keys(rng, kb, ke, n, kind if dense else str(rng.choice(kinds)))
+                    adds.append((k, _vals(rng, dt, k.size)))
+                qs = []
+                for _ in range(int(rng.choice([1, 3, 64, 66]))):
+                    if adds and rng.random() < 0.4:  # a pull of pushed keys (maybe a slice of a window)
+                        k = adds[int(rng.integers(0, len(adds)))][0]
+                        a = int(rng.integers(0, k.size + 1))
+                        qs.append(k[a:a + int(rng.integers(0, 9000))].copy())
+                    else:
+                        qs.append(_keys(rng, kb, ke, int(rng.choice([0, 1, 300, 5000, 8192])), str(rng.choice(kinds))))
+                dev_a = [(tdev(k, cuda), tdev(v, cuda)) for k, v in adds]
+                dev_q = [tdev(q, cuda) for q in qs]
+                tdt = {np.dtype(np.int32): torch.int32, np.dtype(np.float32): torch.float32,
+                       np.dtype(np.float64): torch.float64}[np.dtype(dt)]
+                outs = [torch.empty(q.size, dtype=tdt, device=cuda) for q in qs]
+                keep += [t for kv in dev_a for t in kv] + dev_q + outs
+                sh.add_get_grouped(dev_a, list(zip(dev_q, outs)), sorted_hint=bool(rng.random() < 0.8))
+                for k, v in adds:
+                    ref.add(k, v)
+                for q, o in zip(qs, outs):
+                    check(q, o.cpu().numpy(), step)
+                sh.sync()
             elif op == "get":
                 q = _keys(rng, kb, ke, int(rng.choice(SIZES)), kind)
                 check(q, sh.get(q), step)

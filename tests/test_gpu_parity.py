@@ -462,14 +462,15 @@ def test_zipf_batches_parity(cuda, oracle_mod):
     assert_bits_equal(got, dense, "zipf")
 
 
-@pytest.mark.parametrize("get_ntp", [0, 1])
-def test_zipf_pulls(cuda, oracle_mod, get_ntp):
+@pytest.mark.parametrize("ntp", [0, 1])
+def test_zipf_pulls(cuda, oracle_mod, ntp):
     """K1 on Zipf pulls (hot keys repeated hundreds of times per chunk),
     out-of-range keys, the sentinel 0xFFFFFFFF, never-written keys, and chunks
     that mix dense runs at every phase with scattered keys — bit-exact against
-    the oracle, with cached and non-temporal (option GET_NTP) parameter loads.
-    (Round 3's pull-key dedup variant, GET_DEDUP, measured no gain and was
-    removed in round 4.)"""
+    the oracle, the parameters written by sorted windows with cached and with
+    non-temporal (option NTP) stores.  (Round 3's pull-key dedup variant,
+    GET_DEDUP, measured no gain, and its non-temporal parameter loads, GET_NTP,
+    lost to NTP; both were removed in round 4.)"""
     import torch
 
     import parameter_server_amd as ps
@@ -478,7 +479,7 @@ def test_zipf_pulls(cuda, oracle_mod, get_ntp):
     space = 2_000_000
     zb = workload.zipf_batches(3, space, batch=300_000, device=cuda)
     ref = oracle_mod.MapStorageRef(np.float32)
-    with ps.Shard(0, space, np.float32, overflow_slots=1 << 12, options={"GET_NTP": get_ntp}) as sh:
+    with ps.Shard(0, space, np.float32, overflow_slots=1 << 12, options={"NTP": ntp}) as sh:
         for k, v in zb:
             sh.add(k, v)
             ref.add(k.cpu().numpy().view(np.uint32), v.cpu().numpy())
@@ -486,6 +487,12 @@ def test_zipf_pulls(cuda, oracle_mod, get_ntp):
         xv = np.arange(4, dtype=np.float32) + 0.5
         sh.add(extra, xv)
         ref.add(extra, xv)
+        # windows through the sorted device path (K2g: stores cached or nt)
+        wins = [np.arange(b, b + 20_000, dtype=np.uint32) for b in (7001, 9003, 40_000, 1_000_001)]
+        wv = [np.random.default_rng(int(w[0])).standard_normal(w.size).astype(np.float32) for w in wins]
+        sh.add_grouped([(tdev(w, cuda), tdev(v, cuda)) for w, v in zip(wins, wv)], sorted_hint=True)
+        for w, v in zip(wins, wv):
+            ref.add(w, v)
         q = zb[0][0].cpu().numpy().view(np.uint32).copy()
         q[1000:1000 + 64] = np.arange(5000, 5064, dtype=np.uint32)       # dense runs inside scattered chunks
         q[4096:4096 + 8192] = np.arange(7001, 7001 + 8192, dtype=np.uint32)  # a whole chunk run, phase 1
@@ -498,8 +505,8 @@ def test_zipf_pulls(cuda, oracle_mod, get_ntp):
         parts = [tdev(q[:q.size // 2], cuda), tdev(q[q.size // 2:], cuda)]
         sh.get_grouped(list(zip(parts, outs)))
         got = torch.cat(outs).cpu().numpy()
-        assert sh.get_option("GET_NTP") == get_ntp
-    assert_bits_equal(got, ref.get(q), f"zipf pulls, GET_NTP {get_ntp}")
+        assert sh.get_option("NTP") == ntp
+    assert_bits_equal(got, ref.get(q), f"zipf pulls, NTP {ntp}")
 
 
 @pytest.mark.parametrize("mode", ["assign", "accumulate"])
@@ -1465,7 +1472,7 @@ def test_shard_options_api(cuda, monkeypatch, capfd):
     import parameter_server_amd as ps
     from parameter_server_amd import PskvError, _lib
 
-    names = ["GENERAL", "UNROLL", "NT", "NTP", "EARLY", "GET_NTP", "PAGEABLE_DMA", "DMA_MIN_BYTES", "DMA_MIN_BYTES_GET",
+    names = ["GENERAL", "UNROLL", "NT", "NTP", "FUSE", "EARLY", "PAGEABLE_DMA", "DMA_MIN_BYTES", "DMA_MIN_BYTES_GET",
              "DMA_MIN_BYTES_PINNED", "ZC_MAX_BYTES", "FRAME_ZC_MAX_BYTES", "INLINE", "INLINE_ADD_CHUNKS",
              "INLINE_GET_CHUNKS", "ISPIN", "SERVE", "SERVE_IDLE_US", "TILE_SHIFT", "TILE_GRID", "RB_WBITS",
              "RB_NBD", "RB_TB", "RB_APPLY_LOG2", "RB_BIN_BLOCK"]
@@ -1479,7 +1486,7 @@ def test_shard_options_api(cuda, monkeypatch, capfd):
         sh.set_option("ZC_MAX_BYTES", 12345)
         assert sh.get_option("ZC_MAX_BYTES") == 12345
         for n, bad in (("UNROLL", 5), ("RB_APPLY_LOG2", 12), ("TILE_SHIFT", 3), ("INLINE", 2),
-                        ("RB_BIN_BLOCK", 768), ("NOPE", 1), ("GET_DEDUP", 1), ("RB_INSERT", 1)):
+                        ("RB_BIN_BLOCK", 768), ("NOPE", 1), ("GET_DEDUP", 1), ("RB_INSERT", 1), ("GET_NTP", 1)):
             before = sh.get_option(n) if n in names else None
             with pytest.raises(PskvError) as ei:
                 sh.set_option(n, bad)

@@ -33,6 +33,7 @@
 #   coldopts     the cold form under cache-policy options (GET_NTP, NTP, both, NT=0)
 #   ntp_ab       the headline (and its cold form) with K2g parameter stores and K1 parameter loads cached / nt, twice
 #   emu_ntp      every rank of N = 8 emulated, K2g parameter stores cached / non-temporal
+#   emu8_fuse    every rank of N = 8 emulated with the fused Add + Get launch on / off
 #   smoke        __graft_entry__.smoke() (what the driver runs before the bench)
 #   shardsize    tools/shard_size_probe.py: K2g / K1 per key on 1e8 / 5e8 / 1e9-key shards (same windows)
 #   getntp       tools/shard_size_probe.py with K1 parameter loads cached / non-temporal (GET_NTP=0/1), twice
@@ -135,6 +136,10 @@ for step in "$@"; do
     emu_ntp) for r in 0 1 2 3 4 5 6 7; do for e in 0 1; do
           PSKV_NTP=$e PSKV_BENCH_EMULATE=$r/8 timeout -k 10 200 python3 "$R/bench.py" --steps 50 --no-zipf \
             --no-cpu-baseline --no-extra > "$OUT/emu8_${r}_ntp$e.json" 2> "$OUT/emu8_${r}_ntp$e.err" || exit 1
+        done; done ;;
+    emu8_fuse) for r in 0 1 2 3 4 5 6 7; do for f in 1 0; do
+          PSKV_FUSE=$f PSKV_BENCH_EMULATE=$r/8 timeout -k 10 200 python3 "$R/bench.py" --steps 50 --no-zipf \
+            --no-cpu-baseline --no-extra > "$OUT/emu8_${r}_fuse$f.json" 2> "$OUT/emu8_${r}_fuse$f.err" || exit 1
         done; done ;;
     smoke) timeout -k 10 300 python3 -c "import sys; sys.path.insert(0, '$R'); import __graft_entry__ as g; g.smoke()" \
         > "$OUT/smoke.log" 2>&1 ;;
