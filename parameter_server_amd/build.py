@@ -45,8 +45,12 @@ def build_lib(force=False):
     srcs = [os.path.join(CSRC, s) for s in LIB_SOURCES]
     deps = srcs + [os.path.join(CSRC, h) for h in ("pskv_internal.h", "pskv_frames.h", "pskv_queues.h")] + [os.path.join(INCLUDE, "pskv.h")]
     if force or _stale(LIB_OUT, deps):
+        # built beside, then renamed over: a reader (a test, a GPU-box upload)
+        # never sees a half-written library
+        tmp = LIB_OUT + ".tmp"
         _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-              "-I", INCLUDE, "-I", CSRC, *srcs, "-o", LIB_OUT])
+              "-I", INCLUDE, "-I", CSRC, *srcs, "-o", tmp])
+        os.replace(tmp, LIB_OUT)
     return LIB_OUT
 
 
