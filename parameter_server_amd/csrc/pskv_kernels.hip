@@ -1030,13 +1030,20 @@ __global__ __launch_bounds__(kBlock) void k_add_get(GroupArgs ga, GroupArgs gg, 
   const uint32_t nget = gg.wg_prefix[gg.nb];
   bool bad = false;
   if (s_dense) {
+    // one list of work units, the Add's chunks then the Get's, dealt
+    // round-robin: no unit waits for another, so a workgroup that ran out of
+    // Add chunks takes Get chunks at once and a small launch (a rank's share)
+    // ends on the slowest unit, not on the slowest workgroup's Add tail
     const uint32_t nadd = ga.wg_prefix[ga.nb];
     uint32_t ek[U][4], ev[U][4];
-    for (uint32_t c = wg; c < nadd; c += nwg)
-      bad |= dense_chunk_own<U, NT, NTP, false>(ga, d, c, s_first, s_last, ek, ev);
-    if (bad) *flag = epoch;
     if (tid == 0) __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (uint32_t c = wg; c < nget; c += nwg) fused_get_chunk<U, NT>(gg, ga, d, o, c, s_first, s_last, true);
+    for (uint32_t c = wg; c < nadd + nget; c += nwg) {
+      if (c < nadd)
+        bad |= dense_chunk_own<U, NT, NTP, false>(ga, d, c, s_first, s_last, ek, ev);
+      else
+        fused_get_chunk<U, NT>(gg, ga, d, o, c - nadd, s_first, s_last, true);
+    }
+    if (bad) *flag = epoch;
     return;
   }
   bad = tile_mode<uint32_t, true>(ga, d, g, tile_shift, ntiles, wg, nwg, s_seg_s, s_seg_e, &s_mask);
@@ -2821,9 +2828,12 @@ hipError_t launch_add_get(bool ntp, const GroupArgs& ga, const GroupArgs& gg, co
 }
 
 int add_get_max_grid() {
-  // co-resident workgroups of the fused launch: the occupancy query per CU,
-  // one workgroup per CU to spare (the query can be one high,
-  // MI355X_MICROARCH.md "Residency"), times the CUs
+  // co-resident workgroups of the fused launch: the occupancy query per CU
+  // times the CUs.  At k_add_get's register counts (102 VGPRs: 4 waves per
+  // SIMD; 104 SGPRs) the query is exact (MI355X_MICROARCH.md "Residency": the
+  // SGPR-based hardware limit is 6 workgroups per CU, above the 4 the VGPRs
+  // allow); should other work hold part of the device, the tile mode's
+  // barrier is bounded (k_add_get) and the replay repairs the group
   int dev = 0, cus = 0, per = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
@@ -2833,7 +2843,7 @@ int add_get_max_grid() {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per2, k_add_get<8, true, true>, kBlock, 0) != hipSuccess)
     return 0;
   per = per < per2 ? per : per2;
-  return per > 1 ? (per - 1) * cus : cus;
+  return (per > 0 ? per : 1) * cus;
 }
 
 hipError_t launch_replay_get(const GroupArgs& ga, const GroupArgs& gg, const DenseView& d, const Ovf& o,

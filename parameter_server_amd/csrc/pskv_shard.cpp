@@ -1808,7 +1808,9 @@ int add_get_impl(pskv_shard* s, const std::vector<pskv_batch>& adds, const std::
     while (shift > 12 && (add_elems >> shift) < 2048) --shift;
     if (s->tune_tile_shift) shift = s->tune_tile_shift;
     const uint64_t ntiles = (s->range + (1ull << shift) - 1) >> shift;
-    const uint64_t want = std::max<uint64_t>({(uint64_t)nadd, (uint64_t)nget, std::min<uint64_t>(ntiles, 1024)});
+    // dense mode deals nadd + nget work units over the grid; the tile mode's
+    // grid-stride over the tiles wants at least 1024 workgroups
+    const uint64_t want = std::max<uint64_t>((uint64_t)nadd + nget, std::min<uint64_t>(ntiles, 1024));
     const uint32_t grid = (uint32_t)std::min<uint64_t>(want, (uint64_t)s->fuse_grid_max);
     s->bar_count += grid;
     unsigned long long* bar = reinterpret_cast<unsigned long long*>(s->flag + 2);
