@@ -265,8 +265,14 @@ struct pskv_shard {
   // (profiles/r04_probes/ntp_ab/)
   bool tune_ntp = true;
   // PSKV_FUSE: pskv_add_get_grouped runs its last Add group and first Get group
-  // as ONE launch (K10) where it can (1), or as the separate calls (0)
-  bool tune_fuse = true;
+  // as ONE launch (K10) where it can (1), or as the separate calls (0).  Off:
+  // measured slower than the separate K2g + K1 launches at every size
+  // (headline 5.98 vs 6.11 TB/s, cold 5.72 vs 5.93, emulated N = 8 ranks
+  // 37.7-43.0 vs 33.7-41.5 us; profiles/r04_probes/emu8_fuse/): one register
+  // allocation for both halves holds the Get at 4 waves per SIMD where K1
+  // runs 8, and a rank's step spends its fixed cost inside each kernel's
+  // ramp, not between the launches
+  bool tune_fuse = false;
   int fuse_grid_max = 0;          // K10's co-resident grid (occupancy query, at first use)
   unsigned long long bar_count = 0;  // K10's barrier counter: every launch adds its grid
   int tune_early = 2;    // PSKV_EARLY: K2g early loads (0 never, 1 always, 2 when the group's keys cover < 1/4 of the range)
