@@ -947,6 +947,14 @@ def cold_form(dev, J, B, R, steps, warmup, space, n_pulls):
                              "kernels": kernel_fracs(kt_fused)}}
 
 
+_T0 = time.perf_counter()
+
+
+def progress(what):
+    """One line per phase on stderr (a long run shows where it is)."""
+    print(f"bench [{time.perf_counter() - _T0:7.1f} s] {what}", file=sys.stderr, flush=True)
+
+
 def main(argv=None):
     args = parse(argv)
     if args.vector_only:
@@ -982,6 +990,7 @@ def main(argv=None):
     assert all(overlap_keys(s) == 0 for s in sets), "a pull set overlaps its push set"
     n_pulls = [len(s["pull"]) for s in sets]
     if args.cold_only:
+        progress("cold form only")
         del sets
         rec = cold_form(dev, J, B, R, args.steps, args.warmup, int(args.cold_keys), n_pulls)
         json_out.write(json.dumps({"cold": rec}) + "\n")
@@ -994,7 +1003,9 @@ def main(argv=None):
     form = Form(shard, sets, dev)
     # correctness guard on the benchmarked state: one rotation from a cleared
     # shard, every pull against a model of the shard
+    progress("headline: self-check")
     form.self_check(lo, hi, dev)
+    progress("headline: timed steps")
     head = run_form(form, args.steps, max(args.warmup, R), world, dev)
     ktimes, evented_s = evented(form, args.steps, world, dev)
     # the same step as ONE fused launch (K10, FUSE = 1): measured beside
@@ -1012,10 +1023,12 @@ def main(argv=None):
 
     zipf_res = None
     if not args.no_zipf:
+        progress("cfg 3 (Zipf)")
         zipf_res, zb = zipf_sparse(prank, world, dev, lo, hi, B, args.steps)
     cold = None
     if pworld == 1 and not args.no_cold:
         shard.set_stream(None)  # the cold shard takes the stream meanwhile
+        progress("cold form")
         cold = cold_form(dev, J, B, R, args.steps, args.warmup, int(args.cold_keys), n_pulls)
         shard.set_stream(stream.cuda_stream)
 
@@ -1109,12 +1122,14 @@ def main(argv=None):
     shard.close()
     if rank == 0 and pworld == 1 and not args.no_cpu_baseline:
         sizes = [int(x) for x in args.vector_sizes.split(",") if x]
+        progress("cpu baseline")
         result["cpu_baseline"] = cpu_baseline([f for _, f, _ in sets[0]["slices"]], B, args.cpu_batches, sizes)
         if zipf_res is not None:  # cfg 3's own CPU baseline: the same Zipf batches
             result["cpu_baseline"]["zipf"] = _zipf_cpu_sample(zb[:2], B)
     if zipf_res is not None:
         del zb
     if pworld == 1 and not args.no_extra:
+        progress("side measurements")
         extra["dense_f64_step"] = variant_f64(rank, world, J, B, dev, R, args.steps, lo, hi)
         extra["dense_accumulate_step"] = variant_accumulate(rank, world, J, B, dev, sets, args.steps, lo, hi)
         extra.update(side_measurements(dev, B))

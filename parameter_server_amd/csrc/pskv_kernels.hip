@@ -976,12 +976,22 @@ __device__ __forceinline__ void fused_get_chunk(const GroupArgs& gg, const Group
     if (m == 0) {  // no push window meets this wave's keys (the usual case)
 #pragma unroll
       for (int u = 0; u < U; ++u) gather4<uint32_t>(d, o, k[u], v[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) Vec4<uint32_t>::store<NT>(out + base + (uint64_t)(u * kBlock + tid) * 4, v[u]);
     } else {
-#pragma unroll
-      for (int u = 0; u < U; ++u) fused_group4(ga, d, o, k[u], v[u], m, s_first, s_last);
+      // pull keys that push windows of this launch may cover: one group at a
+      // time, its keys read again (L2-warm) and its values stored at once, so
+      // nothing of the other groups stays live (with every group's keys and
+      // values held across this path the kernel took ~160-200 VGPRs, 2 waves
+      // per SIMD, against 102)
+#pragma unroll 1
+      for (int u = 0; u < U; ++u) {
+        uint32_t kk[4], vv[4];
+        Vec4<uint32_t>::load<false>(keys + base + (uint64_t)(u * kBlock + tid) * 4, kk);
+        fused_group4(ga, d, o, kk, vv, m, s_first, s_last);
+        Vec4<uint32_t>::store<NT>(out + base + (uint64_t)(u * kBlock + tid) * 4, vv);
+      }
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) Vec4<uint32_t>::store<NT>(out + base + (uint64_t)(u * kBlock + tid) * 4, v[u]);
   } else {
     // a partial chunk (the last of a batch): eight keys per lane at a time
     const uint64_t end = n < base + CH ? n : base + CH;
@@ -1012,7 +1022,10 @@ __device__ __forceinline__ void fused_get_chunk(const GroupArgs& gg, const Group
   }
 }
 
-template <int U, bool NT, bool NTP>
+// UA: keys per lane group count of the Add's chunks (4: 4 Ki-key chunks, ~60
+// VGPRs, so the launch keeps 8 waves per SIMD for its Get units too; 8: K2g's
+// 8 Ki-key chunks at 102 VGPRs, 4 waves per SIMD).  UG: the Get's, 8.
+template <int UA, int UG, bool NT, bool NTP>
 __global__ __launch_bounds__(kBlock) void k_add_get(GroupArgs ga, GroupArgs gg, DenseView d, Ovf o,
                                                     uint32_t tile_shift, uint64_t ntiles, uint32_t* flag,
                                                     uint32_t epoch, unsigned long long* bar,
@@ -1034,15 +1047,14 @@ __global__ __launch_bounds__(kBlock) void k_add_get(GroupArgs ga, GroupArgs gg, 
     // round-robin: no unit waits for another, so a workgroup that ran out of
     // Add chunks takes Get chunks at once and a small launch (a rank's share)
     // ends on the slowest unit, not on the slowest workgroup's Add tail
+    // (two loops over the one list: a single loop whose body holds both kinds
+    // of unit took 200 VGPRs, two waves per SIMD)
     const uint32_t nadd = ga.wg_prefix[ga.nb];
-    uint32_t ek[U][4], ev[U][4];
+    uint32_t ek[UA][4], ev[UA][4];
     if (tid == 0) __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (uint32_t c = wg; c < nadd + nget; c += nwg) {
-      if (c < nadd)
-        bad |= dense_chunk_own<U, NT, NTP, false>(ga, d, c, s_first, s_last, ek, ev);
-      else
-        fused_get_chunk<U, NT>(gg, ga, d, o, c - nadd, s_first, s_last, true);
-    }
+    uint32_t c = wg;
+    for (; c < nadd; c += nwg) bad |= dense_chunk_own<UA, NT, NTP, false>(ga, d, c, s_first, s_last, ek, ev);
+    for (c -= nadd; c < nget; c += nwg) fused_get_chunk<UG, NT>(gg, ga, d, o, c, s_first, s_last, true);
     if (bad) *flag = epoch;
     return;
   }
@@ -1071,7 +1083,7 @@ __global__ __launch_bounds__(kBlock) void k_add_get(GroupArgs ga, GroupArgs gg, 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  for (uint32_t c = wg; c < nget; c += nwg) fused_get_chunk<U, NT>(gg, ga, d, o, c, s_first, s_last, false);
+  for (uint32_t c = wg; c < nget; c += nwg) fused_get_chunk<UG, NT>(gg, ga, d, o, c, s_first, s_last, false);
 }
 
 // a + b with two's-complement wrap for int32 (the reference's int values),
@@ -2816,18 +2828,28 @@ hipError_t launch_replay(int dtype, int mode, const GroupArgs& ga, const DenseVi
   return hipGetLastError();
 }
 
-hipError_t launch_add_get(bool ntp, const GroupArgs& ga, const GroupArgs& gg, const DenseView& d, const Ovf& o,
-                          uint32_t tile_shift, uint64_t ntiles, uint32_t grid, uint32_t* flag, uint32_t epoch,
-                          unsigned long long* bar, unsigned long long bar_target, hipStream_t st) {
+hipError_t launch_add_get(int ua, bool ntp, const GroupArgs& ga, const GroupArgs& gg, const DenseView& d,
+                          const Ovf& o, uint32_t tile_shift, uint64_t ntiles, uint32_t grid, uint32_t* flag,
+                          uint32_t epoch, unsigned long long* bar, unsigned long long bar_target, hipStream_t st) {
   if (grid == 0) return hipSuccess;
-  if (ntp)
-    k_add_get<8, true, true><<<grid, kBlock, 0, st>>>(ga, gg, d, o, tile_shift, ntiles, flag, epoch, bar, bar_target);
-  else
-    k_add_get<8, true, false><<<grid, kBlock, 0, st>>>(ga, gg, d, o, tile_shift, ntiles, flag, epoch, bar, bar_target);
+#define PSKV_K10(UA, NTP)                                                                                          \
+  k_add_get<UA, 8, true, NTP><<<grid, kBlock, 0, st>>>(ga, gg, d, o, tile_shift, ntiles, flag, epoch, bar, bar_target)
+  if (ua == 4) {
+    if (ntp)
+      PSKV_K10(4, true);
+    else
+      PSKV_K10(4, false);
+  } else {
+    if (ntp)
+      PSKV_K10(8, true);
+    else
+      PSKV_K10(8, false);
+  }
+#undef PSKV_K10
   return hipGetLastError();
 }
 
-int add_get_max_grid() {
+int add_get_max_grid(int ua) {
   // co-resident workgroups of the fused launch: the occupancy query per CU
   // times the CUs.  At k_add_get's register counts (102 VGPRs: 4 waves per
   // SIMD; 104 SGPRs) the query is exact (MI355X_MICROARCH.md "Residency": the
@@ -2837,11 +2859,16 @@ int add_get_max_grid() {
   int dev = 0, cus = 0, per = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_add_get<8, true, false>, kBlock, 0) != hipSuccess)
-    return 0;
   int per2 = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per2, k_add_get<8, true, true>, kBlock, 0) != hipSuccess)
-    return 0;
+  if (ua == 4) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_add_get<4, 8, true, false>, kBlock, 0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per2, k_add_get<4, 8, true, true>, kBlock, 0) != hipSuccess)
+      return 0;
+  } else {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_add_get<8, 8, true, false>, kBlock, 0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per2, k_add_get<8, 8, true, true>, kBlock, 0) != hipSuccess)
+      return 0;
+  }
   per = per < per2 ? per : per2;
   return (per > 0 ? per : 1) * cus;
 }

@@ -274,6 +274,12 @@ struct pskv_shard {
   // ramp, not between the launches
   bool tune_fuse = false;
   int fuse_grid_max = 0;          // K10's co-resident grid (occupancy query, at first use)
+  // K10's Add chunk (groups of 4 keys per lane): 8, or 4 under the probe
+  // variable PSKV_PROBE_FUSE_UA=4 (measurement only, not an option)
+  int fuse_ua = [] {
+    const char* e = std::getenv("PSKV_PROBE_FUSE_UA");
+    return e && std::atoi(e) == 4 ? 4 : 8;
+  }();
   unsigned long long bar_count = 0;  // K10's barrier counter: every launch adds its grid
   int tune_early = 2;    // PSKV_EARLY: K2g early loads (0 never, 1 always, 2 when the group's keys cover < 1/4 of the range)
   // PSKV_PAGEABLE_DMA: DMA pageable host buffers directly (the runtime moves
@@ -1789,7 +1795,7 @@ int add_get_impl(pskv_shard* s, const std::vector<pskv_batch>& adds, const std::
   rc = srv_stop(s);
   if (rc) return rc;
   if (!s->fuse_grid_max) {
-    s->fuse_grid_max = add_get_max_grid();
+    s->fuse_grid_max = add_get_max_grid(s->fuse_ua);
     if (s->fuse_grid_max <= 0) return fail(PSKV_EHIP, "fused Add+Get: occupancy query failed");
   }
   const auto ag = split_groups(va);
@@ -1803,7 +1809,7 @@ int add_get_impl(pskv_shard* s, const std::vector<pskv_batch>& adds, const std::
     const auto& a = ag.back();
     const auto& g = gg.front();
     GroupArgs gaa, gga;
-    const uint32_t nadd = build_group(va, a.first, a.second, stream_chunk(8), &gaa);
+    const uint32_t nadd = build_group(va, a.first, a.second, stream_chunk(s->fuse_ua), &gaa);
     const uint32_t nget = build_group(vg, g.first, g.second, stream_chunk(8), &gga);
     uint64_t elems = 0;
     for (size_t i = a.first; i < a.second; ++i) elems += va[i].n;
@@ -1822,8 +1828,8 @@ int add_get_impl(pskv_shard* s, const std::vector<pskv_batch>& adds, const std::
     unsigned long long* bar = reinterpret_cast<unsigned long long*>(s->flag + 2);
     {
       LaunchTimer t(s, PSKV_K_ADD_GET, elems);
-      PSKV_HIP(launch_add_get(s->tune_ntp, gaa, gga, s->dview(), s->ovf, shift, ntiles, grid, s->flag, epoch, bar,
-                              s->bar_count, s->stream));
+      PSKV_HIP(launch_add_get(s->fuse_ua, s->tune_ntp, gaa, gga, s->dview(), s->ovf, shift, ntiles, grid, s->flag,
+                              epoch, bar, s->bar_count, s->stream));
       t.done();
     }
     {

@@ -52,6 +52,8 @@ shift
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 for step in "$@"; do
+  echo "[$(date +%T)] step $step start"
+  echo "[$(date +%T)] step $step start" >> "$OUT/steps.log"
   case $step in
     tests_focus) timeout -k 10 300 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread \
         "$R/tests/test_gpu_parity.py" "$R/tests/test_replay.py" \
