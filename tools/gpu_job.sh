@@ -34,6 +34,8 @@
 #   ntp_ab       the headline (and its cold form) with K2g parameter stores and K1 parameter loads cached / nt, twice
 #   emu_ntp      every rank of N = 8 emulated, K2g parameter stores cached / non-temporal
 #   emu8_fuse    every rank of N = 8 emulated with the fused Add + Get launch on / off
+#   emu8_fuse_ua every rank of N = 8: separate launches, fused with 8 Ki-key and with 4 Ki-key Add chunks
+#   bench_fuse_ua the headline (+ cold form) the same three ways
 #   smoke        __graft_entry__.smoke() (what the driver runs before the bench)
 #   shardsize    tools/shard_size_probe.py: K2g / K1 per key on 1e8 / 5e8 / 1e9-key shards (same windows)
 #   getntp       tools/shard_size_probe.py with K1 parameter loads cached / non-temporal (GET_NTP=0/1), twice
@@ -139,6 +141,15 @@ for step in "$@"; do
           PSKV_NTP=$e PSKV_BENCH_EMULATE=$r/8 timeout -k 10 200 python3 "$R/bench.py" --steps 50 --no-zipf \
             --no-cpu-baseline --no-extra > "$OUT/emu8_${r}_ntp$e.json" 2> "$OUT/emu8_${r}_ntp$e.err" || exit 1
         done; done ;;
+    emu8_fuse_ua) for r in 0 1 2 3 4 5 6 7; do for v in "0 8" "1 8" "1 4"; do set -- $v
+          PSKV_FUSE=$1 PSKV_PROBE_FUSE_UA=$2 PSKV_BENCH_EMULATE=$r/8 timeout -k 10 200 python3 "$R/bench.py" --steps 50 \
+            --no-zipf --no-cpu-baseline --no-extra > "$OUT/emu8_${r}_fuse$1_ua$2.json" 2> "$OUT/emu8_${r}_fuse$1_ua$2.err" \
+            || exit 1
+        done; done ;;
+    bench_fuse_ua) for v in "0 8" "1 8" "1 4"; do set -- $v
+          PSKV_FUSE=$1 PSKV_PROBE_FUSE_UA=$2 timeout -k 10 300 python3 "$R/bench.py" --steps 50 --no-zipf --no-extra \
+            --no-cpu-baseline > "$OUT/bench_fuse$1_ua$2.json" 2> "$OUT/bench_fuse$1_ua$2.err" || exit 1
+        done ;;
     emu8_fuse) for r in 0 1 2 3 4 5 6 7; do for f in 1 0; do
           PSKV_FUSE=$f PSKV_BENCH_EMULATE=$r/8 timeout -k 10 200 python3 "$R/bench.py" --steps 50 --no-zipf \
             --no-cpu-baseline --no-extra > "$OUT/emu8_${r}_fuse$f.json" 2> "$OUT/emu8_${r}_fuse$f.err" || exit 1
