@@ -36,6 +36,7 @@
 #   emu8_fuse    every rank of N = 8 emulated with the fused Add + Get launch on / off
 #   emu8_fuse_ua every rank of N = 8: separate launches, fused with 8 Ki-key and with 4 Ki-key Add chunks
 #   bench_fuse_ua the headline (+ cold form) the same three ways
+#   k2g_tune     the headline (+ cold form) under K2g grid / early-load / unroll variants
 #   smoke        __graft_entry__.smoke() (what the driver runs before the bench)
 #   shardsize    tools/shard_size_probe.py: K2g / K1 per key on 1e8 / 5e8 / 1e9-key shards (same windows)
 #   getntp       tools/shard_size_probe.py with K1 parameter loads cached / non-temporal (GET_NTP=0/1), twice
@@ -141,6 +142,12 @@ for step in "$@"; do
           PSKV_NTP=$e PSKV_BENCH_EMULATE=$r/8 timeout -k 10 200 python3 "$R/bench.py" --steps 50 --no-zipf \
             --no-cpu-baseline --no-extra > "$OUT/emu8_${r}_ntp$e.json" 2> "$OUT/emu8_${r}_ntp$e.err" || exit 1
         done; done ;;
+    k2g_tune) for o in "" "PSKV_TILE_GRID=1024" "PSKV_TILE_GRID=2048" "PSKV_TILE_GRID=8192" "PSKV_EARLY=1" \
+          "PSKV_UNROLL=4"; do
+          tag=$(echo "x$o" | tr ' =' '__')
+          env $o timeout -k 10 300 python3 "$R/bench.py" --steps 50 --no-zipf --no-extra --no-cpu-baseline \
+            > "$OUT/tune$tag.json" 2> "$OUT/tune$tag.err" || exit 1
+        done ;;
     emu8_fuse_ua) for r in 0 1 2 3 4 5 6 7; do for v in "0 8" "1 8" "1 4"; do set -- $v
           PSKV_FUSE=$1 PSKV_PROBE_FUSE_UA=$2 PSKV_BENCH_EMULATE=$r/8 timeout -k 10 200 python3 "$R/bench.py" --steps 50 \
             --no-zipf --no-cpu-baseline --no-extra > "$OUT/emu8_${r}_fuse$1_ua$2.json" 2> "$OUT/emu8_${r}_fuse$1_ua$2.err" \
