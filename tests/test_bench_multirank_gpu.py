@@ -1,0 +1,52 @@
+"""bench.py's N > 1 path end to end, as the driver launches it
+(`python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr
+127.0.0.1 ... bench.py --gpus N`), rehearsed on one GPU: two rank processes,
+gloo for the barrier and the reductions, both ranks' shards on cuda:0
+(PSKV_BENCH_BACKEND=gloo, PSKV_BENCH_SHARE_GPU=1 — rehearsal knobs the driver
+never sets).  Every rank runs cfg 4's self-check (its pulls against a model of
+its shard), the timed steps, the fused-launch and Zipf measurements and the
+weak-scaled extra; rank 0 prints the one JSON line.  The 8-GPU run is the
+driver's; this pins that the multi-rank code path runs and reports what it
+should (n_gpus, strong scaling, per-GPU spread, zero push/pull overlap)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_bench_two_ranks_one_gpu(cuda):
+    env = dict(os.environ, PSKV_BENCH_BACKEND="gloo", PSKV_BENCH_SHARE_GPU="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1", "--sets", "4"]
+    r = subprocess.run(["timeout", "-k", "10", "400"] + cmd, capture_output=True, text=True, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-5000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["steps"] == 3 and res["scaling"] == "strong"
+    assert res["value"] > 0 and res["unit"] == "GB/s"
+    cfg = res["config"]
+    assert cfg["key_space"] == 1_000_000_000 and cfg["shard_keys_per_gpu"] == 500_000_000
+    assert cfg["push_pull_overlap_keys"] == 0
+    assert res["per_gpu"]["min_GB/s"] <= res["per_gpu"]["max_GB/s"]
+    assert "k_gather" in res["roofline"]["kernels"] and "k_assign_group" in res["roofline"]["kernels"]
+    assert res["roofline"]["fused_launch"]["GB/s"] > 0
+    assert "cold" not in res["roofline"]  # the cold form is an N = 1 figure
+    assert res["zipf_sparse"]["n_gpus"] == 2
+    assert res["extra"]["weak_scaled"]["GB/s"] > 0
