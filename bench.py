@@ -286,9 +286,7 @@ class Form:
 
     def step(self, i):
         # the grouped Add then the grouped Get, in one call
-        # (pskv_add_get_grouped: the separate K2g + K1 launches by default; the
-        # fused K10 launch with the shard option FUSE = 1, measured slower and
-        # reported as roofline.fused_launch)
+        # (pskv_add_get_grouped: the K2g launch + its conditional replay, then K1)
         self.shard.add_get_grouped(self.adds[i % self.R], self.gets[i % self.R], sorted_hint=self.hint)
 
     def bytes(self, steps):
@@ -341,22 +339,17 @@ def timed(form, steps, world, dev):
     return max_over_ranks(own, world, dev), own
 
 
-def evented(form, steps, world, dev, fuse=None):
+def evented(form, steps, world, dev):
     """The same steps again with HIP events around the streaming kernels on
     their launch stream: per-kernel launches and average duration, and the
-    algorithmic bytes per launch (this rank's).  By default the step runs as
-    the separate K2g / K1 launches; fuse=1 runs it as the fused K10 launch,
-    which moves both halves' bytes (the shard's FUSE option, restored after)."""
+    algorithmic bytes per launch (this rank's)."""
     import torch
 
     from parameter_server_amd import _lib
 
     sh = form.shard
-    old = sh.get_option("FUSE")
-    if fuse is not None:
-        sh.set_option("FUSE", fuse)
     sh.reset_timing()
-    sh.set_timing(True, kernels=[_lib.PSKV_K_GATHER, _lib.PSKV_K_ASSIGN_TILES, _lib.PSKV_K_ADD_GET])
+    sh.set_timing(True, kernels=[_lib.PSKV_K_GATHER, _lib.PSKV_K_ASSIGN_TILES])
     torch.cuda.synchronize()
     t2 = time.perf_counter()
     for i in range(steps):
@@ -364,13 +357,12 @@ def evented(form, steps, world, dev, fuse=None):
     torch.cuda.synchronize()
     t3 = time.perf_counter()
     sh.set_timing(False)
-    sh.set_option("FUSE", old)
     add_b, get_b = form.bytes(steps)
     ktimes = {}
     for k, name in _lib.KERNEL_NAMES.items():
         t = sh.kernel_time(k)
         if t["launches"]:
-            b = {_lib.PSKV_K_GATHER: get_b, _lib.PSKV_K_ADD_GET: add_b + get_b}.get(k, add_b)
+            b = get_b if k == _lib.PSKV_K_GATHER else add_b
             rec = {"launches": t["launches"], "avg_ms": t["total_ms"] / t["launches"],
                    "keys_per_launch": t["elements"] / t["launches"],
                    "algorithmic_bytes": b / t["launches"]}
@@ -380,19 +372,14 @@ def evented(form, steps, world, dev, fuse=None):
     return ktimes, max_over_ranks(t3 - t2, world, dev)
 
 
-def run_form(form, steps, warmup, world, dev, fuse=None):
-    """Warm up, time, and sum the bytes over ranks: the aggregate GB/s of a form
-    (fuse: the shard's FUSE option for this measurement, restored after)."""
+def run_form(form, steps, warmup, world, dev):
+    """Warm up, time, and sum the bytes over ranks: the aggregate GB/s of a form."""
     import torch
 
-    old = form.shard.get_option("FUSE")
-    if fuse is not None:
-        form.shard.set_option("FUSE", fuse)
     for i in range(warmup):
         form.step(i)
     torch.cuda.synchronize()
     elapsed, own = timed(form, steps, world, dev)
-    form.shard.set_option("FUSE", old)
     a, g = form.bytes(steps)
     total = sum_over_ranks(float(a + g), world, dev)
     return {"GB/s": total / elapsed / 1e9, "ms_per_step": elapsed / steps * 1e3, "elapsed": elapsed,
@@ -924,8 +911,6 @@ def cold_form(dev, J, B, R, steps, warmup, space, n_pulls):
         f.self_check(0, space, dev)
         res = run_form(f, steps, max(warmup, R), 1, dev)
         kt, ev_s = evented(f, steps, 1, dev)
-        kt_fused, _ = evented(f, steps, 1, dev, fuse=1)
-        fused = run_form(f, steps, 2, 1, dev, fuse=1)
         sh.set_stream(None)
     a, g = f.bytes(steps)
     del f, sets
@@ -942,9 +927,7 @@ def cold_form(dev, J, B, R, steps, warmup, space, n_pulls):
             "kernels": kernel_fracs(kt),
             "kernel": dom[0], "frac": dom[1]["GB/s"] / HBM_PEAK_GBS, "traffic": traffic,
             "traffic_over_algorithmic": traffic / dom[1]["algorithmic_bytes"] if traffic else None,
-            "traffic_source": src,
-            "fused_launch": {"GB/s": fused["GB/s"], "ms_per_step": fused["ms_per_step"],
-                             "kernels": kernel_fracs(kt_fused)}}
+            "traffic_source": src}
 
 
 _T0 = time.perf_counter()
@@ -1008,9 +991,6 @@ def main(argv=None):
     progress("headline: timed steps")
     head = run_form(form, args.steps, max(args.warmup, R), world, dev)
     ktimes, evented_s = evented(form, args.steps, world, dev)
-    # the same step as ONE fused launch (K10, FUSE = 1): measured beside
-    ktimes_fused, _ = evented(form, args.steps, world, dev, fuse=1)
-    fused = run_form(form, args.steps, 2, world, dev, fuse=1)
     touched = min(form.touched(i) for i in range(R))
     a_b, g_b = form.bytes(args.steps)
     own_bytes = a_b + g_b
@@ -1046,9 +1026,7 @@ def main(argv=None):
                       "kernels, over a second pass of the same K steps run right after the "
                       "event-free timed region",
             "ms_per_step_evented": evented_s / args.steps * 1e3,
-            "kernels": kernel_fracs(ktimes),
-            "fused_launch": {"GB/s": fused["GB/s"], "ms_per_step": fused["ms_per_step"],
-                             "kernels": kernel_fracs(ktimes_fused)}}
+            "kernels": kernel_fracs(ktimes)}
     if cold is not None:
         roof["cold"] = cold
     if traffic_src:

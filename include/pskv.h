@@ -139,9 +139,8 @@ enum pskv_kernel {
   PSKV_K_ACC_DENSE = 7,     /* K7: accumulate dense windows, one RMW per key */
   PSKV_K_INLINE_ADD = 8,    /* K8: small host Add carried in the kernel arguments */
   PSKV_K_INLINE_GET = 9,    /* K8: small host Get, reply written to page-locked memory */
-  PSKV_K_REPLAY = 10,       /* K4r / K10r: conditional replay behind a verifying sorted-path group */
-  PSKV_K_ADD_GET = 11,      /* K10: fused grouped sorted Add + grouped Get */
-  PSKV_K_COUNT = 12
+  PSKV_K_REPLAY = 10,       /* K4r: conditional replay behind a verifying sorted-path group */
+  PSKV_K_COUNT = 11
 };
 
 /* Create a shard owning keys [key_begin, key_end) on `device`.  The dense
@@ -175,14 +174,12 @@ int pskv_get(pskv_shard* s, const uint32_t* keys, uint64_t n, void* out, int fla
  * fixed number of kernel launches. */
 int pskv_add_grouped(pskv_shard* s, const pskv_batch* batches, uint64_t nb, int flags);
 int pskv_get_grouped(pskv_shard* s, const pskv_batch* batches, uint64_t nb, int flags);
-/* pskv_add_grouped(adds) then pskv_get_grouped(gets) in one call: the BSP
- * model's flush of its deferred Adds followed by the Gets that flush releases
+/* pskv_add_grouped(adds) then pskv_get_grouped(gets) in one call (flags as
+ * for both; PSKV_SORTED_HINT applies to the Adds): the BSP model's flush of
+ * its deferred Adds followed by the Gets that flush releases
  * (server/consistency/bsp_model.cpp:14-31), or one worker round's push then
- * pull.  Identical results.  For device batches under PSKV_SORTED_HINT (4-byte
- * values, assign mode, 16-byte-aligned batches) the Add group and the Get
- * group run as ONE launch (option FUSE), the Get's workgroups starting as the
- * Add's finish; a wrong hint is repaired (the Get answered again) as for
- * pskv_add. */
+ * pull.  Identical results to the two calls.  (A single fused launch for the
+ * pair was built and measured slower than the two launches) */
 int pskv_add_get_grouped(pskv_shard* s, const pskv_batch* adds, uint64_t na, const pskv_batch* gets,
                          uint64_t ng, int flags);
 
@@ -202,7 +199,7 @@ int pskv_shard_info(pskv_shard* s, pskv_info* info);
 
 /* Tuning and path options of one shard, by name (DESIGN.md §5 lists them and
  * what each selects): GENERAL (0 = K4 stamps, 1 = auto, 2 = K5 always),
- * UNROLL, NT, NTP, FUSE, EARLY (K2g early loads: 0 never, 1 always, 2 auto),
+ * UNROLL, NT, NTP, EARLY (K2g early loads: 0 never, 1 always, 2 auto),
  * PAGEABLE_DMA, DMA_MIN_BYTES, DMA_MIN_BYTES_GET,
  * DMA_MIN_BYTES_PINNED, ZC_MAX_BYTES, FRAME_ZC_MAX_BYTES, INLINE,
  * INLINE_ADD_CHUNKS, INLINE_GET_CHUNKS, ISPIN, SERVE, SERVE_IDLE_US,
@@ -210,9 +207,6 @@ int pskv_shard_info(pskv_shard* s, pskv_info* info);
  * Every option changes speed only, never results.  Some apply only together
  * with others (a value is accepted and echoed either way):
  *   EARLY = 1     K2g with UNROLL 8 and NT 1 (otherwise the default loads)
- *   FUSE = 1      pskv_add_get_grouped with device batches, PSKV_SORTED_HINT,
- *                 4-byte values, assign mode, 16-byte-aligned batches, UNROLL 8
- *                 and NT 1 (otherwise the separate Add and Get paths)
  *   SERVE = 1     only while the device's hardware queues hold the server
  *                 (DESIGN.md §8); INLINE_*_CHUNKS and ISPIN only on the K8 path
  *   RB_* options  only on the K5 path (unhinted Adds)

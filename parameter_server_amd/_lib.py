@@ -35,8 +35,7 @@ PSKV_K_ACC_DENSE = 7
 PSKV_K_INLINE_ADD = 8
 PSKV_K_INLINE_GET = 9
 PSKV_K_REPLAY = 10
-PSKV_K_ADD_GET = 11
-PSKV_K_COUNT = 12
+PSKV_K_COUNT = 11
 KERNEL_NAMES = {
     PSKV_K_GATHER: "k_gather",
     PSKV_K_ASSIGN_SORTED: "k_assign_sorted",
@@ -49,7 +48,6 @@ KERNEL_NAMES = {
     PSKV_K_INLINE_ADD: "k_inline_add",
     PSKV_K_INLINE_GET: "k_inline_get",
     PSKV_K_REPLAY: "k_replay",
-    PSKV_K_ADD_GET: "k_add_get",
 }
 
 # Every symbol include/pskv.h declares (checked by tests/test_abi.py).

@@ -54,7 +54,7 @@ struct GroupArgs {
   uint32_t wg_prefix[kMaxBatches + 1];  // first workgroup of each batch
   DevBatch b[kMaxBatches];
 };
-static_assert(sizeof(GroupArgs) <= 1800, "two groups (the fused Add+Get launch) fit the 4 KiB kernarg segment");
+static_assert(sizeof(GroupArgs) <= 1800, "a group plus the other arguments fit the 4 KiB kernarg segment");
 
 // K8: a whole small message inside the kernel arguments (<= 4 KiB kernarg).
 struct InlineAdd {
@@ -130,18 +130,6 @@ hipError_t launch_general_mark(int dtype, int mode, const GroupArgs& ga, uint32_
 hipError_t launch_general_commit(int vb, const GroupArgs& ga, uint32_t nwg, const DenseView& d,
                                  const Ovf& o, const unsigned long long* owner,
                                  const uint32_t* cond, uint32_t epoch, hipStream_t st);
-// K10 fused grouped sorted Add + grouped Get (4-byte values, aligned batches,
-// assign): persistent grid of `grid` <= add_get_max_grid() workgroups; the
-// tile mode's grid barrier waits until *bar reaches bar_target (every launch
-// adds `grid` to *bar).  K10r replays + answers the Get again on a tag.
-// ua: groups of 4 keys per lane in the Add's chunks (8: K2g's 8 Ki-key chunks,
-// 102 VGPRs; 4: 4 Ki-key chunks, 81 VGPRs)
-hipError_t launch_add_get(int ua, bool ntp, const GroupArgs& ga, const GroupArgs& gg, const DenseView& d,
-                          const Ovf& o, uint32_t tile_shift, uint64_t ntiles, uint32_t grid, uint32_t* flag,
-                          uint32_t epoch, unsigned long long* bar, unsigned long long bar_target, hipStream_t st);
-int add_get_max_grid(int ua);
-hipError_t launch_replay_get(const GroupArgs& ga, const GroupArgs& gg, const DenseView& d, const Ovf& o,
-                             const uint32_t* cond, uint32_t epoch, hipStream_t st);
 hipError_t launch_ovf_rehash(int vb, const Ovf& from, uint64_t from_cap, const Ovf& to,
                              hipStream_t st);
 // K4r: conditional replay of a group in call order by ONE workgroup (runs only

@@ -160,9 +160,8 @@ struct VecN<unsigned long long> : Vec2x8 {
 // full group) before the workgroup's first memory access.  (Loading the whole
 // table at once needs ~100 SGPRs and costs the gather a wave per SIMD.)
 // Group-wide index of batch j's first element (the K4 stamps' element index):
-// a scalar sum over the batches before it (the kernarg holds no prefix table,
-// which keeps two groups within the 4 KiB kernarg segment of the fused
-// Add+Get launch).
+// a scalar sum over the batches before it (the kernarg segment holds no prefix
+// table: 512 B less to copy per launch, for the stamps variant only).
 __device__ __forceinline__ uint64_t elem_prefix(const GroupArgs& ga, int j) {
   uint64_t e = 0;
   for (int i = 0; i < j; ++i) e += ga.b[i].n;
@@ -704,7 +703,7 @@ __device__ __forceinline__ bool dense_chunk_own(const GroupArgs& ga, const Dense
   return bad;
 }
 
-// The prologue of a grouped sorted Add (K2g and the fused K2g + K1): lanes of
+// The prologue of a grouped sorted Add (K2g): lanes of
 // waves 0 and 1 keep batch jb's endpoints for the whole launch; wave 0
 // publishes them (s_first / s_last) and whether every batch is one dense
 // in-range window (s_dense).  Endpoints out of range or inverted tag `flag`
@@ -846,244 +845,6 @@ __global__ __launch_bounds__(kBlock) void k_assign_group(GroupArgs ga, DenseView
   }
   bad = tile_mode<VT, VEC>(ga, d, g, tile_shift, ntiles, blockIdx.x, gridDim.x, s_seg_s, s_seg_e, &s_mask);
   if (bad) *flag = epoch;
-}
-
-// ------------------------------------------- K10 fused grouped Add + Get
-// One launch for "grouped sorted Add, then grouped Get" (round 4): the Get's
-// workgroups start as the Add's finish instead of behind a kernel boundary
-// and a second launch ramp, which a rank-sized step (cfg 4 at N = 8: ~8 M
-// keys each way) pays in full.  Persistent grid, at most what the device holds
-// at once (pskv_shard.cpp sizes it from the occupancy query, one workgroup per
-// CU to spare): every workgroup applies Add chunks (grid-stride), then Get
-// chunks.  4-byte values, 16-byte-aligned batches, assign mode.
-//   dense mode (every push batch one window, K2g's test): no workgroup waits
-//     for another.  A Get key that no push window of the group covers reads a
-//     parameter this launch does not write (the sorted pass never writes a key
-//     the group does not hold, §4).  A covered key is answered from the push
-//     itself: its value in the LAST covering window, vals_j[k - first_j] —
-//     exactly what the Add stores there once the windows verify.  If any
-//     window fails its verification the group is tagged and K10r replays it
-//     and answers the Get again.
-//   tile mode (sorted batches that are not all windows): the Add's tiles,
-//     then a grid barrier (one device counter; every storing wave drained, an
-//     agent release before the arrival, an agent acquire after the poll,
-//     MI355X_MICROARCH.md "Valid forms"), then plain gathers.  The grid is
-//     co-resident, so the barrier cannot wait on a workgroup that is not
-//     running.  Every launch adds its grid size to the counter (dense mode
-//     arrives without waiting), so a launch waits for `bar_target` = the
-//     counter before it + its grid.
-// K10r k_replay_get (conditional, one workgroup) follows every fused launch:
-// on a tag it replays the Add group (K4r) and then answers the Get group again
-// from the repaired shard.
-
-__device__ __forceinline__ uint32_t wave_min(uint32_t x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, o, 64));
-  return x;
-}
-__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o, 64));
-  return x;
-}
-
-// The value a Get key reads after the group's Add, when push windows of the
-// group may cover it (m: the windows that meet this wave's keys): the last
-// covering window's pushed value, else the shard's.
-__device__ __forceinline__ uint32_t fused_value(const GroupArgs& ga, const DenseView& d, const Ovf& o, uint32_t k,
-                                                unsigned long long m, const uint32_t* s_first,
-                                                const uint32_t* s_last) {
-  while (m) {
-    const int q = 63 - __clzll((long long)m);
-    if (k >= s_first[q] && k <= s_last[q])
-      return reinterpret_cast<const uint32_t*>(ga.b[q].vals)[k - s_first[q]];
-    m &= ~(1ull << q);
-  }
-  return load_one<uint32_t>(d, o, k);
-}
-
-// Four keys of one lane (fused Get, windows m meet the wave): a run inside the
-// LAST window that meets it is one dword-aligned 16-byte load of that window's
-// pushed values; a run no window meets is one parameter load (gather4); a run
-// a window only partly covers, or scattered keys, go key by key.
-__device__ __forceinline__ void fused_group4(const GroupArgs& ga, const DenseView& d, const Ovf& o,
-                                             const uint32_t (&k)[4], uint32_t (&v)[4], unsigned long long m,
-                                             const uint32_t* s_first, const uint32_t* s_last) {
-  const bool run = (k[1] == k[0] + 1u) & (k[2] == k[0] + 2u) & (k[3] == k[0] + 3u) & (k[0] <= 0xFFFFFFFCu);
-  if (run) {
-    const uint32_t k3 = k[0] + 3u;
-    bool partial = false;
-    while (m) {
-      const int q = 63 - __clzll((long long)m);
-      if (s_first[q] <= k[0] && s_last[q] >= k3) {
-        ld16a4<false>(reinterpret_cast<const uint32_t*>(ga.b[q].vals) + (k[0] - s_first[q]), v);
-        return;
-      }
-      if (s_first[q] <= k3 && s_last[q] >= k[0]) {
-        partial = true;
-        break;
-      }
-      m &= ~(1ull << q);
-    }
-    if (!partial) {
-      gather4<uint32_t>(d, o, k, v);
-      return;
-    }
-  }
-#pragma unroll
-  for (int e = 0; e < 4; ++e) v[e] = fused_value(ga, d, o, k[e], m, s_first, s_last);
-}
-
-// The push windows that meet the key span [lo, hi] of this wave (lane j tests
-// window j; every lane of the wave gets the mask).
-__device__ __forceinline__ unsigned long long windows_meeting(const GroupArgs& ga, uint32_t lo, uint32_t hi,
-                                                              const uint32_t* s_first, const uint32_t* s_last) {
-  const int lane = threadIdx.x & 63;
-  lo = wave_min(lo);
-  hi = wave_max(hi);
-  return __ballot(lane < ga.nb && s_first[lane] <= hi && s_last[lane] >= lo);
-}
-
-// Get chunk c of group gg inside the fused launch.  `covered`: the push group
-// ga is in dense mode and its values are not known to be stored yet.
-template <int U, bool NT>
-__device__ __forceinline__ void fused_get_chunk(const GroupArgs& gg, const GroupArgs& ga, const DenseView& d,
-                                                const Ovf& o, uint32_t c, const uint32_t* s_first,
-                                                const uint32_t* s_last, bool covered) {
-  constexpr int CH = kBlock * 4 * U;
-  const int tid = threadIdx.x;
-  const int j = batch_of(gg, c);
-  const uint32_t* __restrict__ keys = gg.b[j].keys;
-  uint32_t* __restrict__ out = reinterpret_cast<uint32_t*>(const_cast<void*>(gg.b[j].vals));
-  const uint64_t n = gg.b[j].n;
-  const uint64_t base = (uint64_t)(c - gg.wg_prefix[j]) * CH;
-  if (base + CH <= n) {
-    uint32_t k[U][4], v[U][4];
-#pragma unroll
-    for (int u = 0; u < U; ++u) Vec4<uint32_t>::load<NT>(keys + base + (uint64_t)(u * kBlock + tid) * 4, k[u]);
-    unsigned long long m = 0;
-    if (covered) {
-      uint32_t lo = 0xFFFFFFFFu, hi = 0u;
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          lo = min(lo, k[u][e]);
-          hi = max(hi, k[u][e]);
-        }
-      m = windows_meeting(ga, lo, hi, s_first, s_last);
-    }
-    if (m == 0) {  // no push window meets this wave's keys (the usual case)
-#pragma unroll
-      for (int u = 0; u < U; ++u) gather4<uint32_t>(d, o, k[u], v[u]);
-#pragma unroll
-      for (int u = 0; u < U; ++u) Vec4<uint32_t>::store<NT>(out + base + (uint64_t)(u * kBlock + tid) * 4, v[u]);
-    } else {
-      // pull keys that push windows of this launch may cover: one group at a
-      // time, its keys read again (L2-warm) and its values stored at once, so
-      // nothing of the other groups stays live (with every group's keys and
-      // values held across this path the kernel took ~160-200 VGPRs, 2 waves
-      // per SIMD, against 102)
-#pragma unroll 1
-      for (int u = 0; u < U; ++u) {
-        uint32_t kk[4], vv[4];
-        Vec4<uint32_t>::load<false>(keys + base + (uint64_t)(u * kBlock + tid) * 4, kk);
-        fused_group4(ga, d, o, kk, vv, m, s_first, s_last);
-        Vec4<uint32_t>::store<NT>(out + base + (uint64_t)(u * kBlock + tid) * 4, vv);
-      }
-    }
-  } else {
-    // a partial chunk (the last of a batch): eight keys per lane at a time
-    const uint64_t end = n < base + CH ? n : base + CH;
-    for (uint64_t i0 = base + tid; i0 < base + CH; i0 += 8ull * kBlock) {
-      uint32_t kk[8], vv[8];
-      uint32_t lo = 0xFFFFFFFFu, hi = 0u;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const uint64_t i = i0 + (uint64_t)q * kBlock;
-        kk[q] = i < end ? keys[i] : 0u;
-        if (i < end) {
-          lo = min(lo, kk[q]);
-          hi = max(hi, kk[q]);
-        }
-      }
-      // every lane of the wave reaches the mask (no lane has left the loop:
-      // its bound is the chunk's, not the batch's)
-      const unsigned long long m = covered ? windows_meeting(ga, lo, hi, s_first, s_last) : 0ull;
-#pragma unroll
-      for (int q = 0; q < 8; ++q)
-        vv[q] = i0 + (uint64_t)q * kBlock < end ? fused_value(ga, d, o, kk[q], m, s_first, s_last) : 0u;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const uint64_t i = i0 + (uint64_t)q * kBlock;
-        if (i < end) out[i] = vv[q];
-      }
-    }
-  }
-}
-
-// UA: keys per lane group count of the Add's chunks (4: 4 Ki-key chunks, ~60
-// VGPRs, so the launch keeps 8 waves per SIMD for its Get units too; 8: K2g's
-// 8 Ki-key chunks at 102 VGPRs, 4 waves per SIMD).  UG: the Get's, 8.
-template <int UA, int UG, bool NT, bool NTP>
-__global__ __launch_bounds__(kBlock) void k_add_get(GroupArgs ga, GroupArgs gg, DenseView d, Ovf o,
-                                                    uint32_t tile_shift, uint64_t ntiles, uint32_t* flag,
-                                                    uint32_t epoch, unsigned long long* bar,
-                                                    unsigned long long bar_target) {
-  __shared__ uint64_t s_seg_s[kMaxBatches];
-  __shared__ uint64_t s_seg_e[kMaxBatches];
-  __shared__ uint32_t s_first[kMaxBatches];
-  __shared__ uint32_t s_last[kMaxBatches];
-  __shared__ unsigned long long s_mask;
-  __shared__ int s_dense;
-  const int tid = threadIdx.x;
-  const GroupEnds g = group_prologue(ga, d, flag, epoch, s_first, s_last, &s_dense);
-  __syncthreads();
-  const uint32_t wg = blockIdx.x, nwg = gridDim.x;
-  const uint32_t nget = gg.wg_prefix[gg.nb];
-  bool bad = false;
-  if (s_dense) {
-    // one list of work units, the Add's chunks then the Get's, dealt
-    // round-robin: no unit waits for another, so a workgroup that ran out of
-    // Add chunks takes Get chunks at once and a small launch (a rank's share)
-    // ends on the slowest unit, not on the slowest workgroup's Add tail
-    // (two loops over the one list: a single loop whose body holds both kinds
-    // of unit took 200 VGPRs, two waves per SIMD)
-    const uint32_t nadd = ga.wg_prefix[ga.nb];
-    uint32_t ek[UA][4], ev[UA][4];
-    if (tid == 0) __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t c = wg;
-    for (; c < nadd; c += nwg) bad |= dense_chunk_own<UA, NT, NTP, false>(ga, d, c, s_first, s_last, ek, ev);
-    for (c -= nadd; c < nget; c += nwg) fused_get_chunk<UG, NT>(gg, ga, d, o, c, s_first, s_last, true);
-    if (bad) *flag = epoch;
-    return;
-  }
-  bad = tile_mode<uint32_t, true>(ga, d, g, tile_shift, ntiles, wg, nwg, s_seg_s, s_seg_e, &s_mask);
-  if (bad) *flag = epoch;
-  // grid barrier: every wave's stores drained, the workgroup joined, one lane
-  // releases (L2 write-back), arrives, polls, acquires
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // bounded: a barrier that has not filled within ~1 s (100 MHz wall clock)
-    // is abandoned, and the group tagged -- K10r then replays the Add and
-    // answers the Get again, so the result is right either way
-    const unsigned long long t0 = wall_clock64();
-    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < bar_target) {
-      __builtin_amdgcn_s_sleep(4);
-      if (wall_clock64() - t0 > 100000000ull) {
-        *flag = epoch;
-        break;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  for (uint32_t c = wg; c < nget; c += nwg) fused_get_chunk<UG, NT>(gg, ga, d, o, c, s_first, s_last, false);
 }
 
 // a + b with two's-complement wrap for int32 (the reference's int values),
@@ -2160,23 +1921,6 @@ __global__ __launch_bounds__(kReplayBlock) void k_replay(GroupArgs ga, DenseView
   replay_group<VT, MODE>(ga, d, o);
 }
 
-// K10r: behind a fused Add + Get launch (K10).  On a tag, replay the Add group
-// (as K4r), then answer the Get group again from the repaired shard: the
-// workgroup's own stores, ordered by its barrier, and parameters no other
-// workgroup of this launch writes.
-__global__ __launch_bounds__(kReplayBlock) void k_replay_get(GroupArgs ga, GroupArgs gg, DenseView d, Ovf o,
-                                                             const uint32_t* cond, uint32_t epoch) {
-  if (*cond != epoch) return;
-  replay_group<uint32_t, 0>(ga, d, o);
-  __syncthreads();
-  for (int j = 0; j < gg.nb; ++j) {
-    const uint32_t* __restrict__ keys = gg.b[j].keys;
-    uint32_t* __restrict__ out = reinterpret_cast<uint32_t*>(const_cast<void*>(gg.b[j].vals));
-    const uint64_t n = gg.b[j].n;
-    for (uint64_t i = threadIdx.x; i < n; i += kReplayBlock) out[i] = load_one<uint32_t>(d, o, keys[i]);
-  }
-}
-
 // ------------------------------------------- K6/K7 dense accumulate
 // Accumulate for grouped batches that are each one contiguous key window
 // (first_j .. first_j + n_j - 1): no atomics and no duplicates to resolve.
@@ -2825,57 +2569,6 @@ hipError_t launch_replay(int dtype, int mode, const GroupArgs& ga, const DenseVi
   } else {
     k_replay<double, 1><<<1, kReplayBlock, 0, st>>>(ga, d, o, cond, epoch);
   }
-  return hipGetLastError();
-}
-
-hipError_t launch_add_get(int ua, bool ntp, const GroupArgs& ga, const GroupArgs& gg, const DenseView& d,
-                          const Ovf& o, uint32_t tile_shift, uint64_t ntiles, uint32_t grid, uint32_t* flag,
-                          uint32_t epoch, unsigned long long* bar, unsigned long long bar_target, hipStream_t st) {
-  if (grid == 0) return hipSuccess;
-#define PSKV_K10(UA, NTP)                                                                                          \
-  k_add_get<UA, 8, true, NTP><<<grid, kBlock, 0, st>>>(ga, gg, d, o, tile_shift, ntiles, flag, epoch, bar, bar_target)
-  if (ua == 4) {
-    if (ntp)
-      PSKV_K10(4, true);
-    else
-      PSKV_K10(4, false);
-  } else {
-    if (ntp)
-      PSKV_K10(8, true);
-    else
-      PSKV_K10(8, false);
-  }
-#undef PSKV_K10
-  return hipGetLastError();
-}
-
-int add_get_max_grid(int ua) {
-  // co-resident workgroups of the fused launch: the occupancy query per CU
-  // times the CUs.  At k_add_get's register counts (102 VGPRs: 4 waves per
-  // SIMD; 104 SGPRs) the query is exact (MI355X_MICROARCH.md "Residency": the
-  // SGPR-based hardware limit is 6 workgroups per CU, above the 4 the VGPRs
-  // allow); should other work hold part of the device, the tile mode's
-  // barrier is bounded (k_add_get) and the replay repairs the group
-  int dev = 0, cus = 0, per = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 0;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-  int per2 = 0;
-  if (ua == 4) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_add_get<4, 8, true, false>, kBlock, 0) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per2, k_add_get<4, 8, true, true>, kBlock, 0) != hipSuccess)
-      return 0;
-  } else {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_add_get<8, 8, true, false>, kBlock, 0) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per2, k_add_get<8, 8, true, true>, kBlock, 0) != hipSuccess)
-      return 0;
-  }
-  per = per < per2 ? per : per2;
-  return (per > 0 ? per : 1) * cus;
-}
-
-hipError_t launch_replay_get(const GroupArgs& ga, const GroupArgs& gg, const DenseView& d, const Ovf& o,
-                             const uint32_t* cond, uint32_t epoch, hipStream_t st) {
-  k_replay_get<<<1, kReplayBlock, 0, st>>>(ga, gg, d, o, cond, epoch);
   return hipGetLastError();
 }
 

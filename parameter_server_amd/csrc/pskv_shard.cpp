@@ -258,29 +258,12 @@ struct pskv_shard {
   uint32_t tune_tile_grid = 4096;
   int tune_unroll = 8;   // PSKV_UNROLL: 4 or 8 (8: measured +5 % on the dense Add)
   bool tune_nt = true;   // PSKV_NT: non-temporal streams (measured +12-15 % on K1 / K2g)
-  // PSKV_NTP: non-temporal parameter stores in the dense Add (K2g, K10).  On
+  // PSKV_NTP: non-temporal parameter stores in the dense Add (K2g).  On
   // since round 4: cached stores leave the Add's parameter lines dirty in the
   // Infinity Cache, and the next Get pays their write-back; the headline step
   // 5.74-5.86 -> 6.11-6.22 TB/s, its Get (K1) 114-116 -> 91 us
   // (profiles/r04_probes/ntp_ab/)
   bool tune_ntp = true;
-  // PSKV_FUSE: pskv_add_get_grouped runs its last Add group and first Get group
-  // as ONE launch (K10) where it can (1), or as the separate calls (0).  Off:
-  // measured slower than the separate K2g + K1 launches at every size
-  // (headline 5.98 vs 6.11 TB/s, cold 5.72 vs 5.93, emulated N = 8 ranks
-  // 37.7-43.0 vs 33.7-41.5 us; profiles/r04_probes/emu8_fuse/): one register
-  // allocation for both halves holds the Get at 4 waves per SIMD where K1
-  // runs 8, and a rank's step spends its fixed cost inside each kernel's
-  // ramp, not between the launches
-  bool tune_fuse = false;
-  int fuse_grid_max = 0;          // K10's co-resident grid (occupancy query, at first use)
-  // K10's Add chunk (groups of 4 keys per lane): 8, or 4 under the probe
-  // variable PSKV_PROBE_FUSE_UA=4 (measurement only, not an option)
-  int fuse_ua = [] {
-    const char* e = std::getenv("PSKV_PROBE_FUSE_UA");
-    return e && std::atoi(e) == 4 ? 4 : 8;
-  }();
-  unsigned long long bar_count = 0;  // K10's barrier counter: every launch adds its grid
   int tune_early = 2;    // PSKV_EARLY: K2g early loads (0 never, 1 always, 2 when the group's keys cover < 1/4 of the range)
   // PSKV_PAGEABLE_DMA: DMA pageable host buffers directly (the runtime moves
   // them at the PCIe rate, measured 55 GB/s) instead of copying them into
@@ -1755,102 +1738,24 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
   return PSKV_OK;
 }
 
-// ---------------------------------------------------- fused Add + Get (K10)
-// pskv_add_get_grouped: the same as pskv_add_grouped(adds) followed by
-// pskv_get_grouped(gets) -- BSPModel::Clock's flush of the deferred Adds
-// followed by the Gets it released (server/consistency/bsp_model.cpp:14-31), or
-// one worker round's push then pull.  Device batches under the sorted hint,
-// 4-byte values, assign mode, every pointer 16-byte aligned, the default
-// streams (UNROLL 8, NT 1) and option FUSE: the last Add launch group and the
-// first Get launch group run as ONE launch (K10) followed by the conditional
-// K10r; every other case, and every other group, takes the separate paths.
+// ------------------------------------------------------------ Add then Get
+// pskv_add_get_grouped: pskv_add_grouped(adds) followed by
+// pskv_get_grouped(gets) in one call -- BSPModel::Clock's flush of the
+// deferred Adds followed by the Gets it releases (server/consistency/
+// bsp_model.cpp:14-31), or one producer round's push then pull.  Round 4
+// built this as ONE fused launch (K10: the Add's and the Get's chunks as work
+// units of one co-resident grid, pull keys the same call pushes answered
+// from the pushed values) and measured it slower than the two launches at
+// every size (headline 5.56 against 6.03 TB/s, the emulated N = 8 ranks
+// 44.0-49.5 against 34.7-41.6 us; profiles/r04_probes/fused/): one register
+// allocation for both halves costs the Get half of its waves, and a rank's
+// fixed cost sits inside each kernel's ramp, not between the launches.  The
+// kernel was removed; the call stays, as the two paths.
 int add_get_impl(pskv_shard* s, const std::vector<pskv_batch>& adds, const std::vector<pskv_batch>& gets,
                  int flags) {
-  std::vector<pskv_batch> va, vg;
-  for (auto& b : adds) {
-    if (b.n == 0) continue;
-    if (!b.keys || !b.vals) return fail(PSKV_EINVAL, "pskv_add: null keys/vals with n > 0");
-    push_pieces(va, b, (size_t)s->vb);
-  }
-  for (auto& b : gets) {
-    if (b.n == 0) continue;
-    if (!b.keys || !b.vals) return fail(PSKV_EINVAL, "pskv_get: null keys/out with n > 0");
-    push_pieces(vg, b, (size_t)s->vb);
-  }
-  bool vec = true;
-  for (auto& b : va) vec &= aligned16(b.keys) & aligned16(b.vals);
-  for (auto& b : vg) vec &= aligned16(b.keys) & aligned16(b.vals);
-  const bool fuse = s->tune_fuse && (flags & PSKV_DEVICE) && (flags & PSKV_SORTED_HINT) &&
-                    s->mode == PSKV_ASSIGN && s->vb == 4 && s->tune_unroll == 8 && s->tune_nt && vec &&
-                    !va.empty() && !vg.empty();
-  if (!fuse) {
-    int rc = add_impl(s, adds, flags);
-    if (rc) return rc;
-    return get_impl(s, gets, flags & ~PSKV_SORTED_HINT);
-  }
-  s->n_add++;
-  s->n_get++;
-  int rc = use_device(s);
+  int rc = add_impl(s, adds, flags);
   if (rc) return rc;
-  rc = srv_stop(s);
-  if (rc) return rc;
-  if (!s->fuse_grid_max) {
-    s->fuse_grid_max = add_get_max_grid(s->fuse_ua);
-    if (s->fuse_grid_max <= 0) return fail(PSKV_EHIP, "fused Add+Get: occupancy query failed");
-  }
-  const auto ag = split_groups(va);
-  const auto gg = split_groups(vg);
-  for (size_t i = 0; i + 1 < ag.size(); ++i) {  // all Add groups but the last: the sorted path
-    rc = sorted_add(s, va, ag[i].first, ag[i].second, true, next_epoch(s), /*repair=*/true, /*maybe_windows=*/true);
-    if (rc) return rc;
-  }
-  {
-    const uint32_t epoch = next_epoch(s);
-    const auto& a = ag.back();
-    const auto& g = gg.front();
-    GroupArgs gaa, gga;
-    const uint32_t nadd = build_group(va, a.first, a.second, stream_chunk(s->fuse_ua), &gaa);
-    const uint32_t nget = build_group(vg, g.first, g.second, stream_chunk(8), &gga);
-    uint64_t elems = 0;
-    for (size_t i = a.first; i < a.second; ++i) elems += va[i].n;
-    for (size_t i = g.first; i < g.second; ++i) elems += vg[i].n;
-    uint64_t add_elems = 0;
-    for (size_t i = a.first; i < a.second; ++i) add_elems += va[i].n;
-    uint32_t shift = 16;  // the tile mode's tiles, as sorted_add
-    while (shift > 12 && (add_elems >> shift) < 2048) --shift;
-    if (s->tune_tile_shift) shift = s->tune_tile_shift;
-    const uint64_t ntiles = (s->range + (1ull << shift) - 1) >> shift;
-    // dense mode deals nadd + nget work units over the grid; the tile mode's
-    // grid-stride over the tiles wants at least 1024 workgroups
-    const uint64_t want = std::max<uint64_t>((uint64_t)nadd + nget, std::min<uint64_t>(ntiles, 1024));
-    const uint32_t grid = (uint32_t)std::min<uint64_t>(want, (uint64_t)s->fuse_grid_max);
-    s->bar_count += grid;
-    unsigned long long* bar = reinterpret_cast<unsigned long long*>(s->flag + 2);
-    {
-      LaunchTimer t(s, PSKV_K_ADD_GET, elems);
-      PSKV_HIP(launch_add_get(s->fuse_ua, s->tune_ntp, gaa, gga, s->dview(), s->ovf, shift, ntiles, grid, s->flag,
-                              epoch, bar, s->bar_count, s->stream));
-      t.done();
-    }
-    {
-      LaunchTimer t(s, PSKV_K_REPLAY, add_elems);
-      PSKV_HIP(launch_replay_get(gaa, gga, s->dview(), s->ovf, s->flag, epoch, s->stream));
-      t.done();
-    }
-    s->n_sorted++;
-    s->n_general++;
-  }
-  for (size_t i = 1; i < gg.size(); ++i) {  // the other Get groups: K1
-    GroupArgs ga;
-    const uint32_t nwg = build_group(vg, gg[i].first, gg[i].second, stream_chunk(gather_unroll(s)), &ga);
-    uint64_t elems = 0;
-    for (size_t k = gg[i].first; k < gg[i].second; ++k) elems += vg[k].n;
-    LaunchTimer t(s, PSKV_K_GATHER, elems);
-    PSKV_HIP(launch_gather(s->vb, true, gather_unroll(s), s->tune_nt, ga, nwg, s->dview(), s->ovf,
-                           s->stream));
-    t.done();
-  }
-  return PSKV_OK;
+  return get_impl(s, gets, flags & ~PSKV_SORTED_HINT);
 }
 
 // ------------------------------------------------------------- options
@@ -1878,7 +1783,6 @@ const Option kOptions[] = {
     PSKV_OPT("UNROLL", 4, 8, tune_unroll, int),              // 4 or 8 (others: 8)
     PSKV_OPT("NT", 0, 1, tune_nt, bool),
     PSKV_OPT("NTP", 0, 1, tune_ntp, bool),
-    PSKV_OPT("FUSE", 0, 1, tune_fuse, bool),
     PSKV_OPT("EARLY", 0, 2, tune_early, int),
     PSKV_OPT("PAGEABLE_DMA", 0, 1, tune_pageable_dma, bool),
     PSKV_OPT("DMA_MIN_BYTES", 0, INT64_MAX, tune_dma_min_bytes, size_t),
@@ -2030,10 +1934,9 @@ int pskv_shard_create_ex(int device, uint32_t key_begin, uint64_t key_end, int d
     return bail(fail(PSKV_ENOMEM, "dense parameter allocation failed"));
   if (hipMemsetAsync(s->dense, 0, s->range * (size_t)vb, s->stream) != hipSuccess)
     return bail(fail(PSKV_EHIP, "hipMemsetAsync failed"));
-  // flag[0]: the sorted path's verification tag; flag[2..3]: K10's barrier
-  // counter (u64, monotonic)
-  if (hipMalloc(&s->flag, 64) != hipSuccess) return bail(fail(PSKV_ENOMEM, "flag allocation failed"));
-  if (hipMemsetAsync(s->flag, 0, 64, s->stream) != hipSuccess)
+  // flag[0]: the sorted path's verification tag
+  if (hipMalloc(&s->flag, 16) != hipSuccess) return bail(fail(PSKV_ENOMEM, "flag allocation failed"));
+  if (hipMemsetAsync(s->flag, 0, 16, s->stream) != hipSuccess)
     return bail(fail(PSKV_EHIP, "hipMemsetAsync failed"));
   s->ocap = next_pow2(std::max<uint64_t>(overflow_slots ? overflow_slots : kDefaultOverflowSlots, 64));
   rc = alloc_overflow(&s->ovf, s->ocap, vb, s->stream);

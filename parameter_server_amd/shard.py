@@ -150,8 +150,8 @@ class Shard:
     def add_get_grouped(self, adds, gets, sorted_hint: bool = False):
         """add_grouped(adds) then get_grouped(gets) in ONE call (pskv_add_get_grouped:
         the BSP model's flush then the Gets it releases, or a worker round's push
-        then pull).  Device batches under the sorted hint run as one fused
-        launch (option FUSE).  adds / gets: batch lists or BatchSets."""
+        then pull); the hint applies to the Adds.  adds / gets: batch lists or
+        BatchSets."""
         ba = adds if isinstance(adds, BatchSet) else self.prepare(adds)
         bg = gets if isinstance(gets, BatchSet) else self.prepare(gets, is_get=True)
         if (ba.flags ^ bg.flags) & _lib.PSKV_DEVICE and ba.n and bg.n:

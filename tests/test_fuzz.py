@@ -36,7 +36,7 @@ N_GROUPS = int(os.environ.get("FUZZ_GROUPS", "4"))  # concurrent groups of 6 sha
 KNOBS = [{}, {}, {}, {"SERVE": 1}, {"GENERAL": "stamps"}, {"INLINE": 0},
          {"UNROLL": 4}, {"PAGEABLE_DMA": 1}, {"ZC_MAX_BYTES": 0},
          {"RB_APPLY_LOG2": 13}, {"RB_BIN_BLOCK": 512}, {"EARLY": 1}, {"EARLY": 0}, {"NTP": 0},
-         {"FUSE": 1}, {"FUSE": 1}]
+         {"TILE_GRID": 1024}, {"NT": 0}]
 SIZES = [0, 1, 5, 100, 256, 257, 1024, 2049, 5000, 40_000, 300_000]
 U32 = 1 << 32
 
@@ -227,9 +227,8 @@ def _run(cuda, oracle_mod, seed, rng, dt, mode, kb, ke, knobs):
                 for k, v in batches:
                     ref.add(k, v)
             elif op == "add_get_dev":
-                # pskv_add_get_grouped: under the FUSE knob the fused launch
-                # (K10) for hinted 4-byte windows, the separate paths
-                # otherwise; the pulls see the pushes of the same call
+                # pskv_add_get_grouped: the grouped Add then the grouped Get;
+                # the pulls see the pushes of the same call
                 nb = int(rng.choice([1, 5, 64, 67]))
                 dense = kind in ("dense", "lookalike")
                 adds = []

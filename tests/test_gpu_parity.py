@@ -1467,12 +1467,12 @@ def test_shard_options_api(cuda, monkeypatch, capfd):
     unknown names and out-of-range values rejected with PSKV_EINVAL (the shard
     unchanged), the environment as the creation default -- where an invalid
     value is reported on stderr and ignored, never a failed creation (ADVICE r3);
-    the options removed in round 4 (GET_DEDUP, RB_INSERT: measured losers) are
+    the options removed in round 4 (GET_DEDUP, RB_INSERT, FUSE: measured losers) are
     unknown names now."""
     import parameter_server_amd as ps
     from parameter_server_amd import PskvError, _lib
 
-    names = ["GENERAL", "UNROLL", "NT", "NTP", "FUSE", "EARLY", "PAGEABLE_DMA", "DMA_MIN_BYTES", "DMA_MIN_BYTES_GET",
+    names = ["GENERAL", "UNROLL", "NT", "NTP", "EARLY", "PAGEABLE_DMA", "DMA_MIN_BYTES", "DMA_MIN_BYTES_GET",
              "DMA_MIN_BYTES_PINNED", "ZC_MAX_BYTES", "FRAME_ZC_MAX_BYTES", "INLINE", "INLINE_ADD_CHUNKS",
              "INLINE_GET_CHUNKS", "ISPIN", "SERVE", "SERVE_IDLE_US", "TILE_SHIFT", "TILE_GRID", "RB_WBITS",
              "RB_NBD", "RB_TB", "RB_APPLY_LOG2", "RB_BIN_BLOCK"]
@@ -1486,7 +1486,7 @@ def test_shard_options_api(cuda, monkeypatch, capfd):
         sh.set_option("ZC_MAX_BYTES", 12345)
         assert sh.get_option("ZC_MAX_BYTES") == 12345
         for n, bad in (("UNROLL", 5), ("RB_APPLY_LOG2", 12), ("TILE_SHIFT", 3), ("INLINE", 2),
-                        ("RB_BIN_BLOCK", 768), ("NOPE", 1), ("GET_DEDUP", 1), ("RB_INSERT", 1), ("GET_NTP", 1)):
+                        ("RB_BIN_BLOCK", 768), ("NOPE", 1), ("GET_DEDUP", 1), ("RB_INSERT", 1), ("GET_NTP", 1), ("FUSE", 1)):
             before = sh.get_option(n) if n in names else None
             with pytest.raises(PskvError) as ei:
                 sh.set_option(n, bad)

@@ -3,7 +3,7 @@
 # first failure (gpurun runs it as: bash tools/gpu_job.sh OUTDIR STEP...).
 #   tests_focus  the parity tests of the dense / repair / golden / replay paths
 #   tests_all    pytest -m gpu (everything)
-#   tests_fused  the fused Add + Get tests, the bench-form and two-rank cfg-4 tests, options
+#   tests_addget the push-then-pull call tests, the bench-form and two-rank cfg-4 tests, options
 #   align        tools/align_probe.py (window phase cost)
 #   emu          bench.py as rank 0 of 8 and of 2 (one rank's cfg-4 share alone)
 #   emu8all      bench.py as each of the 8 ranks of N = 8 in turn (every rank's cfg-4 share alone)
@@ -27,19 +27,14 @@
 #   fuzz2        1500 more fuzz seeds from 5000 and 8 concurrent groups (the EARLY knob and look-alikes in play)
 #   align_own    tools/align_probe.py with K2g slot-aligned chunks (EARLY=0) vs own-range chunks (EARLY=3), twice
 #   zwbits       K5 bucket windows of 2^11 (default) vs 2^12 keys on cfg-3 Zipf and on unhinted dense pushes
-#   rbins        K5a per-lane probe insert (RB_INSERT=1): the K5 parity tests under it, then the cfg-3 A/B
 #   coldmicro    tools/micro/cold_stream: HBM ceilings of the dense step's access shapes, every byte cold
 #   coldbench    bench.py --cold-only (the headline step on a 1e9-key shard: roofline.cold's form)
-#   coldopts     the cold form under cache-policy options (GET_NTP, NTP, both, NT=0)
-#   ntp_ab       the headline (and its cold form) with K2g parameter stores and K1 parameter loads cached / nt, twice
+#   coldopts     the cold form under cache-policy options (NTP off, NT off)
+#   ntp_ab       the headline (and its cold form) with K2g parameter stores cached / nt, twice
 #   emu_ntp      every rank of N = 8 emulated, K2g parameter stores cached / non-temporal
-#   emu8_fuse    every rank of N = 8 emulated with the fused Add + Get launch on / off
-#   emu8_fuse_ua every rank of N = 8: separate launches, fused with 8 Ki-key and with 4 Ki-key Add chunks
-#   bench_fuse_ua the headline (+ cold form) the same three ways
 #   k2g_tune     the headline (+ cold form) under K2g grid / early-load / unroll variants
 #   smoke        __graft_entry__.smoke() (what the driver runs before the bench)
 #   shardsize    tools/shard_size_probe.py: K2g / K1 per key on 1e8 / 5e8 / 1e9-key shards (same windows)
-#   getntp       tools/shard_size_probe.py with K1 parameter loads cached / non-temporal (GET_NTP=0/1), twice
 #   e2e          tools/e2e_probe.py (host-buffer Add / Get against raw PCIe copy rates)
 #   bench        bench.py --steps 20 (the driver's command line)
 #   zipf         tools/zipf_probe.py kernel times on cfg 3
@@ -61,9 +56,10 @@ for step in "$@"; do
     tests_focus) timeout -k 10 300 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread \
         "$R/tests/test_gpu_parity.py" "$R/tests/test_replay.py" \
         -k "phase or dense or lookalike or repaired or hint or golden or replay or options or dedup or zipf or radix or sentinel or random" > "$OUT/tests_focus.log" 2>&1 ;;
-    tests_fused) timeout -k 10 400 python3 -u -m pytest -x -v --timeout 200 --timeout-method thread \
-        "$R/tests/test_fused.py" "$R/tests/test_dist_gpu.py" "$R/tests/test_gpu_parity.py" \
-        -k "fused or cfg4 or headline or options or zipf_pulls" > "$OUT/tests_fused.log" 2>&1 ;;
+    tests_addget) timeout -k 10 600 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread \
+        "$R/tests/test_add_get.py" "$R/tests/test_dist_gpu.py" "$R/tests/test_gpu_parity.py" \
+        "$R/tests/test_bench_multirank_gpu.py" -k "add_get or cfg4 or headline or options or zipf_pulls or two_ranks" \
+        > "$OUT/tests_addget.log" 2>&1 ;;
     tests_all) timeout -k 10 900 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread "$R/tests" -m gpu \
         > "$OUT/tests_all.log" 2>&1 ;;
     align) timeout -k 10 200 python3 "$R/tools/align_probe.py" 0,1,2,3 20 > "$OUT/align.log" 2>&1 ;;
@@ -124,20 +120,16 @@ for step in "$@"; do
     zwbits) PROBE_ROUNDS=10 timeout -k 10 300 python3 "$R/tools/zipf_probe.py" "" "PSKV_RB_WBITS=12" > "$OUT/zwbits_zipf.log" 2>&1 &&
         PROBE_ROUNDS=10 PROBE_WORKLOAD=dense timeout -k 10 300 python3 "$R/tools/zipf_probe.py" "" "PSKV_RB_WBITS=12" \
           > "$OUT/zwbits_dense.log" 2>&1 ;;
-    rbins) PSKV_RB_INSERT=1 timeout -k 10 400 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread \
-          "$R/tests/test_gpu_parity.py" -k "zipf or radix or random or golden or accumulate or sentinel or ragged" \
-          > "$OUT/rbins_tests.log" 2>&1 &&
-        PROBE_ROUNDS=10 timeout -k 10 300 python3 "$R/tools/zipf_probe.py" "" "PSKV_RB_INSERT=1" > "$OUT/rbins_zipf.log" 2>&1 ;;
     coldmicro) timeout -k 10 200 "$R/tools/micro/cold_stream" > "$OUT/cold_stream.log" 2>&1 ;;
     coldbench) timeout -k 10 300 python3 "$R/bench.py" --cold-only --steps 50 > "$OUT/cold.json" 2> "$OUT/cold.err" ;;
-    coldopts) for o in "" "PSKV_GET_NTP=1" "PSKV_NTP=1" "PSKV_GET_NTP=1 PSKV_NTP=1" "PSKV_NT=0"; do
+    coldopts) for o in "" "PSKV_NTP=0" "PSKV_NT=0"; do
           tag=$(echo "x$o" | tr ' =' '__')
           env $o timeout -k 10 300 python3 "$R/bench.py" --cold-only --steps 50 > "$OUT/cold$tag.json" 2> "$OUT/cold$tag.err" || exit 1
         done ;;
-    ntp_ab) for r in 1 2; do for e in 0 1; do for g in 0 1; do
-          PSKV_NTP=$e PSKV_GET_NTP=$g timeout -k 10 300 python3 "$R/bench.py" --steps 50 --no-zipf --no-extra \
-            --no-cpu-baseline > "$OUT/ntp${e}_getntp${g}_$r.json" 2> "$OUT/ntp${e}_getntp${g}_$r.err" || exit 1
-        done; done; done ;;
+    ntp_ab) for r in 1 2; do for e in 0 1; do
+          PSKV_NTP=$e timeout -k 10 300 python3 "$R/bench.py" --steps 50 --no-zipf --no-extra \
+            --no-cpu-baseline > "$OUT/ntp${e}_$r.json" 2> "$OUT/ntp${e}_$r.err" || exit 1
+        done; done ;;
     emu_ntp) for r in 0 1 2 3 4 5 6 7; do for e in 0 1; do
           PSKV_NTP=$e PSKV_BENCH_EMULATE=$r/8 timeout -k 10 200 python3 "$R/bench.py" --steps 50 --no-zipf \
             --no-cpu-baseline --no-extra > "$OUT/emu8_${r}_ntp$e.json" 2> "$OUT/emu8_${r}_ntp$e.err" || exit 1
@@ -148,31 +140,15 @@ for step in "$@"; do
           env $o timeout -k 10 300 python3 "$R/bench.py" --steps 50 --no-zipf --no-extra --no-cpu-baseline \
             > "$OUT/tune$tag.json" 2> "$OUT/tune$tag.err" || exit 1
         done ;;
-    emu8_fuse_ua) for r in 0 1 2 3 4 5 6 7; do for v in "0 8" "1 8" "1 4"; do set -- $v
-          PSKV_FUSE=$1 PSKV_PROBE_FUSE_UA=$2 PSKV_BENCH_EMULATE=$r/8 timeout -k 10 200 python3 "$R/bench.py" --steps 50 \
-            --no-zipf --no-cpu-baseline --no-extra > "$OUT/emu8_${r}_fuse$1_ua$2.json" 2> "$OUT/emu8_${r}_fuse$1_ua$2.err" \
-            || exit 1
-        done; done ;;
-    bench_fuse_ua) for v in "0 8" "1 8" "1 4"; do set -- $v
-          PSKV_FUSE=$1 PSKV_PROBE_FUSE_UA=$2 timeout -k 10 300 python3 "$R/bench.py" --steps 50 --no-zipf --no-extra \
-            --no-cpu-baseline > "$OUT/bench_fuse$1_ua$2.json" 2> "$OUT/bench_fuse$1_ua$2.err" || exit 1
-        done ;;
-    emu8_fuse) for r in 0 1 2 3 4 5 6 7; do for f in 1 0; do
-          PSKV_FUSE=$f PSKV_BENCH_EMULATE=$r/8 timeout -k 10 200 python3 "$R/bench.py" --steps 50 --no-zipf \
-            --no-cpu-baseline --no-extra > "$OUT/emu8_${r}_fuse$f.json" 2> "$OUT/emu8_${r}_fuse$f.err" || exit 1
-        done; done ;;
     smoke) timeout -k 10 300 python3 -c "import sys; sys.path.insert(0, '$R'); import __graft_entry__ as g; g.smoke()" \
         > "$OUT/smoke.log" 2>&1 ;;
     shardsize) timeout -k 10 400 python3 "$R/tools/shard_size_probe.py" > "$OUT/shard_size.log" 2>&1 &&
         FLUSH=1 timeout -k 10 400 python3 "$R/tools/shard_size_probe.py" > "$OUT/shard_size_flush.log" 2>&1 ;;
-    getntp) for r in 1 2; do for e in 0 1; do
-          PSKV_GET_NTP=$e timeout -k 10 400 python3 "$R/tools/shard_size_probe.py" > "$OUT/getntp${e}_$r.log" 2>&1 || exit 1
-        done; done ;;
     e2e) timeout -k 10 200 python3 "$R/tools/e2e_probe.py" > "$OUT/e2e.log" 2>&1 ;;
     bench) timeout -k 10 400 python3 "$R/bench.py" --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     profile) bash "$R/tools/gpu_profile.sh" "$(basename "$OUT")/prof" > "$OUT/profile.log" 2>&1 ;;
     profile_cold) MODE=cold bash "$R/tools/gpu_profile.sh" "$(basename "$OUT")/prof_cold" > "$OUT/profile_cold.log" 2>&1 ;;
-    zipf) timeout -k 10 300 python3 "$R/tools/zipf_probe.py" "" "PSKV_GET_DEDUP=1" > "$OUT/zipf.log" 2>&1 ;;
+    zipf) timeout -k 10 300 python3 "$R/tools/zipf_probe.py" "" > "$OUT/zipf.log" 2>&1 ;;
     zipf_bin) timeout -k 10 300 python3 "$R/tools/zipf_probe.py" "" "PSKV_RB_BIN_BLOCK=1024" "PSKV_RB_BIN_BLOCK=512" \
         > "$OUT/zipf_bin.log" 2>&1 ;;
     vector) timeout -k 10 600 python3 -u "$R/bench.py" --vector-only --vector-sizes 1000000 \
