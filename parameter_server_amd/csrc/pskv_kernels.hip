@@ -621,8 +621,9 @@ __device__ __forceinline__ bool dense_chunk(const GroupArgs& ga, const DenseView
 // prologue (the first and last key of every batch) has come back; it cannot
 // skip the values of a chunk a later window covers (they are already in
 // flight), so it is for small launches whose windows rarely overlap (a rank's
-// ~8 windows at N = 8).  PRE: k / v already hold the (whole) chunk.
-template <int U, bool NT, bool NTP, bool PRE>
+// ~8 windows at N = 8).  PRE: 1 = k / v already hold the (whole) chunk, 2 = k
+// does (the keys-early form: values are still skipped for a covered chunk).
+template <int U, bool NT, bool NTP, int PRE>
 __device__ __forceinline__ bool dense_chunk_own(const GroupArgs& ga, const DenseView& d, uint32_t c,
                                                 const uint32_t* s_first, const uint32_t* s_last,
                                                 uint32_t (&k)[U][4], uint32_t (&v)[U][4]) {
@@ -657,11 +658,11 @@ __device__ __forceinline__ bool dense_chunk_own(const GroupArgs& ga, const Dense
     const uint32_t* __restrict__ kc = keys + base;
     const uint32_t* __restrict__ vc = vals + base;
     uint32_t* __restrict__ pc = param + p0 + base;
-    if (!PRE) {
+    if (PRE != 1) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t o = (uint32_t)(u * kBlock + tid) * 4u;
-        Vec4<uint32_t>::load<NT>(kc + o, k[u]);
+        if (PRE == 0) Vec4<uint32_t>::load<NT>(kc + o, k[u]);
         if (!covered) Vec4<uint32_t>::load<NT>(vc + o, v[u]);
       }
     }
@@ -788,7 +789,9 @@ __device__ __forceinline__ bool tile_mode(const GroupArgs& ga, const DenseView& 
 }
 
 // Mode B (general sorted batches): key-tile owner, static strided schedule.
-template <typename VT, bool VEC, int U, bool NT, bool NTP, bool EARLY = false>
+// EARLY: 0 = loads after the prologue; 1 = the first chunk's keys and values
+// before it; 2 = its keys only (a covered chunk still skips its values).
+template <typename VT, bool VEC, int U, bool NT, bool NTP, int EARLY = 0>
 __global__ __launch_bounds__(kBlock) void k_assign_group(GroupArgs ga, DenseView d,
                                                          uint32_t tile_shift, uint64_t ntiles,
                                                          uint32_t* flag, uint32_t epoch) {
@@ -806,7 +809,7 @@ __global__ __launch_bounds__(kBlock) void k_assign_group(GroupArgs ga, DenseView
   // before the prologue below (its loads need no batch endpoint)
   uint32_t ek[OWN ? U : 1][4], ev[OWN ? U : 1][4];
   bool pre = false;
-  if constexpr (EARLY) {
+  if constexpr (EARLY != 0) {
     if (blockIdx.x < ga.wg_prefix[ga.nb]) {
       const int j0 = batch_of(ga, blockIdx.x);
       const uint64_t base0 = (uint64_t)(blockIdx.x - ga.wg_prefix[j0]) * CH;
@@ -818,7 +821,7 @@ __global__ __launch_bounds__(kBlock) void k_assign_group(GroupArgs ga, DenseView
         for (int u = 0; u < U; ++u) {
           const uint32_t o = (uint32_t)(u * kBlock + tid) * 4u;
           Vec4<uint32_t>::load<NT>(kc + o, ek[u]);
-          Vec4<uint32_t>::load<NT>(vc + o, ev[u]);
+          if (EARLY == 1) Vec4<uint32_t>::load<NT>(vc + o, ev[u]);
         }
       }
     }
@@ -831,11 +834,11 @@ __global__ __launch_bounds__(kBlock) void k_assign_group(GroupArgs ga, DenseView
     if constexpr (OWN) {
       uint32_t c = blockIdx.x;
       if (pre) {
-        bad |= dense_chunk_own<U, NT, NTP, true>(ga, d, c, s_first, s_last, ek, ev);
+        bad |= dense_chunk_own<U, NT, NTP, EARLY>(ga, d, c, s_first, s_last, ek, ev);
         c += gridDim.x;
       }
       for (; c < nchunks; c += gridDim.x)
-        bad |= dense_chunk_own<U, NT, NTP, false>(ga, d, c, s_first, s_last, ek, ev);
+        bad |= dense_chunk_own<U, NT, NTP, 0>(ga, d, c, s_first, s_last, ek, ev);
     } else {
       for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x)
         bad |= dense_chunk<VT, VEC, U, NT, NTP>(ga, d, c, s_first, s_last);
@@ -2462,12 +2465,15 @@ hipError_t launch_assign_sorted(int vb, bool vec, const uint32_t* keys, const vo
 }
 
 template <typename VT, bool VEC, bool NTP>
-static void group_dispatch2(int unroll, bool nt, bool early, uint32_t grid, const GroupArgs& ga,
+static void group_dispatch2(int unroll, bool nt, int early, uint32_t grid, const GroupArgs& ga,
                             const DenseView& d, uint32_t shift, uint64_t ntiles, uint32_t* flag,
                             uint32_t epoch, hipStream_t st) {
   if constexpr (sizeof(VT) == 4 && VEC) {
     if (early && unroll == 8 && nt) {  // early mode: the default unroll and streams only
-      k_assign_group<VT, VEC, 8, true, NTP, true><<<grid, kBlock, 0, st>>>(ga, d, shift, ntiles, flag, epoch);
+      if (early == 1)
+        k_assign_group<VT, VEC, 8, true, NTP, 1><<<grid, kBlock, 0, st>>>(ga, d, shift, ntiles, flag, epoch);
+      else
+        k_assign_group<VT, VEC, 8, true, NTP, 2><<<grid, kBlock, 0, st>>>(ga, d, shift, ntiles, flag, epoch);
       return;
     }
   }
@@ -2485,7 +2491,7 @@ static void group_dispatch2(int unroll, bool nt, bool early, uint32_t grid, cons
 }
 
 template <typename VT, bool VEC>
-static void group_dispatch(int unroll, bool nt, bool ntp, bool early, uint32_t grid, const GroupArgs& ga,
+static void group_dispatch(int unroll, bool nt, bool ntp, int early, uint32_t grid, const GroupArgs& ga,
                            const DenseView& d, uint32_t shift, uint64_t ntiles, uint32_t* flag,
                            uint32_t epoch, hipStream_t st) {
   if (ntp)
@@ -2494,7 +2500,7 @@ static void group_dispatch(int unroll, bool nt, bool ntp, bool early, uint32_t g
     group_dispatch2<VT, VEC, false>(unroll, nt, early, grid, ga, d, shift, ntiles, flag, epoch, st);
 }
 
-hipError_t launch_assign_group(int vb, bool vec, int unroll, bool nt, bool ntp, bool early,
+hipError_t launch_assign_group(int vb, bool vec, int unroll, bool nt, bool ntp, int early,
                                const GroupArgs& ga,
                                const DenseView& d, uint32_t tile_shift, uint64_t ntiles,
                                uint32_t grid, uint32_t* flag, uint32_t epoch, hipStream_t st) {

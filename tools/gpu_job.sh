@@ -13,6 +13,7 @@
 #   ztrace       rocprofv3 kernel trace of zipf_probe at K5a 1024 and 512 threads (K5a / K5b split)
 #   zpmc         tools/zipf_pmc.sh: wave-state, LDS and HBM counters of the cfg-3 path
 #   k5phases     tools/micro/k5_phases (diagnostic build: K5a / K5b phase stamps), assign and accumulate
+#   k5dist       the same (assign) on Zipf keys, uniform keys and a uniform pool matched to Zipf's distinct count
 #   abz          tools/ab_lib.sh with AB_PROG=zipf: ab/libpskv_base.so vs ab/libpskv_new.so on cfg 3, 3 rounds each
 #   sizes        tools/size_probe.py: K2g / K1 time against window count (fixed cost per launch)
 #   abs          tools/ab_lib.sh with AB_PROG=sizes: base vs new library under tools/size_probe.py
@@ -88,6 +89,9 @@ for step in "$@"; do
     zpmc) timeout -k 10 600 bash "$R/tools/zipf_pmc.sh" "$(basename "$OUT")/zpmc" > "$OUT/zpmc.log" 2>&1 ;;
     k5phases) timeout -k 10 200 "$R/tools/micro/k5_phases" 0 > "$OUT/k5_phases_assign.log" 2>&1 &&
         timeout -k 10 200 "$R/tools/micro/k5_phases" 1 > "$OUT/k5_phases_accumulate.log" 2>&1 ;;
+    k5dist) for dist in zipf uniform matched; do
+          timeout -k 10 200 "$R/tools/micro/k5_phases" 0 $dist > "$OUT/k5_phases_$dist.log" 2>&1 || exit 1
+        done ;;
     ldsrand) timeout -k 10 120 "$R/tools/micro/lds_atomic_rand" > "$OUT/lds_atomic_rand.log" 2>&1 ;;
     abz) AB_PROG=zipf timeout -k 10 900 bash "$R/tools/ab_lib.sh" "$(basename "$OUT")/abz" > "$OUT/abz.log" 2>&1 ;;
     sizes) timeout -k 10 300 python3 "$R/tools/size_probe.py" > "$OUT/size_probe.log" 2>&1 ;;
@@ -134,7 +138,7 @@ for step in "$@"; do
           PSKV_NTP=$e PSKV_BENCH_EMULATE=$r/8 timeout -k 10 200 python3 "$R/bench.py" --steps 50 --no-zipf \
             --no-cpu-baseline --no-extra > "$OUT/emu8_${r}_ntp$e.json" 2> "$OUT/emu8_${r}_ntp$e.err" || exit 1
         done; done ;;
-    k2g_tune) for o in "" "PSKV_TILE_GRID=1024" "PSKV_TILE_GRID=2048" "PSKV_TILE_GRID=8192" "PSKV_EARLY=1" \
+    k2g_tune) for o in "" "PSKV_TILE_GRID=1024" "PSKV_TILE_GRID=2048" "PSKV_TILE_GRID=8192" "PSKV_EARLY=1" "PSKV_EARLY=3" \
           "PSKV_UNROLL=4"; do
           tag=$(echo "x$o" | tr ' =' '__')
           env $o timeout -k 10 300 python3 "$R/bench.py" --steps 50 --no-zipf --no-extra --no-cpu-baseline \

@@ -4,7 +4,16 @@
 // Keys: 8 x 1M Zipf(0.99) ranks (inverse CDF) mapped through a seeded
 // permutation of [0, 1e8), as workload.zipf_batches draws them (not the same
 // stream: std::mt19937_64, so statistics match, values do not).
-//   bash tools/micro/build_k5_phases.sh && tools/micro/k5_phases
+// A second argument picks the key distribution, to tell what the hot keys of
+// Zipf cost the insert phase:
+//   zipf     (default) as above
+//   uniform  uniform over the 1e8 keys (no hot keys, ~every key distinct)
+//   matched  uniform over a pool sized so a super-chunk of 8 Ki keys holds as
+//            many distinct keys as a Zipf super-chunk does (same duplicate
+//            count, spread evenly: no key hotter than another)
+//   bash tools/micro/build_k5_phases.sh && tools/micro/k5_phases [mode] [dist]
+#include <cstring>
+#include <unordered_set>
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -28,6 +37,7 @@ int main(int argc, char** argv) {
   const uint64_t space = 100000000ull;
   const int J = 8, B = 1000000, reps = 6;
   const int mode = argc > 1 ? std::atoi(argv[1]) : PSKV_ASSIGN;
+  const char* dist = argc > 2 ? argv[2] : "zipf";
   std::vector<double> cdf(space);
   double acc = 0;
   for (uint64_t r = 0; r < space; ++r) cdf[r] = (acc += std::pow((double)(r + 1), -0.99));
@@ -45,6 +55,39 @@ int main(int argc, char** argv) {
       keys[j][i] = perm[rank];
       vals[j][i] = (float)u01(rng);
     }
+  // distinct keys per 8 Ki-key super-chunk (K5a's unit for 4-byte values)
+  auto distinct_per_sc = [&]() {
+    double tot = 0;
+    int n = 0;
+    for (int j = 0; j < J; ++j)
+      for (int b = 0; b + 8192 <= B; b += 8192) {
+        std::unordered_set<uint32_t> u(keys[j].begin() + b, keys[j].begin() + b + 8192);
+        tot += (double)u.size();
+        ++n;
+      }
+    return tot / n;
+  };
+  const double zipf_distinct = distinct_per_sc();
+  if (std::strcmp(dist, "uniform") == 0 || std::strcmp(dist, "matched") == 0) {
+    uint64_t pool = space;
+    if (dist[0] == 'm') {
+      // pool S with S * (1 - exp(-8192 / S)) = the Zipf super-chunk's distinct count
+      double lo = zipf_distinct, hi = 1e9;
+      for (int it = 0; it < 200; ++it) {
+        const double mid = 0.5 * (lo + hi);
+        (mid * (1.0 - std::exp(-8192.0 / mid)) < zipf_distinct ? lo : hi) = mid;
+      }
+      pool = (uint64_t)std::llround(lo);
+    }
+    std::uniform_int_distribution<uint64_t> pick(0, pool - 1);
+    for (int j = 0; j < J; ++j)
+      for (int i = 0; i < B; ++i) keys[j][i] = perm[pick(rng)];
+    std::printf("keys: %s (pool %llu)\n", dist, (unsigned long long)pool);
+  } else if (std::strcmp(dist, "zipf") != 0) {
+    std::fprintf(stderr, "dist: zipf, uniform or matched\n");
+    return 2;
+  }
+  std::printf("distinct keys per 8 Ki-key super-chunk: %.0f (Zipf: %.0f)\n", distinct_per_sc(), zipf_distinct);
   cdf.clear();
   cdf.shrink_to_fit();
   pskv_shard* s = nullptr;
@@ -80,8 +123,8 @@ int main(int argc, char** argv) {
   const char* na[] = {"insert (CAS + max/add)", "keep check + bucket count", "bucket scan",
                       "row + staging", "copy-out + clear", "next pass"};
   const char* nb[] = {"run wait + totals", "direct passes", "stores + next loads"};
-  std::printf("mode %s, 8 x 1M Zipf(0.99) keys over 1e8, %d timed Adds; shader-clock cycles per phase\n",
-              mode == PSKV_ASSIGN ? "assign" : "accumulate", reps - 1);
+  std::printf("mode %s, 8 x 1M %s keys over 1e8, %d timed Adds; shader-clock cycles per phase\n",
+              mode == PSKV_ASSIGN ? "assign" : "accumulate", dist, reps - 1);
   for (int k = 0; k < 2; ++k) {
     std::printf("%s\n", k == 0 ? "K5a k_rb_bin (per super-chunk pass)" : "K5b k_rb_resolve (per bucket)");
     const int nph = k == 0 ? 5 : 3;
