@@ -903,13 +903,19 @@ def cold_form(dev, J, B, R, steps, warmup, space, n_pulls):
 
     import parameter_server_amd as ps
 
-    sets = [make_set(0, 1, J, B, dev, r, space=space, n_pull=n_pulls[r % len(n_pulls)]) for r in range(R)]
+    sets = []
+    for r in range(R):
+        sets.append(make_set(0, 1, J, B, dev, r, space=space, n_pull=n_pulls[r % len(n_pulls)]))
+        progress(f"cold form: set {r + 1} of {R} built")
     assert all(overlap_keys(s) == 0 for s in sets)
     with ps.Shard(0, space, np.float32, device=dev.index) as sh:
+        progress("cold form: shard created")
         sh.set_stream(torch.cuda.current_stream().cuda_stream)
         f = Form(sh, sets, dev)
         f.self_check(0, space, dev)
+        progress("cold form: self-check done")
         res = run_form(f, steps, max(warmup, R), 1, dev)
+        progress("cold form: timed steps done")
         kt, ev_s = evented(f, steps, 1, dev)
         sh.set_stream(None)
     a, g = f.bytes(steps)

@@ -791,8 +791,14 @@ __device__ __forceinline__ bool tile_mode(const GroupArgs& ga, const DenseView& 
 // Mode B (general sorted batches): key-tile owner, static strided schedule.
 // EARLY: 0 = loads after the prologue; 1 = the first chunk's keys and values
 // before it; 2 = its keys only (a covered chunk still skips its values).
+// PSKV_K2G_WAVES (A/B builds only, tools/ab_lib.sh): a waves-per-SIMD floor.
+#ifdef PSKV_K2G_WAVES
+#define PSKV_K2G_ATTR __attribute__((amdgpu_waves_per_eu(PSKV_K2G_WAVES)))
+#else
+#define PSKV_K2G_ATTR
+#endif
 template <typename VT, bool VEC, int U, bool NT, bool NTP, int EARLY = 0>
-__global__ __launch_bounds__(kBlock) void k_assign_group(GroupArgs ga, DenseView d,
+__global__ __launch_bounds__(kBlock) PSKV_K2G_ATTR void k_assign_group(GroupArgs ga, DenseView d,
                                                          uint32_t tile_shift, uint64_t ntiles,
                                                          uint32_t* flag, uint32_t epoch) {
   constexpr bool OWN = sizeof(VT) == 4 && VEC;  // dense_chunk_own
