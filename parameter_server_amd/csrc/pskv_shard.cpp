@@ -255,7 +255,10 @@ struct pskv_shard {
   int general_path = 1;  // PSKV_GENERAL: stamps = 0 (K4 always), auto = 1, radix = 2 (K5 always)
   // tuning knobs (environment, read at creation): PSKV_TILE_SHIFT, PSKV_TILE_GRID
   uint32_t tune_tile_shift = 0;
-  uint32_t tune_tile_grid = 4096;
+  // grid cap of K2g / K7: one workgroup per dense-mode chunk up to 512 Mi keys
+  // (round 4: at 4096 a workgroup took two of cfg 2's 8192 chunks, K2g 112.7
+  // against 111.4 us; 2048 / 1024: 116.5 / 117.3; profiles/r04_probes/k2g_tune/)
+  uint32_t tune_tile_grid = 65536;
   int tune_unroll = 8;   // PSKV_UNROLL: 4 or 8 (8: measured +5 % on the dense Add)
   bool tune_nt = true;   // PSKV_NT: non-temporal streams (measured +12-15 % on K1 / K2g)
   // PSKV_NTP: non-temporal parameter stores in the dense Add (K2g).  On

@@ -43,6 +43,7 @@
 #   zipf_bin     the same for K5a at 1024- and 512-thread workgroups
 #   profile      tools/gpu_profile.sh: rocprofv3 kernel trace + stats, FETCH / WRITE PMC passes (headline)
 #   profile_cold the same for the cold form (bench.py --cold-only)
+#   pmcprobe     tools/pmc_shard_probe.py under one --pmc pass (where the cold form's PMC pass stops)
 #   vector       bench.py --vector-only at 1e6 keys (config 1's VectorStorage restatement, CPU, once)
 #   asan         tools/asan_build.sh (host ASan + UBSan) and the C++ boundary programs under it
 set -o pipefail
@@ -140,8 +141,7 @@ for step in "$@"; do
           PSKV_NTP=$e PSKV_BENCH_EMULATE=$r/8 timeout -k 10 200 python3 "$R/bench.py" --steps 50 --no-zipf \
             --no-cpu-baseline --no-extra > "$OUT/emu8_${r}_ntp$e.json" 2> "$OUT/emu8_${r}_ntp$e.err" || exit 1
         done; done ;;
-    k2g_tune) for o in "" "PSKV_TILE_GRID=1024" "PSKV_TILE_GRID=2048" "PSKV_TILE_GRID=8192" "PSKV_EARLY=1" "PSKV_EARLY=3" \
-          "PSKV_UNROLL=4"; do
+    k2g_tune) for o in "" "PSKV_TILE_GRID=4096" "PSKV_UNROLL=4" "PSKV_TILE_GRID=8192"; do
           tag=$(echo "x$o" | tr ' =' '__')
           env $o timeout -k 10 300 python3 "$R/bench.py" --steps 50 --no-zipf --no-extra --no-cpu-baseline \
             > "$OUT/tune$tag.json" 2> "$OUT/tune$tag.err" || exit 1
@@ -157,6 +157,8 @@ for step in "$@"; do
     zipf) timeout -k 10 300 python3 "$R/tools/zipf_probe.py" "" > "$OUT/zipf.log" 2>&1 ;;
     zipf_bin) timeout -k 10 300 python3 "$R/tools/zipf_probe.py" "" "PSKV_RB_BIN_BLOCK=1024" "PSKV_RB_BIN_BLOCK=512" \
         > "$OUT/zipf_bin.log" 2>&1 ;;
+    pmcprobe) timeout -k 5 -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcprobe" -o fetch \
+          -- python3 "$R/tools/pmc_shard_probe.py" > "$OUT/pmcprobe.log" 2>&1 ;;
     vector) timeout -k 10 600 python3 -u "$R/bench.py" --vector-only --vector-sizes 1000000 \
         > "$OUT/vector_1e6.json" 2> "$OUT/vector_1e6.err" ;;
     asan) SAN=address,undefined timeout -k 10 400 bash "$R/tools/asan_build.sh" > "$OUT/asan_build.log" 2>&1 &&
