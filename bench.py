@@ -908,6 +908,7 @@ def cold_form(dev, J, B, R, steps, warmup, space, n_pulls):
         sets.append(make_set(0, 1, J, B, dev, r, space=space, n_pull=n_pulls[r % len(n_pulls)]))
         progress(f"cold form: set {r + 1} of {R} built")
     assert all(overlap_keys(s) == 0 for s in sets)
+    progress("cold form: creating the shard")
     with ps.Shard(0, space, np.float32, device=dev.index) as sh:
         progress("cold form: shard created")
         sh.set_stream(torch.cuda.current_stream().cuda_stream)

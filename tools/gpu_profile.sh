@@ -19,9 +19,9 @@ else
 fi
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT" -o trace -- \
   python3 "$R/bench.py" $ARGS > "$OUT/trace.log" 2>&1 || exit 1
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT" -o fetch -- \
+timeout -k 5 -s KILL 170 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT" -o fetch -- \
   python3 "$R/bench.py" $ARGS > "$OUT/fetch.log" 2>&1 || exit 2
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT" -o write -- \
+timeout -k 5 -s KILL 170 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT" -o write -- \
   python3 "$R/bench.py" $ARGS > "$OUT/write.log" 2>&1 || exit 3
 python3 "$R/tools/collect_pmc.py" "$OUT/fetch_counter_collection.csv" \
   "$OUT/write_counter_collection.csv" "$OUT/pmc.json" "$CONFIG" > /dev/null || exit 4
