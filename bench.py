@@ -908,7 +908,8 @@ def cold_form(dev, J, B, R, steps, warmup, space, n_pulls):
         sets.append(make_set(0, 1, J, B, dev, r, space=space, n_pull=n_pulls[r % len(n_pulls)]))
         progress(f"cold form: set {r + 1} of {R} built")
     assert all(overlap_keys(s) == 0 for s in sets)
-    progress("cold form: creating the shard")
+    torch.cuda.synchronize()
+    progress("cold form: sets resident; creating the shard")
     with ps.Shard(0, space, np.float32, device=dev.index) as sh:
         progress("cold form: shard created")
         sh.set_stream(torch.cuda.current_stream().cuda_stream)
@@ -976,16 +977,17 @@ def main(argv=None):
     prank, pworld = rank, world
     if os.environ.get("PSKV_BENCH_EMULATE") and world == 1:
         prank, pworld = (int(x) for x in os.environ["PSKV_BENCH_EMULATE"].split("/"))
-    sets = [make_set(prank, pworld, J, B, dev, r) for r in range(R)]
-    assert all(overlap_keys(s) == 0 for s in sets), "a pull set overlaps its push set"
-    n_pulls = [len(s["pull"]) for s in sets]
     if args.cold_only:
+        # the cold form pulls as many windows as cfg 2's set r: host planning only
         progress("cold form only")
-        del sets
+        n_pulls = [len(plan_pull(0, 1, J, B, r, plan_rank(0, 1, J, B, r)[4])[0]) for r in range(R)]
         rec = cold_form(dev, J, B, R, args.steps, args.warmup, int(args.cold_keys), n_pulls)
         json_out.write(json.dumps({"cold": rec}) + "\n")
         json_out.flush()
         return
+    sets = [make_set(prank, pworld, J, B, dev, r) for r in range(R)]
+    assert all(overlap_keys(s) == 0 for s in sets), "a pull set overlaps its push set"
+    n_pulls = [len(s["pull"]) for s in sets]
     key_space, lo, hi = plan_rank(prank, pworld, J, B)[:3]
     stream = torch.cuda.current_stream()
     shard = ps.Shard(lo, hi, np.float32, device=local)

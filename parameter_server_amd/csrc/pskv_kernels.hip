@@ -832,7 +832,7 @@ __global__ __launch_bounds__(kBlock) PSKV_K2G_ATTR void k_assign_group(GroupArgs
       }
     }
   }
-  const GroupEnds g = group_prologue(ga, d, flag, epoch, s_first, s_last, &s_dense);
+  (void)group_prologue(ga, d, flag, epoch, s_first, s_last, &s_dense);
   __syncthreads();
   bool bad = false;
   if (s_dense) {
@@ -851,6 +851,20 @@ __global__ __launch_bounds__(kBlock) PSKV_K2G_ATTR void k_assign_group(GroupArgs
     }
     if (bad) *flag = epoch;
     return;
+  }
+  // the endpoints again, from LDS and the arguments: carried over the dense
+  // path in registers they cost it a wave per SIMD (100 VGPRs against 94)
+  GroupEnds g;
+  {
+    const int jb = threadIdx.x & 63;
+    if (threadIdx.x < 128 && jb < ga.nb && ga.b[jb].n > 0) {
+      g.keys = ga.b[jb].keys;
+      g.n = ga.b[jb].n;
+      g.first = s_first[jb];
+      g.last = s_last[jb];
+      g.ok = (uint64_t)(uint32_t)(g.first - d.key_begin) < d.range &&
+             (uint64_t)(uint32_t)(g.last - d.key_begin) < d.range && g.first <= g.last;
+    }
   }
   bad = tile_mode<VT, VEC>(ga, d, g, tile_shift, ntiles, blockIdx.x, gridDim.x, s_seg_s, s_seg_e, &s_mask);
   if (bad) *flag = epoch;
