@@ -832,7 +832,7 @@ __global__ __launch_bounds__(kBlock) PSKV_K2G_ATTR void k_assign_group(GroupArgs
       }
     }
   }
-  (void)group_prologue(ga, d, flag, epoch, s_first, s_last, &s_dense);
+  const GroupEnds g = group_prologue(ga, d, flag, epoch, s_first, s_last, &s_dense);
   __syncthreads();
   bool bad = false;
   if (s_dense) {
@@ -852,20 +852,10 @@ __global__ __launch_bounds__(kBlock) PSKV_K2G_ATTR void k_assign_group(GroupArgs
     if (bad) *flag = epoch;
     return;
   }
-  // the endpoints again, from LDS and the arguments: carried over the dense
-  // path in registers they cost it a wave per SIMD (100 VGPRs against 94)
-  GroupEnds g;
-  {
-    const int jb = threadIdx.x & 63;
-    if (threadIdx.x < 128 && jb < ga.nb && ga.b[jb].n > 0) {
-      g.keys = ga.b[jb].keys;
-      g.n = ga.b[jb].n;
-      g.first = s_first[jb];
-      g.last = s_last[jb];
-      g.ok = (uint64_t)(uint32_t)(g.first - d.key_begin) < d.range &&
-             (uint64_t)(uint32_t)(g.last - d.key_begin) < d.range && g.first <= g.last;
-    }
-  }
+  // (Round 4: re-deriving g here from LDS and the arguments instead takes the
+  // dense path from 100 to 94 VGPRs, 4 -> 5 waves per SIMD, and measured
+  // 1-3 % SLOWER on the headline and cold steps: profiles/r04_probes/k2g_waves5_noreg/;
+  // forcing 5 waves with amdgpu_waves_per_eu spills and loses too, k2g_waves5/.)
   bad = tile_mode<VT, VEC>(ga, d, g, tile_shift, ntiles, blockIdx.x, gridDim.x, s_seg_s, s_seg_e, &s_mask);
   if (bad) *flag = epoch;
 }

@@ -35,6 +35,7 @@
 #   ntp_ab       the headline (and its cold form) with K2g parameter stores cached / nt, twice
 #   emu_ntp      every rank of N = 8 emulated, K2g parameter stores cached / non-temporal
 #   k2g_tune     the headline (+ cold form) under K2g grid / early-load / unroll variants
+#   early_cold   the headline (+ cold form, where auto picks early loads) with EARLY auto / 0, twice
 #   smoke        __graft_entry__.smoke() (what the driver runs before the bench)
 #   shardsize    tools/shard_size_probe.py: K2g / K1 per key on 1e8 / 5e8 / 1e9-key shards (same windows)
 #   e2e          tools/e2e_probe.py (host-buffer Add / Get against raw PCIe copy rates)
@@ -140,6 +141,10 @@ for step in "$@"; do
     emu_ntp) for r in 0 1 2 3 4 5 6 7; do for e in 0 1; do
           PSKV_NTP=$e PSKV_BENCH_EMULATE=$r/8 timeout -k 10 200 python3 "$R/bench.py" --steps 50 --no-zipf \
             --no-cpu-baseline --no-extra > "$OUT/emu8_${r}_ntp$e.json" 2> "$OUT/emu8_${r}_ntp$e.err" || exit 1
+        done; done ;;
+    early_cold) for r in 1 2; do for e in 2 0; do
+          PSKV_EARLY=$e timeout -k 10 300 python3 "$R/bench.py" --steps 50 --no-zipf --no-extra --no-cpu-baseline \
+            > "$OUT/early${e}_$r.json" 2> "$OUT/early${e}_$r.err" || exit 1
         done; done ;;
     k2g_tune) for o in "" "PSKV_TILE_GRID=4096" "PSKV_UNROLL=4" "PSKV_TILE_GRID=8192"; do
           tag=$(echo "x$o" | tr ' =' '__')
