@@ -199,14 +199,14 @@ int pskv_shard_info(pskv_shard* s, pskv_info* info);
 
 /* Tuning and path options of one shard, by name (DESIGN.md §5 lists them and
  * what each selects): GENERAL (0 = K4 stamps, 1 = auto, 2 = K5 always),
- * UNROLL, NT, NTP, EARLY (K2g early loads: 0 never, 1 always, 2 auto, 3 keys only),
+ * UNROLL, NT, NTP, EARLY (K2g early loads: 0 never, 1 always, 2 auto),
  * PAGEABLE_DMA, DMA_MIN_BYTES, DMA_MIN_BYTES_GET,
  * DMA_MIN_BYTES_PINNED, ZC_MAX_BYTES, FRAME_ZC_MAX_BYTES, INLINE,
  * INLINE_ADD_CHUNKS, INLINE_GET_CHUNKS, ISPIN, SERVE, SERVE_IDLE_US,
  * TILE_SHIFT, TILE_GRID, RB_WBITS, RB_NBD, RB_TB, RB_APPLY_LOG2, RB_BIN_BLOCK.
  * Every option changes speed only, never results.  Some apply only together
  * with others (a value is accepted and echoed either way):
- *   EARLY = 1, 3  K2g with UNROLL 8 and NT 1 (otherwise the default loads)
+ *   EARLY = 1     K2g with UNROLL 8 and NT 1 (otherwise the default loads)
  *   SERVE = 1     only while the device's hardware queues hold the server
  *                 (DESIGN.md §8); INLINE_*_CHUNKS and ISPIN only on the K8 path
  *   RB_* options  only on the K5 path (unhinted Adds)

@@ -120,7 +120,7 @@ hipError_t launch_assign_sorted(int vb, bool vec, const uint32_t* keys, const vo
 // Grouped sorted Add.  `ga` must be built with stream_chunk(unroll) elements per chunk
 // (used by the dense-window mode); the tile mode ignores the chunking.
 // ntp: non-temporal parameter stores in the dense-window mode
-hipError_t launch_assign_group(int vb, bool vec, int unroll, bool nt, bool ntp, int early,
+hipError_t launch_assign_group(int vb, bool vec, int unroll, bool nt, bool ntp, bool early,
                                const GroupArgs& ga,
                                const DenseView& d, uint32_t tile_shift, uint64_t ntiles,
                                uint32_t grid, uint32_t* flag, uint32_t epoch, hipStream_t st);

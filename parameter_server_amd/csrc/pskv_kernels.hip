@@ -621,9 +621,10 @@ __device__ __forceinline__ bool dense_chunk(const GroupArgs& ga, const DenseView
 // prologue (the first and last key of every batch) has come back; it cannot
 // skip the values of a chunk a later window covers (they are already in
 // flight), so it is for small launches whose windows rarely overlap (a rank's
-// ~8 windows at N = 8).  PRE: 1 = k / v already hold the (whole) chunk, 2 = k
-// does (the keys-early form: values are still skipped for a covered chunk).
-template <int U, bool NT, bool NTP, int PRE>
+// ~8 windows at N = 8).  PRE: k / v already hold the (whole) chunk.  (Round 4
+// measured a keys-only early form, values still skipped for a covered chunk:
+// K2g 115.4 against 112.7 us on the headline; removed.)
+template <int U, bool NT, bool NTP, bool PRE>
 __device__ __forceinline__ bool dense_chunk_own(const GroupArgs& ga, const DenseView& d, uint32_t c,
                                                 const uint32_t* s_first, const uint32_t* s_last,
                                                 uint32_t (&k)[U][4], uint32_t (&v)[U][4]) {
@@ -658,11 +659,11 @@ __device__ __forceinline__ bool dense_chunk_own(const GroupArgs& ga, const Dense
     const uint32_t* __restrict__ kc = keys + base;
     const uint32_t* __restrict__ vc = vals + base;
     uint32_t* __restrict__ pc = param + p0 + base;
-    if (PRE != 1) {
+    if (!PRE) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t o = (uint32_t)(u * kBlock + tid) * 4u;
-        if (PRE == 0) Vec4<uint32_t>::load<NT>(kc + o, k[u]);
+        Vec4<uint32_t>::load<NT>(kc + o, k[u]);
         if (!covered) Vec4<uint32_t>::load<NT>(vc + o, v[u]);
       }
     }
@@ -789,16 +790,8 @@ __device__ __forceinline__ bool tile_mode(const GroupArgs& ga, const DenseView& 
 }
 
 // Mode B (general sorted batches): key-tile owner, static strided schedule.
-// EARLY: 0 = loads after the prologue; 1 = the first chunk's keys and values
-// before it; 2 = its keys only (a covered chunk still skips its values).
-// PSKV_K2G_WAVES (A/B builds only, tools/ab_lib.sh): a waves-per-SIMD floor.
-#ifdef PSKV_K2G_WAVES
-#define PSKV_K2G_ATTR __attribute__((amdgpu_waves_per_eu(PSKV_K2G_WAVES)))
-#else
-#define PSKV_K2G_ATTR
-#endif
-template <typename VT, bool VEC, int U, bool NT, bool NTP, int EARLY = 0>
-__global__ __launch_bounds__(kBlock) PSKV_K2G_ATTR void k_assign_group(GroupArgs ga, DenseView d,
+template <typename VT, bool VEC, int U, bool NT, bool NTP, bool EARLY = false>
+__global__ __launch_bounds__(kBlock) void k_assign_group(GroupArgs ga, DenseView d,
                                                          uint32_t tile_shift, uint64_t ntiles,
                                                          uint32_t* flag, uint32_t epoch) {
   constexpr bool OWN = sizeof(VT) == 4 && VEC;  // dense_chunk_own
@@ -815,7 +808,7 @@ __global__ __launch_bounds__(kBlock) PSKV_K2G_ATTR void k_assign_group(GroupArgs
   // before the prologue below (its loads need no batch endpoint)
   uint32_t ek[OWN ? U : 1][4], ev[OWN ? U : 1][4];
   bool pre = false;
-  if constexpr (EARLY != 0) {
+  if constexpr (EARLY) {
     if (blockIdx.x < ga.wg_prefix[ga.nb]) {
       const int j0 = batch_of(ga, blockIdx.x);
       const uint64_t base0 = (uint64_t)(blockIdx.x - ga.wg_prefix[j0]) * CH;
@@ -827,7 +820,7 @@ __global__ __launch_bounds__(kBlock) PSKV_K2G_ATTR void k_assign_group(GroupArgs
         for (int u = 0; u < U; ++u) {
           const uint32_t o = (uint32_t)(u * kBlock + tid) * 4u;
           Vec4<uint32_t>::load<NT>(kc + o, ek[u]);
-          if (EARLY == 1) Vec4<uint32_t>::load<NT>(vc + o, ev[u]);
+          Vec4<uint32_t>::load<NT>(vc + o, ev[u]);
         }
       }
     }
@@ -840,11 +833,11 @@ __global__ __launch_bounds__(kBlock) PSKV_K2G_ATTR void k_assign_group(GroupArgs
     if constexpr (OWN) {
       uint32_t c = blockIdx.x;
       if (pre) {
-        bad |= dense_chunk_own<U, NT, NTP, EARLY>(ga, d, c, s_first, s_last, ek, ev);
+        bad |= dense_chunk_own<U, NT, NTP, true>(ga, d, c, s_first, s_last, ek, ev);
         c += gridDim.x;
       }
       for (; c < nchunks; c += gridDim.x)
-        bad |= dense_chunk_own<U, NT, NTP, 0>(ga, d, c, s_first, s_last, ek, ev);
+        bad |= dense_chunk_own<U, NT, NTP, false>(ga, d, c, s_first, s_last, ek, ev);
     } else {
       for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x)
         bad |= dense_chunk<VT, VEC, U, NT, NTP>(ga, d, c, s_first, s_last);
@@ -2475,15 +2468,12 @@ hipError_t launch_assign_sorted(int vb, bool vec, const uint32_t* keys, const vo
 }
 
 template <typename VT, bool VEC, bool NTP>
-static void group_dispatch2(int unroll, bool nt, int early, uint32_t grid, const GroupArgs& ga,
+static void group_dispatch2(int unroll, bool nt, bool early, uint32_t grid, const GroupArgs& ga,
                             const DenseView& d, uint32_t shift, uint64_t ntiles, uint32_t* flag,
                             uint32_t epoch, hipStream_t st) {
   if constexpr (sizeof(VT) == 4 && VEC) {
     if (early && unroll == 8 && nt) {  // early mode: the default unroll and streams only
-      if (early == 1)
-        k_assign_group<VT, VEC, 8, true, NTP, 1><<<grid, kBlock, 0, st>>>(ga, d, shift, ntiles, flag, epoch);
-      else
-        k_assign_group<VT, VEC, 8, true, NTP, 2><<<grid, kBlock, 0, st>>>(ga, d, shift, ntiles, flag, epoch);
+      k_assign_group<VT, VEC, 8, true, NTP, true><<<grid, kBlock, 0, st>>>(ga, d, shift, ntiles, flag, epoch);
       return;
     }
   }
@@ -2501,7 +2491,7 @@ static void group_dispatch2(int unroll, bool nt, int early, uint32_t grid, const
 }
 
 template <typename VT, bool VEC>
-static void group_dispatch(int unroll, bool nt, bool ntp, int early, uint32_t grid, const GroupArgs& ga,
+static void group_dispatch(int unroll, bool nt, bool ntp, bool early, uint32_t grid, const GroupArgs& ga,
                            const DenseView& d, uint32_t shift, uint64_t ntiles, uint32_t* flag,
                            uint32_t epoch, hipStream_t st) {
   if (ntp)
@@ -2510,7 +2500,7 @@ static void group_dispatch(int unroll, bool nt, bool ntp, int early, uint32_t gr
     group_dispatch2<VT, VEC, false>(unroll, nt, early, grid, ga, d, shift, ntiles, flag, epoch, st);
 }
 
-hipError_t launch_assign_group(int vb, bool vec, int unroll, bool nt, bool ntp, int early,
+hipError_t launch_assign_group(int vb, bool vec, int unroll, bool nt, bool ntp, bool early,
                                const GroupArgs& ga,
                                const DenseView& d, uint32_t tile_shift, uint64_t ntiles,
                                uint32_t grid, uint32_t* flag, uint32_t epoch, hipStream_t st) {

@@ -267,7 +267,7 @@ struct pskv_shard {
   // 5.74-5.86 -> 6.11-6.22 TB/s, its Get (K1) 114-116 -> 91 us
   // (profiles/r04_probes/ntp_ab/)
   bool tune_ntp = true;
-  int tune_early = 2;    // PSKV_EARLY: K2g early loads (0 never, 1 always, 2 when the group's keys cover < 1/4 of the range, 3 keys only, always)
+  int tune_early = 2;    // PSKV_EARLY: K2g early loads (0 never, 1 always, 2 when the group's keys cover < 1/4 of the range)
   // PSKV_PAGEABLE_DMA: DMA pageable host buffers directly (the runtime moves
   // them at the PCIe rate, measured 55 GB/s) instead of copying them into
   // pinned staging first; 0 selects the staging path.  cfg-2-shaped Add of
@@ -884,8 +884,7 @@ int sorted_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t
     // values of a chunk a later window covers.  Results are the same either way.
     // A host group the CPU found sorted but not all windows goes to the tile
     // mode, where early loads would only be read again (maybe_windows false).
-    int early = s->tune_early == 1 || (s->tune_early == 2 && maybe_windows && elems * 4 < s->range) ? 1 : 0;
-    if (s->tune_early == 3) early = 2;  // the first chunk's keys before the prologue, its values after
+    const bool early = s->tune_early == 1 || (s->tune_early == 2 && maybe_windows && elems * 4 < s->range);
     LaunchTimer t(s, PSKV_K_ASSIGN_TILES, elems);
     PSKV_HIP(launch_assign_group(s->vb, vec, s->tune_unroll, s->tune_nt, s->tune_ntp, early, ga, s->dview(),
                                  shift, ntiles, grid, s->flag, epoch, s->stream));
@@ -1787,7 +1786,7 @@ const Option kOptions[] = {
     PSKV_OPT("UNROLL", 4, 8, tune_unroll, int),              // 4 or 8 (others: 8)
     PSKV_OPT("NT", 0, 1, tune_nt, bool),
     PSKV_OPT("NTP", 0, 1, tune_ntp, bool),
-    PSKV_OPT("EARLY", 0, 3, tune_early, int),
+    PSKV_OPT("EARLY", 0, 2, tune_early, int),
     PSKV_OPT("PAGEABLE_DMA", 0, 1, tune_pageable_dma, bool),
     PSKV_OPT("DMA_MIN_BYTES", 0, INT64_MAX, tune_dma_min_bytes, size_t),
     PSKV_OPT("DMA_MIN_BYTES_GET", 0, INT64_MAX, tune_dma_min_bytes_get, size_t),

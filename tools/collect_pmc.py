@@ -31,7 +31,7 @@ def per_dispatch(path, counter):
 
 
 def short(name):
-    for k in ("k_add_get", "k_replay_get", "k_gather", "k_assign_group", "k_assign_sorted", "k_general_mark",
+    for k in ("k_gather", "k_assign_group", "k_assign_sorted", "k_general_mark",
               "k_general_commit", "k_replay", "k_rb_bin", "k_rb_resolve"):
         if k in name:
             return k + name[name.index(k) + len(k):].split("(")[0]
