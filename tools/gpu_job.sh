@@ -18,6 +18,7 @@
 #   sizes        tools/size_probe.py: K2g / K1 time against window count (fixed cost per launch)
 #   abs          tools/ab_lib.sh with AB_PROG=sizes: base vs new library under tools/size_probe.py
 #   abb          tools/ab_lib.sh under bench.py (headline + cold form): base vs new library, 3 rounds
+#   abe          the same with rank 0 of N = 8 emulated (PSKV_BENCH_EMULATE=0/8)
 #   fuzz         tests/test_fuzz.py over FUZZ_SCENARIOS (1500) new seeds from FUZZ_SEED0 (3500), single and concurrent
 #   sizetrace    rocprofv3 kernel trace of tools/size_probe.py (exact K2g / K4r / K1 durations and gaps)
 #   idle         tools/micro/idle_launch: an idle conditional launch's cost between two streaming kernels
@@ -99,6 +100,8 @@ for step in "$@"; do
     abz) AB_PROG=zipf timeout -k 10 900 bash "$R/tools/ab_lib.sh" "$(basename "$OUT")/abz" > "$OUT/abz.log" 2>&1 ;;
     sizes) timeout -k 10 300 python3 "$R/tools/size_probe.py" > "$OUT/size_probe.log" 2>&1 ;;
     abb) timeout -k 10 900 bash "$R/tools/ab_lib.sh" "$(basename "$OUT")/abb" > "$OUT/abb.log" 2>&1 ;;
+    abe) PSKV_BENCH_EMULATE=0/8 timeout -k 10 900 bash "$R/tools/ab_lib.sh" "$(basename "$OUT")/abe" \
+          "--no-extra --no-cpu-baseline --no-zipf --steps 50" > "$OUT/abe.log" 2>&1 ;;
     abs) AB_PROG=sizes timeout -k 10 900 bash "$R/tools/ab_lib.sh" "$(basename "$OUT")/abs" > "$OUT/abs.log" 2>&1 ;;
     fuzz3) FUZZ_SEED0=6500 FUZZ_SCENARIOS=1500 FUZZ_GROUPS=8 timeout -k 10 1000 python3 -u -m pytest \
         "$R/tests/test_fuzz.py" -m gpu -q --timeout 300 --timeout-method thread > "$OUT/fuzz3.log" 2>&1 ;;
