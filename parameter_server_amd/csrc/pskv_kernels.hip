@@ -2416,9 +2416,14 @@ __global__ __launch_bounds__(kInlineMax) void k_serve(SrvRing* ring, DenseView d
 template <typename VT, bool VEC>
 static void gather_dispatch(int unroll, bool nt, uint32_t nwg, const GroupArgs& ga,
                             const DenseView& d, const Ovf& o, hipStream_t st) {
+#ifdef PSKV_K1_LDS_CAP  // occupancy probe builds only
+  const uint32_t cap = PSKV_K1_LDS_CAP;
+#else
+  const uint32_t cap = 0;
+#endif
   if (unroll == 8) {
     if (nt)
-      k_gather<VT, VEC, 8, true><<<nwg, kBlock, 0, st>>>(ga, d, o);
+      k_gather<VT, VEC, 8, true><<<nwg, kBlock, cap, st>>>(ga, d, o);
     else
       k_gather<VT, VEC, 8, false><<<nwg, kBlock, 0, st>>>(ga, d, o);
   } else {
@@ -2467,21 +2472,31 @@ hipError_t launch_assign_sorted(int vb, bool vec, const uint32_t* keys, const vo
   return hipGetLastError();
 }
 
+// Workgroups of the 4-byte K2g per CU: at most 3, held there by a dynamic LDS
+// reservation the kernel never touches (static 1.5 KiB + 48 KiB: 3 fit the
+// CU's 160 KiB).  Its registers allow 4; 3 streams of keys, values and
+// parameters per CU measured faster (PSKV_K2G_OCC_PROBE builds: see DESIGN §7).
+#ifndef PSKV_K2G_LDS_CAP
+#define PSKV_K2G_LDS_CAP (48u << 10)
+#endif
+constexpr uint32_t kK2gLdsCap = PSKV_K2G_LDS_CAP;
+
 template <typename VT, bool VEC, bool NTP>
 static void group_dispatch2(int unroll, bool nt, bool early, uint32_t grid, const GroupArgs& ga,
                             const DenseView& d, uint32_t shift, uint64_t ntiles, uint32_t* flag,
                             uint32_t epoch, hipStream_t st) {
+  const uint32_t cap = sizeof(VT) == 4 && VEC && unroll == 8 ? kK2gLdsCap : 0u;
   if constexpr (sizeof(VT) == 4 && VEC) {
     if (early && unroll == 8 && nt) {  // early mode: the default unroll and streams only
-      k_assign_group<VT, VEC, 8, true, NTP, true><<<grid, kBlock, 0, st>>>(ga, d, shift, ntiles, flag, epoch);
+      k_assign_group<VT, VEC, 8, true, NTP, true><<<grid, kBlock, cap, st>>>(ga, d, shift, ntiles, flag, epoch);
       return;
     }
   }
   if (unroll == 8) {
     if (nt)
-      k_assign_group<VT, VEC, 8, true, NTP><<<grid, kBlock, 0, st>>>(ga, d, shift, ntiles, flag, epoch);
+      k_assign_group<VT, VEC, 8, true, NTP><<<grid, kBlock, cap, st>>>(ga, d, shift, ntiles, flag, epoch);
     else
-      k_assign_group<VT, VEC, 8, false, NTP><<<grid, kBlock, 0, st>>>(ga, d, shift, ntiles, flag, epoch);
+      k_assign_group<VT, VEC, 8, false, NTP><<<grid, kBlock, cap, st>>>(ga, d, shift, ntiles, flag, epoch);
   } else {
     if (nt)
       k_assign_group<VT, VEC, 4, true, NTP><<<grid, kBlock, 0, st>>>(ga, d, shift, ntiles, flag, epoch);

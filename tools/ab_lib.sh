@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B two builds of libpskv.so on one box (ab/libpskv_base.so, ab/libpskv_new.so,
-# built beforehand): alternate them (swapping the in-tree library file, which
+# built beforehand; AB_VARIANTS="base x y" alternates ab/libpskv_{base,x,y}.so): alternate them (swapping the in-tree library file, which
 # is restored to the tree's own build on exit), 3
 # rounds each, under bench.py (default) or, with AB_PROG=zipf, under
 # tools/zipf_probe.py (the cfg-3 K5 / K1 kernel times), with AB_PROG=sizes under
@@ -16,7 +16,7 @@ SAVE=$(mktemp) && cp "$LIB" "$SAVE" || exit 1   # the tree's own build, put back
 restore() { cp "$SAVE" "$LIB"; rm -f "$SAVE"; }
 trap restore EXIT
 for i in 1 2 3; do
-  for v in base new; do
+  for v in ${AB_VARIANTS:-base new}; do
     cp "$R/ab/libpskv_$v.so" "$R/parameter_server_amd/libpskv.so" || exit 1
     if [ "${AB_PROG:-bench}" = sizes ]; then
       timeout -k 10 200 python3 "$R/tools/size_probe.py" > "$OUT/$v$i.log" 2>&1 || exit 2

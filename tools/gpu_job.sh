@@ -19,6 +19,9 @@
 #   abs          tools/ab_lib.sh with AB_PROG=sizes: base vs new library under tools/size_probe.py
 #   abb          tools/ab_lib.sh under bench.py (headline + cold form): base vs new library, 3 rounds
 #   abe          the same with rank 0 of N = 8 emulated (PSKV_BENCH_EMULATE=0/8)
+#   abocc        bench A/B of ab/libpskv_{base,occ3,occ4b}.so (K2g LDS cap off / 3 / 4 workgroups per CU)
+#   abocce       the same on rank 0 of N = 8 emulated
+#   abk1         bench A/B of ab/libpskv_{base,k1occ6,k1occ4}.so (K1 held to 8 / 6 / 4 workgroups per CU), headline and rank 0 of 8
 #   fuzz         tests/test_fuzz.py over FUZZ_SCENARIOS (1500) new seeds from FUZZ_SEED0 (3500), single and concurrent
 #   sizetrace    rocprofv3 kernel trace of tools/size_probe.py (exact K2g / K4r / K1 durations and gaps)
 #   idle         tools/micro/idle_launch: an idle conditional launch's cost between two streaming kernels
@@ -102,6 +105,14 @@ for step in "$@"; do
     abb) timeout -k 10 900 bash "$R/tools/ab_lib.sh" "$(basename "$OUT")/abb" > "$OUT/abb.log" 2>&1 ;;
     abe) PSKV_BENCH_EMULATE=0/8 timeout -k 10 900 bash "$R/tools/ab_lib.sh" "$(basename "$OUT")/abe" \
           "--no-extra --no-cpu-baseline --no-zipf --steps 50" > "$OUT/abe.log" 2>&1 ;;
+    abocc) AB_VARIANTS="base occ3 occ4b" timeout -k 10 900 bash "$R/tools/ab_lib.sh" "$(basename "$OUT")/abocc" \
+          > "$OUT/abocc.log" 2>&1 ;;
+    abocce) PSKV_BENCH_EMULATE=0/8 AB_VARIANTS="base occ3 occ4b" timeout -k 10 900 bash "$R/tools/ab_lib.sh" \
+          "$(basename "$OUT")/abocce" "--no-extra --no-cpu-baseline --no-zipf --no-cold --steps 50" > "$OUT/abocce.log" 2>&1 ;;
+    abk1) AB_VARIANTS="base k1occ6 k1occ4" timeout -k 10 900 bash "$R/tools/ab_lib.sh" "$(basename "$OUT")/abk1" \
+          > "$OUT/abk1.log" 2>&1 &&
+        PSKV_BENCH_EMULATE=0/8 AB_VARIANTS="base k1occ6 k1occ4" timeout -k 10 900 bash "$R/tools/ab_lib.sh" \
+          "$(basename "$OUT")/abk1e" "--no-extra --no-cpu-baseline --no-zipf --no-cold --steps 50" > "$OUT/abk1e.log" 2>&1 ;;
     abs) AB_PROG=sizes timeout -k 10 900 bash "$R/tools/ab_lib.sh" "$(basename "$OUT")/abs" > "$OUT/abs.log" 2>&1 ;;
     fuzz3) FUZZ_SEED0=6500 FUZZ_SCENARIOS=1500 FUZZ_GROUPS=8 timeout -k 10 1000 python3 -u -m pytest \
         "$R/tests/test_fuzz.py" -m gpu -q --timeout 300 --timeout-method thread > "$OUT/fuzz3.log" 2>&1 ;;
