@@ -2416,14 +2416,11 @@ __global__ __launch_bounds__(kInlineMax) void k_serve(SrvRing* ring, DenseView d
 template <typename VT, bool VEC>
 static void gather_dispatch(int unroll, bool nt, uint32_t nwg, const GroupArgs& ga,
                             const DenseView& d, const Ovf& o, hipStream_t st) {
-#ifdef PSKV_K1_LDS_CAP  // occupancy probe builds only
-  const uint32_t cap = PSKV_K1_LDS_CAP;
-#else
-  const uint32_t cap = 0;
-#endif
+  // (K1 held to 6 or 4 workgroups per CU by an LDS reservation, as K2g is to
+  // 3: no gain anywhere, profiles/r04_probes/k1_occupancy/)
   if (unroll == 8) {
     if (nt)
-      k_gather<VT, VEC, 8, true><<<nwg, kBlock, cap, st>>>(ga, d, o);
+      k_gather<VT, VEC, 8, true><<<nwg, kBlock, 0, st>>>(ga, d, o);
     else
       k_gather<VT, VEC, 8, false><<<nwg, kBlock, 0, st>>>(ga, d, o);
   } else {
@@ -2474,8 +2471,10 @@ hipError_t launch_assign_sorted(int vb, bool vec, const uint32_t* keys, const vo
 
 // Workgroups of the 4-byte K2g per CU: at most 3, held there by a dynamic LDS
 // reservation the kernel never touches (static 1.5 KiB + 48 KiB: 3 fit the
-// CU's 160 KiB).  Its registers allow 4; 3 streams of keys, values and
-// parameters per CU measured faster (PSKV_K2G_OCC_PROBE builds: see DESIGN §7).
+// CU's 160 KiB).  Its registers allow 4; 3 per CU measured faster on the
+// headline (K2g 108.5 against 109.8 us), equal on the cold form and a rank's
+// share; 2 per CU lost 3 % cold (profiles/r04_probes/k2g_occupancy/; A/B builds
+// set PSKV_K2G_LDS_CAP).
 #ifndef PSKV_K2G_LDS_CAP
 #define PSKV_K2G_LDS_CAP (48u << 10)
 #endif
