@@ -23,6 +23,8 @@
 #   abocce       the same on rank 0 of N = 8 emulated
 #   abke         bench A/B of ab/libpskv_{base,kearly}.so (K2g keys before its prologue), headline and rank 0 of 8,
 #                then the headline with PSKV_EARLY=1 twice
+#   graph        tools/graph_probe.py: one rotation of the benchmarked steps as a HIP graph vs launched eagerly
+#                (cfg 2 and rank 0 of N = 8)
 #   abk1         bench A/B of ab/libpskv_{base,k1occ6,k1occ4}.so (K1 held to 8 / 6 / 4 workgroups per CU), headline and rank 0 of 8
 #   fuzz         tests/test_fuzz.py over FUZZ_SCENARIOS (1500) new seeds from FUZZ_SEED0 (3500), single and concurrent
 #   sizetrace    rocprofv3 kernel trace of tools/size_probe.py (exact K2g / K4r / K1 durations and gaps)
@@ -121,6 +123,8 @@ for step in "$@"; do
           "$(basename "$OUT")/abkee" "--no-extra --no-cpu-baseline --no-zipf --no-cold --steps 50" > "$OUT/abkee.log" 2>&1 &&
         for r in 1 2; do PSKV_EARLY=1 timeout -k 10 300 python3 "$R/bench.py" --steps 50 --no-zipf --no-extra \
           --no-cpu-baseline > "$OUT/early1_$r.json" 2> "$OUT/early1_$r.err" || exit 1; done ;;
+    graph) timeout -k 10 300 python3 "$R/tools/graph_probe.py" 10 > "$OUT/graph_n1.log" 2>&1 &&
+        PSKV_BENCH_EMULATE=0/8 timeout -k 10 300 python3 "$R/tools/graph_probe.py" 10 > "$OUT/graph_r0of8.log" 2>&1 ;;
     abs) AB_PROG=sizes timeout -k 10 900 bash "$R/tools/ab_lib.sh" "$(basename "$OUT")/abs" > "$OUT/abs.log" 2>&1 ;;
     fuzz3) FUZZ_SEED0=6500 FUZZ_SCENARIOS=1500 FUZZ_GROUPS=8 timeout -k 10 1000 python3 -u -m pytest \
         "$R/tests/test_fuzz.py" -m gpu -q --timeout 300 --timeout-method thread > "$OUT/fuzz3.log" 2>&1 ;;
