@@ -48,6 +48,7 @@
 #   shardsize    tools/shard_size_probe.py: K2g / K1 per key on 1e8 / 5e8 / 1e9-key shards (same windows)
 #   e2e          tools/e2e_probe.py (host-buffer Add / Get against raw PCIe copy rates)
 #   bench        bench.py --steps 20 (the driver's command line)
+#   benchdef     bench.py with no arguments (its defaults), timed by the job
 #   zipf         tools/zipf_probe.py kernel times on cfg 3
 #   zipf_bin     the same for K5a at 1024- and 512-thread workgroups
 #   profile      tools/gpu_profile.sh: rocprofv3 kernel trace + stats, FETCH / WRITE PMC passes (headline)
@@ -182,6 +183,8 @@ for step in "$@"; do
     shardsize) timeout -k 10 400 python3 "$R/tools/shard_size_probe.py" > "$OUT/shard_size.log" 2>&1 &&
         FLUSH=1 timeout -k 10 400 python3 "$R/tools/shard_size_probe.py" > "$OUT/shard_size_flush.log" 2>&1 ;;
     e2e) timeout -k 10 200 python3 "$R/tools/e2e_probe.py" > "$OUT/e2e.log" 2>&1 ;;
+    benchdef) t0=$(date +%s); timeout -k 10 900 python3 "$R/bench.py" > "$OUT/benchdef.json" 2> "$OUT/benchdef.err" &&
+        echo "bench.py defaults: $(( $(date +%s) - t0 )) s" >> "$OUT/benchdef.err" ;;
     bench) timeout -k 10 400 python3 "$R/bench.py" --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     profile) bash "$R/tools/gpu_profile.sh" "$(basename "$OUT")/prof" > "$OUT/profile.log" 2>&1 ;;
     profile_cold) MODE=cold bash "$R/tools/gpu_profile.sh" "$(basename "$OUT")/prof_cold" > "$OUT/profile_cold.log" 2>&1 ;;
