@@ -3,8 +3,9 @@
 One step = one pass of the hot path over one push set and one pull set: a
 grouped Add of the step's push batches, then a grouped Get of windows the push
 did NOT touch (zero push/pull overlap, config.push_pull_overlap_keys = 0;
-round 4).  Consecutive steps rotate over R window sets (--sets, default 16;
-set r drawn with seed set_seed(r), set 0 being the config's own seed).  The
+round 4).  Consecutive steps rotate over R window sets (--sets, default 16 at
+N = 1 and 64 at N > 1; set r drawn with seed set_seed(r), set 0 being the
+config's own seed).  The
 round-2 form (the Get pulls the windows it just pushed, Infinity-Cache warm)
 is kept as extra.cache_warm_step.  Inputs are resident in HBM before timing.
 
@@ -73,9 +74,12 @@ def parse(argv=None):
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--batches", type=int, default=64, help="push batches (N=1) / producer streams (N>1) per step")
     p.add_argument("--batch-keys", type=int, default=1_000_000)
-    p.add_argument("--sets", type=int, default=16,
-                   help="window sets rotated over the steps (producers push new windows every step; at N > 1 "
-                        "more sets also even out the ranks' shares over the timed steps)")
+    p.add_argument("--sets", type=int, default=None,
+                   help="window sets rotated over the steps (producers push new windows every step); default 16 "
+                        "at N = 1, 64 at N > 1, where each set is a fresh random draw of the 64 producer windows "
+                        "and more draws bring the ranks' totals over the timed steps to what an endless stream "
+                        "of draws gives them (the largest rank share over the mean at N = 8: 1.078 with 16 sets, "
+                        "1.027 with 64)"),
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extra", action="store_true", help="skip the side measurements (e2e, f64, accumulate)")
     p.add_argument("--no-zipf", action="store_true", help="skip the cfg-3 sparse (Zipf) measurement")
@@ -91,6 +95,13 @@ def parse(argv=None):
                    help="time only the VectorStorage restatement at --vector-sizes (no GPU; e.g. the one "
                         "measured 1e6-key run of config 1) and print its JSON")
     return p.parse_args(argv)
+
+
+def default_sets(sets, world):
+    """Window sets rotated over the steps: --sets, or 16 at N = 1 and 64 at
+    N > 1 (each a fresh cfg-4 draw; with 64 the largest of 8 ranks' totals is
+    1.027 of the mean, with 16 1.078); at least 2."""
+    return max(2, sets if sets is not None else (16 if world == 1 else 64))
 
 
 def dist_init(args):
@@ -970,13 +981,14 @@ def main(argv=None):
 
     rank, world, local = dist_init(args)
     dev = torch.device(f"cuda:{local}")
-    J, B, R = args.batches, args.batch_keys, max(2, args.sets)
+    J, B = args.batches, args.batch_keys
     # planning rank / world: the process's own, or (probe knob, one process,
     # never used by the driver) PSKV_BENCH_EMULATE="r/N" = rank r's share of
     # the N-GPU cfg-4 workload alone on this GPU
     prank, pworld = rank, world
     if os.environ.get("PSKV_BENCH_EMULATE") and world == 1:
         prank, pworld = (int(x) for x in os.environ["PSKV_BENCH_EMULATE"].split("/"))
+    R = default_sets(args.sets, pworld)
     if args.cold_only:
         # the cold form pulls as many windows as cfg 2's set r: host planning only
         progress("cold form only")

@@ -175,3 +175,15 @@ def test_interval_union_and_global_windows():
     # producer s draws with seed 1000 + s: the same stream whatever the count
     assert list(workload.global_windows(3, 1_000_000_000, 1_000_000, seed=1000)) == list(b[:3])
     assert any(int(x) % 4 for x in b)  # any alignment
+
+
+def test_bench_default_window_sets():
+    """bench.py's --sets default: 16 window sets at N = 1, 64 at N > 1 (fresh
+    cfg-4 draws: the largest rank's share over the timed steps approaches the
+    mean), an explicit value wins."""
+    import bench
+
+    assert bench.parse([]).sets is None
+    assert bench.parse(["--sets", "4"]).sets == 4
+    assert bench.default_sets(None, 1) == 16 and bench.default_sets(None, 8) == 64
+    assert bench.default_sets(4, 8) == 4 and bench.default_sets(1, 1) == 2
