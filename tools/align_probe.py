@@ -1,8 +1,9 @@
-"""How much does a window's alignment cost the streaming kernels?  cfg-2 shaped
-steps (64 x 1M windows over a 1e8-key float shard, pull of the next set) with
-every window base shifted by `delta` keys (0: 16-byte aligned parameter
-accesses; 1-3: every 4-key group straddles two 16-byte parameter slots), in one
-process, per-kernel HIP-event times.  cfg 4's producer windows start at any key.
+"""How much does a window's alignment cost the streaming kernels?  bench.py's
+cfg-2 step (64 x 1M windows pushed over a 1e8-key float shard, the free window
+slots pulled) with every pushed and pulled window shifted by `delta` keys (0:
+16-byte aligned parameter accesses; 1-3: every 4-key group straddles two
+16-byte parameter slots), in one process, per-kernel HIP-event times.  cfg 4's
+producer windows start at any key.
 
   python tools/align_probe.py [deltas, default 0,1,2,3] [steps]
 """
@@ -30,15 +31,20 @@ def main():
         for d in deltas:
             sets = []
             for s in base_sets:
-                sl = [(w, min(f + d, 100_000_000 - B), n) for w, f, n in s["slices"]]
-                bt = [(torch.arange(f, f + n, dtype=torch.int64, device=dev).to(torch.int32), v)
+                # every window moved up by d keys; the last slot's loses its
+                # top d keys (the shard ends at 1e8), so none meets another
+                sl = [(w, f + d, min(n, 100_000_000 - f - d)) for w, f, n in s["slices"]]
+                bt = [(torch.arange(f, f + n, dtype=torch.int64, device=dev).to(torch.int32), v[:n])
                       for (_, f, n), (_, v) in zip(sl, s["batches"])]
+                pl = [(w, f + d, min(n, 100_000_000 - f - d)) for w, f, n in s["pull"]]
+                pk = [torch.arange(f, f + n, dtype=torch.int64, device=dev).to(torch.int32) for _, f, n in pl]
                 from parameter_server_amd import workload
                 sets.append({"slices": sl, "batches": bt, "u": workload.interval_union([(f, n) for _, f, n in sl]),
-                             "r": s["r"]})
+                             "r": s["r"], "pull": pl, "pull_keys": pk})
+                assert bench.overlap_keys(sets[-1]) == 0
             with ps.Shard(0, 100_000_000, np.float32) as sh:
                 sh.set_stream(torch.cuda.current_stream().cuda_stream)
-                f = bench.Form(sh, sets, 1, dev)
+                f = bench.Form(sh, sets, dev)
                 if rep == 0:
                     f.self_check(0, 100_000_000, dev)
                 res = bench.run_form(f, steps, 4, 1, dev)
