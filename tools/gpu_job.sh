@@ -25,6 +25,7 @@
 #                then the headline with PSKV_EARLY=1 twice
 #   graph        tools/graph_probe.py: one rotation of the benchmarked steps as a HIP graph vs launched eagerly
 #                (cfg 2 and rank 0 of N = 8)
+#   k5tests      the K5 (unhinted Add) parity tests: Zipf, radix, random, accumulate, sentinel, ragged, full-size cfg 3
 #   abk1         bench A/B of ab/libpskv_{base,k1occ6,k1occ4}.so (K1 held to 8 / 6 / 4 workgroups per CU), headline and rank 0 of 8
 #   fuzz         tests/test_fuzz.py over FUZZ_SCENARIOS (1500) new seeds from FUZZ_SEED0 (3500), single and concurrent
 #   sizetrace    rocprofv3 kernel trace of tools/size_probe.py (exact K2g / K4r / K1 durations and gaps)
@@ -126,6 +127,9 @@ for step in "$@"; do
           --no-cpu-baseline > "$OUT/early1_$r.json" 2> "$OUT/early1_$r.err" || exit 1; done ;;
     graph) timeout -k 10 300 python3 "$R/tools/graph_probe.py" 10 > "$OUT/graph_n1.log" 2>&1 &&
         PSKV_BENCH_EMULATE=0/8 timeout -k 10 300 python3 "$R/tools/graph_probe.py" 10 > "$OUT/graph_r0of8.log" 2>&1 ;;
+    k5tests) timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread \
+          "$R/tests/test_gpu_parity.py" "$R/tests/test_fuzz.py" -m gpu \
+          -k "zipf or radix or random or accumulate or sentinel or ragged or cfg3 or fuzz" > "$OUT/k5tests.log" 2>&1 ;;
     abs) AB_PROG=sizes timeout -k 10 900 bash "$R/tools/ab_lib.sh" "$(basename "$OUT")/abs" > "$OUT/abs.log" 2>&1 ;;
     fuzz3) FUZZ_SEED0=6500 FUZZ_SCENARIOS=1500 FUZZ_GROUPS=8 timeout -k 10 1000 python3 -u -m pytest \
         "$R/tests/test_fuzz.py" -m gpu -q --timeout 300 --timeout-method thread > "$OUT/fuzz3.log" 2>&1 ;;
