@@ -708,6 +708,7 @@ def zipf_sparse(rank, world, dev, lo, hi, B, steps, J=8):
     zb = workload.zipf_batches(J, space, batch=B, device=dev, perm_seed=7 + rank, seed=42 + 1000 * rank,
                                lo=lo)
     zo = [torch.empty_like(v) for _, v in zb]
+    progress("cfg 3: batches built")
     uniq = int(torch.unique(zb[0][0]).numel())
     u_all = int(torch.unique(torch.cat([k for k, _ in zb])).numel())
     with ps.Shard(lo, hi, np.float32, device=dev.index) as sh:
@@ -728,6 +729,7 @@ def zipf_sparse(rank, world, dev, lo, hi, B, steps, J=8):
         got = sh.get(probe).cpu().numpy()
         assert np.array_equal(got, np.array([last[int(x)] for x in probe.cpu().numpy()], np.float32)), \
             "zipf self-check failed"
+        progress("cfg 3: self-check done")
         barrier(world)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -757,6 +759,7 @@ def zipf_sparse(rank, world, dev, lo, hi, B, steps, J=8):
         b = add_b if n.startswith("k_rb") else get_b
         kernels[n] = {"avg_ms": ms, "algorithmic_bytes": b, "GB/s": b / (ms * 1e-3) / 1e9,
                       "frac": b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    progress("cfg 3: timed; random-access floor")
     floor = random_access_floor(zb, lo, space, dev)
     if floor is not None:
         k5_ms = kernels["k_rb_bin+k_rb_resolve (K5 Add)"]["avg_ms"]

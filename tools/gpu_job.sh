@@ -25,6 +25,8 @@
 #                then the headline with PSKV_EARLY=1 twice
 #   graph        tools/graph_probe.py: one rotation of the benchmarked steps as a HIP graph vs launched eagerly
 #                (cfg 2 and rank 0 of N = 8)
+#   ranks8diag   bench.py as 8 ranks on one GPU: headline only, then with the Zipf measurement
+#   ranks48      bench.py as 4 and as 8 ranks on one GPU (gloo, shared device; --sets 4): the N = 4 / 8 code path
 #   k5tests      the K5 (unhinted Add) parity tests: Zipf, radix, random, accumulate, sentinel, ragged, full-size cfg 3
 #   abk1         bench A/B of ab/libpskv_{base,k1occ6,k1occ4}.so (K1 held to 8 / 6 / 4 workgroups per CU), headline and rank 0 of 8
 #   fuzz         tests/test_fuzz.py over FUZZ_SCENARIOS (1500) new seeds from FUZZ_SEED0 (3500), single and concurrent
@@ -127,6 +129,17 @@ for step in "$@"; do
           --no-cpu-baseline > "$OUT/early1_$r.json" 2> "$OUT/early1_$r.err" || exit 1; done ;;
     graph) timeout -k 10 300 python3 "$R/tools/graph_probe.py" 10 > "$OUT/graph_n1.log" 2>&1 &&
         PSKV_BENCH_EMULATE=0/8 timeout -k 10 300 python3 "$R/tools/graph_probe.py" 10 > "$OUT/graph_r0of8.log" 2>&1 ;;
+    ranks8diag) PSKV_BENCH_BACKEND=gloo PSKV_BENCH_SHARE_GPU=1 timeout -k 10 170 python3 -m torch.distributed.run \
+          --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29611 "$R/bench.py" --gpus 8 --steps 5 \
+          --warmup 2 --sets 4 --no-zipf --no-extra > "$OUT/ranks8_nozipf.json" 2> "$OUT/ranks8_nozipf.err" &&
+        PSKV_BENCH_BACKEND=gloo PSKV_BENCH_SHARE_GPU=1 timeout -k 10 170 python3 -m torch.distributed.run \
+          --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29612 "$R/bench.py" --gpus 8 --steps 5 \
+          --warmup 2 --sets 4 --no-extra > "$OUT/ranks8_zipf.json" 2> "$OUT/ranks8_zipf.err" ;;
+    ranks48) for n in 4 8; do
+          PSKV_BENCH_BACKEND=gloo PSKV_BENCH_SHARE_GPU=1 timeout -k 10 500 python3 -m torch.distributed.run --nnodes=1 \
+            --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29600 + n)) "$R/bench.py" --gpus $n --steps 5 \
+            --warmup 2 --sets 4 > "$OUT/ranks$n.json" 2> "$OUT/ranks$n.err" || exit 1
+        done ;;
     k5tests) timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread \
           "$R/tests/test_gpu_parity.py" "$R/tests/test_fuzz.py" -m gpu \
           -k "zipf or radix or random or accumulate or sentinel or ragged or cfg3 or fuzz" > "$OUT/k5tests.log" 2>&1 ;;
