@@ -25,6 +25,7 @@
 #                then the headline with PSKV_EARLY=1 twice
 #   graph        tools/graph_probe.py: one rotation of the benchmarked steps as a HIP graph vs launched eagerly
 #                (cfg 2 and rank 0 of N = 8)
+#   emuzipf      bench.py as rank 0 of 8 and of 4, alone, with the cfg-3 (Zipf) measurement (time-limited)
 #   ranks8diag   bench.py as 8 ranks on one GPU: headline only, then with the Zipf measurement
 #   ranks48      bench.py as 4 and as 8 ranks on one GPU (gloo, shared device; --sets 4): the N = 4 / 8 code path
 #   k5tests      the K5 (unhinted Add) parity tests: Zipf, radix, random, accumulate, sentinel, ragged, full-size cfg 3
@@ -129,6 +130,10 @@ for step in "$@"; do
           --no-cpu-baseline > "$OUT/early1_$r.json" 2> "$OUT/early1_$r.err" || exit 1; done ;;
     graph) timeout -k 10 300 python3 "$R/tools/graph_probe.py" 10 > "$OUT/graph_n1.log" 2>&1 &&
         PSKV_BENCH_EMULATE=0/8 timeout -k 10 300 python3 "$R/tools/graph_probe.py" 10 > "$OUT/graph_r0of8.log" 2>&1 ;;
+    emuzipf) PSKV_BENCH_EMULATE=0/4 timeout -k 10 120 python3 "$R/bench.py" --steps 5 --warmup 2 --sets 4 --no-extra \
+          --no-cpu-baseline > "$OUT/emuzipf4.json" 2> "$OUT/emuzipf4.err" &&
+        PSKV_BENCH_EMULATE=0/8 timeout -k 10 120 python3 "$R/bench.py" --steps 5 --warmup 2 --sets 4 --no-extra \
+          --no-cpu-baseline > "$OUT/emuzipf8.json" 2> "$OUT/emuzipf8.err" ;;
     ranks8diag) PSKV_BENCH_BACKEND=gloo PSKV_BENCH_SHARE_GPU=1 timeout -k 10 170 python3 -m torch.distributed.run \
           --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29611 "$R/bench.py" --gpus 8 --steps 5 \
           --warmup 2 --sets 4 --no-zipf --no-extra > "$OUT/ranks8_nozipf.json" 2> "$OUT/ranks8_nozipf.err" &&
