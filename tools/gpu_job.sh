@@ -28,6 +28,7 @@
 #   emuzipf      bench.py as rank 0 of 8 and of 4, alone, with the cfg-3 (Zipf) measurement (time-limited)
 #   ranks8diag   bench.py as 8 ranks on one GPU: headline only, then with the Zipf measurement
 #   ranks48      bench.py as 4 and as 8 ranks on one GPU (gloo, shared device; --sets 4): the N = 4 / 8 code path
+#   zsweep       tools/zipf_probe.py: K5 bucket bits / resolve table / windows / K5a block at the head, 10 rounds
 #   k5tests      the K5 (unhinted Add) parity tests: Zipf, radix, random, accumulate, sentinel, ragged, full-size cfg 3
 #   abk1         bench A/B of ab/libpskv_{base,k1occ6,k1occ4}.so (K1 held to 8 / 6 / 4 workgroups per CU), headline and rank 0 of 8
 #   fuzz         tests/test_fuzz.py over FUZZ_SCENARIOS (1500) new seeds from FUZZ_SEED0 (3500), single and concurrent
@@ -145,6 +146,8 @@ for step in "$@"; do
             --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29600 + n)) "$R/bench.py" --gpus $n --steps 5 \
             --warmup 2 --sets 4 > "$OUT/ranks$n.json" 2> "$OUT/ranks$n.err" || exit 1
         done ;;
+    zsweep) PROBE_ROUNDS=10 timeout -k 10 500 python3 "$R/tools/zipf_probe.py" "" "PSKV_RB_TB=10" "PSKV_RB_APPLY_LOG2=13" \
+          "PSKV_RB_WBITS=12" "PSKV_RB_WBITS=10" "PSKV_RB_BIN_BLOCK=512" > "$OUT/zsweep.log" 2>&1 ;;
     k5tests) timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread \
           "$R/tests/test_gpu_parity.py" "$R/tests/test_fuzz.py" -m gpu \
           -k "zipf or radix or random or accumulate or sentinel or ragged or cfg3 or fuzz" > "$OUT/k5tests.log" 2>&1 ;;
