@@ -467,8 +467,11 @@ def cpu_baseline(bases, B, n_batches, vector_sizes):
 def vector_storage_fit(oracle, sizes):
     """Config 1 (VectorStorage Add+Get of n contiguous float keys,
     server/vector_storage_test.cpp's shape) timed at several n; Get is the
-    O(stored x queried) scan of vector_storage.hpp:34-43, so t(n) is fitted with
-    a quadratic and extrapolated to the config's 1e6 keys."""
+    O(stored x queried) scan of vector_storage.hpp:34-43, so t(n) = a * n^2
+    (least squares, no lower-order terms: a quadratic scan has no intercept and
+    no negative linear part -- round 4's full quadratic fit had both and
+    extrapolated 288 s where the measured run took 215 s) is extrapolated to
+    the config's 1e6 keys.  The one measured 1e6 run is carried beside it."""
     import threading
 
     pts = []
@@ -496,15 +499,17 @@ def vector_storage_fit(oracle, sizes):
         vec.close()
     ns = np.array([p[0] for p in pts], dtype=np.float64)
     ts = np.array([p[1] for p in pts], dtype=np.float64)
-    coef = np.polyfit(ns, ts, 2) if len(pts) >= 3 else np.array([ts[-1] / ns[-1] ** 2, 0.0, 0.0])
-    t1e6 = float(np.polyval(coef, 1e6))
+    a = float(np.sum(ts * ns ** 2) / np.sum(ns ** 4))
+    t1e6 = a * 1e12
     return {"samples": [{"n": int(n), "seconds": t, "GB/s": 24.0 * n / t / 1e9} for n, t in pts],
-            "fit_seconds": {"a_n2": float(coef[0]), "b_n": float(coef[1]), "c": float(coef[2])},
+            "fit_seconds": {"a_n2": a, "form": "t = a * n^2, least squares"},
             "extrapolated_1e6_seconds": t1e6,
             "value": 24.0 * 1e6 / t1e6 / 1e9, "unit": "GB/s",
+            "measured_1e6": {"seconds": 215.0, "GB/s": 24.0 * 1e6 / 215.0 / 1e9,
+                             "source": "bench.py --vector-only --vector-sizes 1000000 on an MI355X box's host "
+                                       "(AMD EPYC 9575F), profiles/r03_vector_storage_1e6.log"},
             "sample": "VectorStorage restatement (append + O(stored x queried) last-match scan), config 1's "
-                      "contiguous float keys at the sizes listed, 1 thread; value = the quadratic fit at 1e6 keys "
-                      "(the measured 1e6 run, bench.py --vector-only: profiles/r03_vector_storage_1e6.log, 215 s)"}
+                      "contiguous float keys at the sizes listed, 1 thread; value = the a*n^2 fit at 1e6 keys"}
 
 
 def _cpu_model():
@@ -711,14 +716,21 @@ def zipf_sparse(rank, world, dev, lo, hi, B, steps, J=8):
     progress("cfg 3: batches built")
     uniq = int(torch.unique(zb[0][0]).numel())
     u_all = int(torch.unique(torch.cat([k for k, _ in zb])).numel())
+    progress("cfg 3: distinct keys counted")
     with ps.Shard(lo, hi, np.float32, device=dev.index) as sh:
+        progress("cfg 3: shard created")
         sh.set_stream(torch.cuda.current_stream().cuda_stream)
         adds = sh.prepare(zb)
         gets = sh.prepare([(k, o) for (k, _), o in zip(zb, zo)], is_get=True)
-        for _ in range(2):
+        for i in range(2):
             sh.add_grouped(adds)
+            sh.sync()  # bounded (SYNC_TIMEOUT_MS): a K5 that never completes is reported, not waited on
+            if i == 0:
+                progress("cfg 3: first Add (K5) complete")
             sh.get_grouped(gets)
-        torch.cuda.synchronize()
+            sh.sync()
+            if i == 0:
+                progress("cfg 3: first Get (K1) complete")
         # self-check: every key in the tail of the LAST batch was last written
         # there (a later write would be later in that tail), so it reads its
         # last occurrence's value
@@ -726,7 +738,10 @@ def zipf_sparse(rank, world, dev, lo, hi, B, steps, J=8):
         kk, vv = zb[-1][0].cpu().numpy(), zb[-1][1].cpu().numpy()
         last.update(zip(kk[-4096:].tolist(), vv[-4096:].tolist()))
         probe = torch.tensor(list(last), dtype=torch.int32, device=dev)
-        got = sh.get(probe).cpu().numpy()
+        progress("cfg 3: probe keys resident")
+        got_t = sh.get(probe)
+        sh.sync()
+        got = got_t.cpu().numpy()
         assert np.array_equal(got, np.array([last[int(x)] for x in probe.cpu().numpy()], np.float32)), \
             "zipf self-check failed"
         progress("cfg 3: self-check done")
@@ -955,13 +970,29 @@ def cold_form(dev, J, B, R, steps, warmup, space, n_pulls):
 _T0 = time.perf_counter()
 
 
+_RANK_TAG = f" r{os.environ['RANK']}" if int(os.environ.get("WORLD_SIZE", "1")) > 1 else ""
+
+
 def progress(what):
-    """One line per phase on stderr (a long run shows where it is)."""
-    print(f"bench [{time.perf_counter() - _T0:7.1f} s] {what}", file=sys.stderr, flush=True)
+    """One line per phase on stderr (a long run shows where it is; rank-tagged
+    at N > 1)."""
+    print(f"bench{_RANK_TAG} [{time.perf_counter() - _T0:7.1f} s] {what}", file=sys.stderr, flush=True)
+
+
+def watchdog():
+    """PSKV_BENCH_WATCHDOG=<s> (diagnostics, never set by the driver): every s
+    seconds dump every thread's Python stack to stderr, so a run that stops
+    making progress shows where each rank waits."""
+    s = float(os.environ.get("PSKV_BENCH_WATCHDOG", "0") or 0)
+    if s > 0:
+        import faulthandler
+
+        faulthandler.dump_traceback_later(s, repeat=True, file=sys.stderr)
 
 
 def main(argv=None):
     args = parse(argv)
+    watchdog()
     if args.vector_only:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle  # test infrastructure: the CPU baseline leg (VectorStorage restatement)

@@ -184,7 +184,12 @@ int pskv_add_get_grouped(pskv_shard* s, const pskv_batch* adds, uint64_t na, con
                          uint64_t ng, int flags);
 
 /* Wait for the shard's stream, grow the overflow table if needed, report
- * sticky device errors. */
+ * sticky device errors.  Every host wait of the library (this one, a host
+ * Get's, the staging and scratch waits, destroy's) is bounded by the option
+ * SYNC_TIMEOUT_MS (default 120000; 0 = unbounded): work that does not complete
+ * in time fails the call with PSKV_ESTATE, and pskv_last_error() names the
+ * stream or event waited for, the device and the last kernel the shard
+ * queued.  Nothing is cancelled or restarted. */
 int pskv_sync(pskv_shard* s);
 /* Zero every value (dense array and overflow table). */
 int pskv_clear(pskv_shard* s);
@@ -203,7 +208,8 @@ int pskv_shard_info(pskv_shard* s, pskv_info* info);
  * PAGEABLE_DMA, DMA_MIN_BYTES, DMA_MIN_BYTES_GET,
  * DMA_MIN_BYTES_PINNED, ZC_MAX_BYTES, FRAME_ZC_MAX_BYTES, INLINE,
  * INLINE_ADD_CHUNKS, INLINE_GET_CHUNKS, ISPIN, SERVE, SERVE_IDLE_US,
- * TILE_SHIFT, TILE_GRID, RB_WBITS, RB_NBD, RB_TB, RB_APPLY_LOG2, RB_BIN_BLOCK.
+ * TILE_SHIFT, TILE_GRID, RB_WBITS, RB_NBD, RB_TB, RB_APPLY_LOG2, RB_BIN_BLOCK,
+ * SYNC_TIMEOUT_MS (the bound of every host wait, pskv_sync).
  * Every option changes speed only, never results.  Some apply only together
  * with others (a value is accepted and echoed either way):
  *   EARLY = 1     K2g with UNROLL 8 and NT 1 (otherwise the default loads)
@@ -213,7 +219,8 @@ int pskv_shard_info(pskv_shard* s, pskv_info* info);
  * pskv_set_option returns PSKV_EINVAL for an unknown name or a value out of
  * range (the shard is unchanged).  The environment variable PSKV_<NAME> sets a
  * creation default; an invalid value there is reported on stderr and ignored
- * (the built-in default stays; creation does not fail). */
+ * (the built-in default stays; creation does not fail); so is a retired
+ * option's variable (RB_INSERT, GET_DEDUP, GET_NTP, FUSE). */
 int pskv_set_option(pskv_shard* s, const char* name, int64_t value);
 int pskv_get_option(pskv_shard* s, const char* name, int64_t* value);
 

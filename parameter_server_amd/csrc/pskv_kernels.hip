@@ -1223,6 +1223,68 @@ __device__ __forceinline__ uint32_t lds_insert(uint32_t* hk, uint32_t* sent,
   return own;
 }
 
+// K5a's insert: the streamed form below (1), or lds_insert (0; the A/B base)
+#ifndef PSKV_K5A_STREAM
+#define PSKV_K5A_STREAM 1
+#endif
+
+// The same insert with collisions deferred into the lane's key stream (round 5,
+// K5a).  lds_insert issues one compare-and-swap instruction per key position
+// and then, per position, a probe instruction for as long as ANY of the 64
+// lanes is still colliding there: the wave pays the sum over positions of the
+// worst lane's probe count (~27 CAS instructions per 8 keys at K5a's table
+// load on cfg-3 Zipf, in a model of the table; tools/k5_probe_model.py).  Here
+// every lane walks its own keys as one stream, one CAS per step: a step places
+// the current key or moves it one slot on, and a placed key hands the next
+// step to the lane's next key.  The wave then pays the worst lane's TOTAL
+// (~15 per 8 keys), each instruction as full as the lanes' work allows.  The
+// price is a dependent LDS round trip per step (the other 15 waves of the
+// workgroup keep the LDS busy meanwhile) and a few VALU per step to pick the
+// lane's current key and record its slot.  Same results as lds_insert: the
+// first lane to CAS a key into a slot owns it (bit q of the return), later
+// ones find it.
+// valid_mask must be a prefix (positions 0..n-1): K5a's element order makes it
+// one (li_of is increasing in q).  The sentinel key 0xFFFFFFFF goes through the
+// same CAS instruction, aimed at the side word (0 -> 1: the lane that flips it
+// owns the key).
+template <int PER, int SLOTS>
+__device__ __forceinline__ uint32_t lds_insert_stream(uint32_t* hk, uint32_t* sent,
+                                                      const uint32_t (&key)[PER], uint32_t valid_mask,
+                                                      uint32_t (&slot)[PER]) {
+  const uint32_t n = (uint32_t)__builtin_popcount(valid_mask);
+  // the lane's keys as a shift register: kq[0] is the current key, position
+  // cq.  Static indices only -- an index by the lane-varying cq is lowered to
+  // a scratch array
+  uint32_t kq[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    kq[q] = key[q];
+    slot[q] = kEmpty32;
+  }
+  uint32_t own = 0, cq = 0;
+  uint32_t h = fmix32(kq[0]) & (SLOTS - 1);
+  while (cq < n) {
+    const uint32_t ck = kq[0];
+    const bool sen = ck == kEmpty32;
+    uint32_t* const a = sen ? sent : &hk[h];
+    const uint32_t o = atomicCAS(a, sen ? 0u : kEmpty32, sen ? 1u : ck);
+    const bool mine = sen ? o == 0u : o == kEmpty32;
+    if (sen || mine || o == ck) {  // placed: the next key takes the next step
+      const uint32_t at = sen ? (uint32_t)SLOTS : h;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) slot[i] = cq == (uint32_t)i ? at : slot[i];
+      own |= mine ? (1u << cq) : 0u;
+      ++cq;
+#pragma unroll
+      for (int i = 0; i + 1 < PER; ++i) kq[i] = kq[i + 1];
+      h = fmix32(kq[0]) & (SLOTS - 1);
+    } else {
+      h = (h + 1) & (SLOTS - 1);
+    }
+  }
+  return own;
+}
+
 // An empty asm that reads x: the compiler's wait-count pass must have x's loads
 // complete here.  Used to place the wait for a software-pipelined register set
 // before the next set's loads are issued (see k_rb_bin, k_rb_resolve).
@@ -1367,7 +1429,11 @@ __global__ __launch_bounds__(BINB) void k_rb_bin(GroupArgs ga, DenseView d, RbMa
 #pragma unroll
     for (int q = 0; q < KPT; ++q) valid |= li_of(q) < cur.nvalid ? (1u << q) : 0u;
     uint32_t slot[KPT];
+#if PSKV_K5A_STREAM
+    const uint32_t own = lds_insert_stream<KPT, SLOTS>(hk, &sent, kc, valid, slot);
+#else
     const uint32_t own = lds_insert<KPT, SLOTS>(hk, &sent, kc, valid, slot);
+#endif
 #pragma unroll
     for (int q = 0; q < KPT; ++q) {
       if (!(valid >> q & 1u)) continue;

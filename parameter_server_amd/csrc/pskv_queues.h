@@ -21,12 +21,13 @@ namespace pskv {
 
 constexpr int kMaxDevices = 64;
 
-// GPU_MAX_HW_QUEUES as HIP reads it (unset, empty, non-numeric or < 1: 4).
+// GPU_MAX_HW_QUEUES as HIP reads it: the runtime accepts 1..32 and treats
+// anything else (unset, empty, non-numeric, < 1 or > 32) as its default 4.
 inline int hw_queues_from_env(const char* v) {
   if (!v || !*v) return 4;
   char* end = nullptr;
   const long q = std::strtol(v, &end, 10);
-  if (end == v || *end != '\0' || q < 1 || q > 1024) return 4;
+  if (end == v || *end != '\0' || q < 1 || q > 32) return 4;
   return static_cast<int>(q);
 }
 

@@ -112,9 +112,13 @@ def complement_windows(push_bases, lo: int, hi: int, batch: int = MILLION, seed:
     weak-scaled cfg 4): every `batch`-aligned window slot of [lo, hi) that the
     step's push set does not touch, in a seeded random order, at most n_max of
     them.  The pull then reads only parameters the step did not write, and reads
-    each once (no repeated window inside one Get)."""
+    each once (no repeated window inside one Get).  A push window that starts
+    off the slot grid covers two slots; both count as touched."""
     slots = (hi - lo) // batch
-    pushed = {(int(b) - lo) // batch for b in push_bases}
+    pushed = set()
+    for b in push_bases:
+        first, last = (int(b) - lo) // batch, (int(b) + batch - 1 - lo) // batch
+        pushed.update(range(first, last + 1))
     free = np.array([s for s in range(slots) if s not in pushed], dtype=np.int64)
     free = free[np.random.default_rng(seed).permutation(free.size)]
     if n_max is not None:
@@ -122,19 +126,27 @@ def complement_windows(push_bases, lo: int, hi: int, batch: int = MILLION, seed:
     return lo + free * batch
 
 
-def disjoint_windows(push_bases, n: int, key_space: int, batch: int = MILLION, seed: int = 0) -> np.ndarray:
+def disjoint_windows(push_bases, n: int, key_space: int, batch: int = MILLION, seed: int = 0,
+                     max_draws: int = 100_000) -> np.ndarray:
     """The pull windows of a cfg-4 step: n windows at uniformly random bases in
     [0, key_space - batch] (any alignment), drawn in turn with seed `seed` + s and
     redrawn until the window meets neither a pushed window nor an earlier pull
-    window — zero push/pull overlap, no key pulled twice."""
+    window — zero push/pull overlap, no key pulled twice.  A window that finds
+    no free place within `max_draws` draws (the push and pull windows cannot
+    fit the key space: too many or too large batches) raises ValueError instead
+    of drawing for ever."""
     taken = sorted((int(b), int(b) + batch) for b in push_bases)
     out = []
     for s in range(n):
         rng = np.random.default_rng(seed + s)
-        while True:
+        for _ in range(max_draws):
             b = int(rng.integers(0, key_space - batch + 1))
             if all(e <= b or b + batch <= a for a, e in taken):
                 break
+        else:
+            raise ValueError(f"disjoint_windows: pull window {s} of {n} ({batch} keys) found no place free of "
+                             f"{len(push_bases)} push and {s} pull windows in a {key_space}-key space after "
+                             f"{max_draws} draws")
         taken.append((b, b + batch))
         out.append(b)
     return np.asarray(out, dtype=np.int64)

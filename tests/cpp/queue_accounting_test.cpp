@@ -33,6 +33,11 @@ int main() {
   EXPECT(hw_queues_from_env("8x") == 4);
   EXPECT(hw_queues_from_env("8") == 8);
   EXPECT(hw_queues_from_env("32") == 32);
+  // beyond the runtime's range (1..32) HIP keeps its default, and so do we
+  EXPECT(hw_queues_from_env("33") == 4);
+  EXPECT(hw_queues_from_env("64") == 4);
+  EXPECT(hw_queues_from_env("1024") == 4);
+  EXPECT(hw_queues_from_env("1") == 1);
   {
     // one shard on a device, default 4 queues: 2*1 + 1 = 3 <= 4 -> serves
     DeviceQueues q;

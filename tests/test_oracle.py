@@ -162,6 +162,12 @@ def test_disjoint_and_complement_windows():
     assert len(workload.complement_windows([0], 0, 100, 20, seed=3, n_max=2)) == 2
     c2 = workload.complement_windows([1000, 1040], 1000, 1100, 20, seed=1)
     assert sorted(int(x) for x in c2) == [1020, 1060, 1080]
+    # an unaligned push window touches two slots: neither is pulled
+    c3 = workload.complement_windows([10, 65], 0, 100, 20, seed=2)
+    assert sorted(int(x) for x in c3) == [40]
+    # a pull that cannot fit raises instead of drawing for ever
+    with pytest.raises(ValueError, match="found no place"):
+        workload.disjoint_windows([0, 30, 60], 2, 100, 30, seed=1, max_draws=1000)
 
 
 def test_interval_union_and_global_windows():

@@ -25,7 +25,7 @@ def known_case_names():
 
     with open(os.path.join(ROOT, "tests", "golden", "reference_known_answers.json")) as f:
         k = json.load(f)
-    return [c["name"] for c in k["model_cases"] + k["util_cases"]]
+    return [c["name"] for c in k["model_cases"] + k["util_cases"] + k.get("restatement_cases", [])]
 
 
 @pytest.mark.parametrize("model", ["ssp", "bsp", "asp"])

@@ -14,6 +14,7 @@
 #   zpmc         tools/zipf_pmc.sh: wave-state, LDS and HBM counters of the cfg-3 path
 #   k5phases     tools/micro/k5_phases (diagnostic build: K5a / K5b phase stamps), assign and accumulate
 #   k5dist       the same (assign) on Zipf keys, uniform keys and a uniform pool matched to Zipf's distinct count
+#   k5ab         ab/diag_{base,new}/k5_phases (assign, accumulate), then abz: base vs new K5 build phase stamps and times
 #   abz          tools/ab_lib.sh with AB_PROG=zipf: ab/libpskv_base.so vs ab/libpskv_new.so on cfg 3, 3 rounds each
 #   sizes        tools/size_probe.py: K2g / K1 time against window count (fixed cost per launch)
 #   abs          tools/ab_lib.sh with AB_PROG=sizes: base vs new library under tools/size_probe.py
@@ -27,6 +28,8 @@
 #                (cfg 2 and rank 0 of N = 8)
 #   emuzipf      bench.py as rank 0 of 8 and of 4, alone, with the cfg-3 (Zipf) measurement (time-limited)
 #   ranks8diag   bench.py as 8 ranks on one GPU: headline only, then with the Zipf measurement
+#   ranks8z      every rank of N = 8 alone with cfg 3 (emulated), then bench.py as 8 ranks on one GPU with cfg 3 at
+#                GPU_MAX_HW_QUEUES = 1 and 4 (bounded waits, Python stack dumps every 30 s)
 #   ranks48      bench.py as 4 and as 8 ranks on one GPU (gloo, shared device; --sets 4): the N = 4 / 8 code path
 #   zsweep       tools/zipf_probe.py: K5 bucket bits / resolve table / windows / K5a block at the head, 10 rounds
 #   k5tests      the K5 (unhinted Add) parity tests: Zipf, radix, random, accumulate, sentinel, ragged, full-size cfg 3
@@ -106,6 +109,10 @@ for step in "$@"; do
     zpmc) timeout -k 10 600 bash "$R/tools/zipf_pmc.sh" "$(basename "$OUT")/zpmc" > "$OUT/zpmc.log" 2>&1 ;;
     k5phases) timeout -k 10 200 "$R/tools/micro/k5_phases" 0 > "$OUT/k5_phases_assign.log" 2>&1 &&
         timeout -k 10 200 "$R/tools/micro/k5_phases" 1 > "$OUT/k5_phases_accumulate.log" 2>&1 ;;
+    k5ab) for v in base new; do for m in 0 1; do
+          timeout -k 10 200 "$R/ab/diag_$v/k5_phases" $m > "$OUT/k5_phases_${v}_m$m.log" 2>&1 || exit 1
+        done; done &&
+        AB_PROG=zipf timeout -k 10 900 bash "$R/tools/ab_lib.sh" "$(basename "$OUT")/abz" > "$OUT/abz.log" 2>&1 ;;
     k5dist) for dist in zipf uniform matched; do
           timeout -k 10 200 "$R/tools/micro/k5_phases" 0 $dist > "$OUT/k5_phases_$dist.log" 2>&1 || exit 1
         done ;;
@@ -141,6 +148,16 @@ for step in "$@"; do
         PSKV_BENCH_BACKEND=gloo PSKV_BENCH_SHARE_GPU=1 timeout -k 10 170 python3 -m torch.distributed.run \
           --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29612 "$R/bench.py" --gpus 8 --steps 5 \
           --warmup 2 --sets 4 --no-extra > "$OUT/ranks8_zipf.json" 2> "$OUT/ranks8_zipf.err" ;;
+    ranks8z) for r in 1 2 3 4 5 6 7; do
+          PSKV_BENCH_EMULATE=$r/8 PSKV_SYNC_TIMEOUT_MS=30000 timeout -k 10 90 python3 "$R/bench.py" --steps 3 \
+            --warmup 1 --sets 2 --no-extra --no-cpu-baseline --no-cold > "$OUT/emuz8_$r.json" 2> "$OUT/emuz8_$r.err" || exit 1
+        done &&
+        for q in ${RANKS8_QUEUES:-1 4}; do
+          GPU_MAX_HW_QUEUES=$q PSKV_SYNC_TIMEOUT_MS=40000 PSKV_BENCH_WATCHDOG=30 PSKV_BENCH_BACKEND=gloo \
+            PSKV_BENCH_SHARE_GPU=1 timeout -k 10 150 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+            --master-addr 127.0.0.1 --master-port $((29620 + q)) "$R/bench.py" --gpus 8 --steps 3 --warmup 1 --sets 2 \
+            --no-extra > "$OUT/ranks8_q$q.json" 2> "$OUT/ranks8_q$q.err" || exit 1
+        done ;;
     ranks48) for n in 4 8; do
           PSKV_BENCH_BACKEND=gloo PSKV_BENCH_SHARE_GPU=1 timeout -k 10 500 python3 -m torch.distributed.run --nnodes=1 \
             --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29600 + n)) "$R/bench.py" --gpus $n --steps 5 \
