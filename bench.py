@@ -90,7 +90,7 @@ def parse(argv=None):
     p.add_argument("--cpu-batches", type=int, default=64,
                    help="1M-key windows in the 1-thread CPU baseline sample (~10 s)")
     p.add_argument("--vector-sizes", default="100000,200000,300000",
-                   help="VectorStorage restatement sample sizes (quadratic fit to 1e6)")
+                   help="VectorStorage restatement sample sizes (a*n^2 fit to 1e6)")
     p.add_argument("--vector-only", action="store_true",
                    help="time only the VectorStorage restatement at --vector-sizes (no GPU; e.g. the one "
                         "measured 1e6-key run of config 1) and print its JSON")
@@ -403,7 +403,7 @@ def run_form(form, steps, warmup, world, dev):
 def cpu_baseline(bases, B, n_batches, vector_sizes):
     """The oracle (C++ restatement of server/map_storage.hpp, 1 thread) on a
     bounded sample of the same workload; VectorStorage (cfg 1) at several sizes
-    with the quadratic fit extrapolated to config 1's 1e6 keys."""
+    with the a*n^2 fit extrapolated to config 1's 1e6 keys."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test infrastructure: the CPU baseline leg
 

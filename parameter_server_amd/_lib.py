@@ -11,7 +11,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpskv.so")
+# PSKV_LIB_PATH: a diagnostic build of the same library (tools/step_stamps.py);
+# never set by tests, smoke() or bench.py
+LIB_PATH = os.environ.get("PSKV_LIB_PATH") or os.path.join(_HERE, "libpskv.so")
 
 # keep in sync with include/pskv.h
 PSKV_OK = 0

@@ -223,6 +223,29 @@ __device__ __forceinline__ VT load_one(const DenseView& d, const Ovf& o, uint32_
   return s >= 0 ? reinterpret_cast<const VT*>(o.vals)[s] : VT(0);
 }
 
+// An empty asm that reads x: the compiler's wait-count pass must have x's loads
+// complete here.  Used to place the wait for a software-pipelined register set
+// before the next set's loads are issued (see k_rb_bin, k_rb_resolve).
+template <typename T, int N>
+__device__ __forceinline__ void ready(const T (&x)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" ::"v"(x[i]));
+}
+
+// Diagnostic build only (-DPSKV_STEP_STAMPS, tools/step_stamps.py): the
+// real-time clock (s_memrealtime, 100 MHz, one clock for every XCD) at phase
+// boundaries of every workgroup of the dense Add (K2g) and the Get (K1) of the
+// most recent launch: [kernel][workgroup][phase], phase 0 = entry; K2g: 1 =
+// prologue published, 2 = first chunk verified, 3 = last store issued; K1: 1 =
+// keys loaded, 2 = last store issued.  Read back by pskv_diag_step_stamps.
+#ifdef PSKV_STEP_STAMPS
+__device__ unsigned long long g_step_stamps[2][8192][4];
+#define STEP_STAMP(K, PH) \
+  if (threadIdx.x == 0 && blockIdx.x < 8192u) g_step_stamps[K][blockIdx.x][PH] = __builtin_amdgcn_s_memrealtime()
+#else
+#define STEP_STAMP(K, PH) (void)0
+#endif
+
 // ------------------------------------------------------------- K1 gather
 
 // Four keys of one lane: when they are four consecutive in-range keys (dense
@@ -298,17 +321,23 @@ __global__ __launch_bounds__(kBlock) void k_gather(GroupArgs ga, DenseView d, Ov
       return;
     }
   }
+  STEP_STAMP(1, 0);
   if (VEC && base + CH <= n) {
     uint32_t k[U][4];
 #pragma unroll
     for (int u = 0; u < U; ++u)
       Vec4<uint32_t>::load<NT>(keys + base + (uint64_t)(u * kBlock + tid) * 4, k[u]);
+#ifdef PSKV_STEP_STAMPS
+    ready(k[0]);
+    STEP_STAMP(1, 1);
+#endif
     VT v[U][4];
 #pragma unroll
     for (int u = 0; u < U; ++u) gather4<VT>(d, o, k[u], v[u]);
 #pragma unroll
     for (int u = 0; u < U; ++u)
       Vec4<VT>::template store<NT>(out + base + (uint64_t)(u * kBlock + tid) * 4, v[u]);
+    STEP_STAMP(1, 2);
   } else {
     // a partial (or unaligned) chunk: eight keys per lane loaded together,
     // then their gathers, then the stores — one dependent round trip per
@@ -825,8 +854,10 @@ __global__ __launch_bounds__(kBlock) void k_assign_group(GroupArgs ga, DenseView
       }
     }
   }
+  STEP_STAMP(0, 0);
   const GroupEnds g = group_prologue(ga, d, flag, epoch, s_first, s_last, &s_dense);
   __syncthreads();
+  STEP_STAMP(0, 1);
   bool bad = false;
   if (s_dense) {
     const uint32_t nchunks = ga.wg_prefix[ga.nb];
@@ -834,10 +865,12 @@ __global__ __launch_bounds__(kBlock) void k_assign_group(GroupArgs ga, DenseView
       uint32_t c = blockIdx.x;
       if (pre) {
         bad |= dense_chunk_own<U, NT, NTP, true>(ga, d, c, s_first, s_last, ek, ev);
+        STEP_STAMP(0, 2);
         c += gridDim.x;
       }
       for (; c < nchunks; c += gridDim.x)
         bad |= dense_chunk_own<U, NT, NTP, false>(ga, d, c, s_first, s_last, ek, ev);
+      STEP_STAMP(0, 3);
     } else {
       for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x)
         bad |= dense_chunk<VT, VEC, U, NT, NTP>(ga, d, c, s_first, s_last);
@@ -1223,77 +1256,6 @@ __device__ __forceinline__ uint32_t lds_insert(uint32_t* hk, uint32_t* sent,
   return own;
 }
 
-// K5a's insert: the streamed form below (1), or lds_insert (0; the A/B base)
-#ifndef PSKV_K5A_STREAM
-#define PSKV_K5A_STREAM 1
-#endif
-
-// The same insert with collisions deferred into the lane's key stream (round 5,
-// K5a).  lds_insert issues one compare-and-swap instruction per key position
-// and then, per position, a probe instruction for as long as ANY of the 64
-// lanes is still colliding there: the wave pays the sum over positions of the
-// worst lane's probe count (~27 CAS instructions per 8 keys at K5a's table
-// load on cfg-3 Zipf, in a model of the table; tools/k5_probe_model.py).  Here
-// every lane walks its own keys as one stream, one CAS per step: a step places
-// the current key or moves it one slot on, and a placed key hands the next
-// step to the lane's next key.  The wave then pays the worst lane's TOTAL
-// (~15 per 8 keys), each instruction as full as the lanes' work allows.  The
-// price is a dependent LDS round trip per step (the other 15 waves of the
-// workgroup keep the LDS busy meanwhile) and a few VALU per step to pick the
-// lane's current key and record its slot.  Same results as lds_insert: the
-// first lane to CAS a key into a slot owns it (bit q of the return), later
-// ones find it.
-// valid_mask must be a prefix (positions 0..n-1): K5a's element order makes it
-// one (li_of is increasing in q).  The sentinel key 0xFFFFFFFF goes through the
-// same CAS instruction, aimed at the side word (0 -> 1: the lane that flips it
-// owns the key).
-template <int PER, int SLOTS>
-__device__ __forceinline__ uint32_t lds_insert_stream(uint32_t* hk, uint32_t* sent,
-                                                      const uint32_t (&key)[PER], uint32_t valid_mask,
-                                                      uint32_t (&slot)[PER]) {
-  const uint32_t n = (uint32_t)__builtin_popcount(valid_mask);
-  // the lane's keys as a shift register: kq[0] is the current key, position
-  // cq.  Static indices only -- an index by the lane-varying cq is lowered to
-  // a scratch array
-  uint32_t kq[PER];
-#pragma unroll
-  for (int q = 0; q < PER; ++q) {
-    kq[q] = key[q];
-    slot[q] = kEmpty32;
-  }
-  uint32_t own = 0, cq = 0;
-  uint32_t h = fmix32(kq[0]) & (SLOTS - 1);
-  while (cq < n) {
-    const uint32_t ck = kq[0];
-    const bool sen = ck == kEmpty32;
-    uint32_t* const a = sen ? sent : &hk[h];
-    const uint32_t o = atomicCAS(a, sen ? 0u : kEmpty32, sen ? 1u : ck);
-    const bool mine = sen ? o == 0u : o == kEmpty32;
-    if (sen || mine || o == ck) {  // placed: the next key takes the next step
-      const uint32_t at = sen ? (uint32_t)SLOTS : h;
-#pragma unroll
-      for (int i = 0; i < PER; ++i) slot[i] = cq == (uint32_t)i ? at : slot[i];
-      own |= mine ? (1u << cq) : 0u;
-      ++cq;
-#pragma unroll
-      for (int i = 0; i + 1 < PER; ++i) kq[i] = kq[i + 1];
-      h = fmix32(kq[0]) & (SLOTS - 1);
-    } else {
-      h = (h + 1) & (SLOTS - 1);
-    }
-  }
-  return own;
-}
-
-// An empty asm that reads x: the compiler's wait-count pass must have x's loads
-// complete here.  Used to place the wait for a software-pipelined register set
-// before the next set's loads are issued (see k_rb_bin, k_rb_resolve).
-template <typename T, int N>
-__device__ __forceinline__ void ready(const T (&x)[N]) {
-#pragma unroll
-  for (int i = 0; i < N; ++i) asm volatile("" ::"v"(x[i]));
-}
-
 // K5a k_rb_bin: persistent workgroups of BINB threads over super-chunks of
 // SC = 8 * BINB keys of one batch (4-byte values; 4 * BINB for 8-byte ones),
 // the next super-chunk's loads in flight.  BINB = 1024: one workgroup per CU
@@ -1429,11 +1391,15 @@ __global__ __launch_bounds__(BINB) void k_rb_bin(GroupArgs ga, DenseView d, RbMa
 #pragma unroll
     for (int q = 0; q < KPT; ++q) valid |= li_of(q) < cur.nvalid ? (1u << q) : 0u;
     uint32_t slot[KPT];
-#if PSKV_K5A_STREAM
-    const uint32_t own = lds_insert_stream<KPT, SLOTS>(hk, &sent, kc, valid, slot);
-#else
+    // (Round 5 measured a streamed insert -- each lane walking its keys as one
+    // stream of compare-and-swaps, a collided key retried in the next step
+    // instead of in a probe round of its own: ~15 instead of ~27 CAS
+    // instructions per wave in a model of the table, tools/k5_probe_model.py
+    // -- and it LOST: insert 17.8 K against 15.5 K cycles per pass, K5 +2 %,
+    // profiles/r05_probes/k5ab/.  Each step's dependent LDS round trip and
+    // the ~50 VALU picking the lane's key and recording its slot cost more
+    // than the probe instructions it saved.)
     const uint32_t own = lds_insert<KPT, SLOTS>(hk, &sent, kc, valid, slot);
-#endif
 #pragma unroll
     for (int q = 0; q < KPT; ++q) {
       if (!(valid >> q & 1u)) continue;
@@ -2787,6 +2753,18 @@ hipError_t launch_inline_get(int vb, const InlineGet& a, const DenseView& d, con
 }
 
 }  // namespace pskv
+
+#ifdef PSKV_STEP_STAMPS
+// Diagnostic build only: copy out (then clear) the K2g / K1 step stamps,
+// 2 x 8192 x 4 u64 ([K2g|K1][workgroup][phase], 0 = not reached).
+extern "C" int pskv_diag_step_stamps(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pskv::g_step_stamps), sizeof(pskv::g_step_stamps)) != hipSuccess)
+    return -2;
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(pskv::g_step_stamps)) != hipSuccess) return -2;
+  return hipMemset(p, 0, sizeof(pskv::g_step_stamps)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 #ifdef PSKV_K5_STAMPS
 // Diagnostic build only: copy out (then clear) the K5 phase stamps, 2 x 512 x 8

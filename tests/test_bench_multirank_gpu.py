@@ -1,6 +1,7 @@
 """bench.py's N > 1 path end to end, as the driver launches it
 (`python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr
-127.0.0.1 ... bench.py --gpus N`), rehearsed on one GPU: two rank processes,
+127.0.0.1 ... bench.py --gpus N`), rehearsed on one GPU: two and four rank
+processes,
 gloo for the barrier and the reductions, both ranks' shards on cuda:0
 (PSKV_BENCH_BACKEND=gloo, PSKV_BENCH_SHARE_GPU=1 — rehearsal knobs the driver
 never sets).  Every rank runs cfg 4's self-check (its pulls against a model of
@@ -29,23 +30,26 @@ def _free_port():
     return p
 
 
-def test_bench_two_ranks_one_gpu(cuda):
-    env = dict(os.environ, PSKV_BENCH_BACKEND="gloo", PSKV_BENCH_SHARE_GPU="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_ranks_one_gpu(cuda, world):
+    # bounded host waits (SYNC_TIMEOUT_MS): a rank whose work never completes
+    # fails with the wait it was in instead of hanging the run
+    env = dict(os.environ, PSKV_BENCH_BACKEND="gloo", PSKV_BENCH_SHARE_GPU="1", PSKV_SYNC_TIMEOUT_MS="60000")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1", "--sets", "4"]
+           os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "3", "--warmup", "1", "--sets", "4"]
     r = subprocess.run(["timeout", "-k", "10", "400"] + cmd, capture_output=True, text=True, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-5000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-3000:]
     res = json.loads(lines[0])
-    assert res["n_gpus"] == 2 and res["steps"] == 3 and res["scaling"] == "strong"
+    assert res["n_gpus"] == world and res["steps"] == 3 and res["scaling"] == "strong"
     assert res["value"] > 0 and res["unit"] == "GB/s"
     cfg = res["config"]
-    assert cfg["key_space"] == 1_000_000_000 and cfg["shard_keys_per_gpu"] == 500_000_000
+    assert cfg["key_space"] == 1_000_000_000 and cfg["shard_keys_per_gpu"] == 1_000_000_000 // world
     assert cfg["push_pull_overlap_keys"] == 0
     assert res["per_gpu"]["min_GB/s"] <= res["per_gpu"]["max_GB/s"]
     assert "k_gather" in res["roofline"]["kernels"] and "k_assign_group" in res["roofline"]["kernels"]
     assert "cold" not in res["roofline"]  # the cold form is an N = 1 figure
-    assert res["zipf_sparse"]["n_gpus"] == 2
+    assert res["zipf_sparse"]["n_gpus"] == world  # cfg 3 on every rank
     assert res["extra"]["weak_scaled"]["GB/s"] > 0

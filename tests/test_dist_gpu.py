@@ -1,6 +1,6 @@
-"""cfg 4's multi-rank path on the GPU: two rank processes (gloo, both on cuda:0,
-bench.py's PSKV_BENCH_SHARE_GPU rehearsal setup) each own one 5e8-key range
-shard of the 1e9-key space (base/range_partition_manager.hpp's map) and run
+"""cfg 4's multi-rank path on the GPU: two or four rank processes (gloo, all on
+cuda:0, bench.py's PSKV_BENCH_SHARE_GPU rehearsal setup) each own one range
+shard of the 1e9-key space (5e8 / 2.5e8 keys) (base/range_partition_manager.hpp's map) and run
 bench.py's own step — 64 producer windows at uniformly random bases, sliced by
 the range map (straddling windows split), pushed as one grouped Add per rank,
 then windows no push of the step touched pulled — through the timed region (barrier,
@@ -47,14 +47,14 @@ def _rank(rank, world, port, q):
         dev = torch.device("cuda:0")
         J, B, R = 64, 1_000_000, 3
         sets = [bench.make_set(rank, world, J, B, dev, r) for r in range(2)]
-        # a third set whose windows surely straddle the 5e8 boundary (and
+        # a third set whose windows surely straddle every range boundary (and
         # overlap each other across it): the range map splits each in two
-        mid = 500_000_000
-        sets.append(bench.make_set(rank, world, 4, B, dev, 2,
-                                   bases=np.array([mid - 300_001, mid - 999_999, mid - 1, mid - 300_001])))
-        assert len(sets[2]["slices"]) == 4 and all(n < B for _, _, n in sets[2]["slices"])
+        bases = straddle_bases(world)
+        sets.append(bench.make_set(rank, world, len(bases), B, dev, 2, bases=bases))
+        own_edges = sum(1 for m in edges(world) if m in (rank * (10 ** 9 // world), (rank + 1) * (10 ** 9 // world)))
+        assert len(sets[2]["slices"]) == 4 * own_edges and all(n < B for _, _, n in sets[2]["slices"])
         _, lo, hi, _, _ = bench.plan_rank(rank, world, J, B)
-        assert hi - lo == 500_000_000
+        assert hi - lo == 1_000_000_000 // world
         ref = np.zeros(hi - lo, np.float32)
         host = [[(f, v.cpu().numpy()) for (_, f, _), (_, v) in zip(s["slices"], s["batches"])] for s in sets]
         with ps.Shard(lo, hi, np.float32, device=0) as sh:
@@ -100,25 +100,36 @@ def _rank(rank, world, port, q):
         raise
 
 
-def test_cfg4_two_ranks_bit_exact():
+def edges(world):
+    """The inner range boundaries of the 1e9-key space over `world` shards."""
+    return [r * (10 ** 9 // world) for r in range(1, world)]
+
+
+def straddle_bases(world):
+    """Four windows across every boundary m: m - 300001, m - 999999, m - 1 and
+    m - 300001 again (a repeated, overlapping window)."""
+    return np.array([b for m in edges(world) for b in (m - 300_001, m - 999_999, m - 1, m - 300_001)])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_cfg4_ranks_bit_exact(world):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    world = 2
     ps = [ctx.Process(target=_rank, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
     res = []
     for _ in range(world):
-        res.append(q.get(timeout=240))
+        res.append(q.get(timeout=300))
     for p in ps:
         p.join(60)
     errs = [r for r in res if r[1] != "ok"]
     assert not errs, "\n".join(str(e[2]) for e in errs)
     assert all(p.exitcode == 0 for p in ps)
     res.sort()
-    # every set's windows arrived whole over the two ranks (split ones in two)
-    assert res[0][4] == (2 * 64 + 4) * 1_000_000
+    # every set's windows arrived whole over the ranks (split ones in two)
+    assert res[0][4] == (2 * 64 + len(straddle_bases(world))) * 1_000_000
     assert all(r[2] > 0 and r[3] >= 4 and r[5] > 0 for r in res)

@@ -605,12 +605,12 @@ def test_device_overflow_burst_fails_loudly(cuda, path):
 
 def test_bounded_waits_report_pending_work(cuda):
     """Every host wait is bounded (option SYNC_TIMEOUT_MS, round 5; VERDICT r4
-    item 1): with ~3 s of earlier work on the legacy default stream -- which the
-    shard's own blocking stream orders behind -- a sync, a device Get's host
-    read-back and a host Get fail with PSKV_ESTATE after the 300 ms bound, the
-    message naming the stream waited for and the last kernel the shard queued;
-    nothing is cancelled, so once the bound is lifted the same shard completes
-    and reads what was written, bit-exact."""
+    item 1): with ~3 s of earlier work on the stream the shard runs on (torch's
+    current stream, pskv_set_stream), a sync and a host Get fail with
+    PSKV_ESTATE after the 300 ms bound, the message naming the stream waited
+    for and the last kernel the shard queued; nothing is cancelled, so once the
+    bound is lifted the same shard completes and reads what was written,
+    bit-exact."""
     import torch
 
     import parameter_server_amd as ps
@@ -626,10 +626,15 @@ def test_bounded_waits_report_pending_work(cuda):
     v = (k * 0.5).astype(np.float32)
     with ps.Shard(0, 10_000, np.float32, options={"SYNC_TIMEOUT_MS": 300}) as sh:
         assert sh.get_option("SYNC_TIMEOUT_MS") == 300
+        sh.set_stream(torch.cuda.current_stream().cuda_stream)
         sh.add(k, v)
         sh.sync()
-        torch.cuda._sleep(int(3000 * cycles_per_ms))  # ~3 s on the null stream
-        sh.add(tdev(k, cuda), tdev(v + 1, cuda))  # queued behind it (K5)
+        # device inputs made BEFORE the sleep: a pageable host-to-device copy
+        # made after it would wait for it inside torch
+        kd, vd = tdev(k, cuda), tdev(v + 1, cuda)
+        torch.cuda.synchronize()
+        torch.cuda._sleep(int(3000 * cycles_per_ms))  # ~3 s ahead of the shard's work
+        sh.add(kd, vd)  # queued behind it (K5)
         # the sync waits behind the sleep and the queued K5 Add; the host Get
         # of 1000 keys goes out as inline K8 launches and polls their reply
         for what, call, last in (("sync", sh.sync, "K5"), ("host get", lambda: sh.get(k[:1000]), "K8")):
@@ -641,6 +646,7 @@ def test_bounded_waits_report_pending_work(cuda):
         sh.set_option("SYNC_TIMEOUT_MS", 0)  # unbounded: the queued work completes
         sh.sync()
         assert np.array_equal(sh.get(k), v + 1)
+        sh.set_stream(None)
 
 
 def test_size_mismatch_is_rejected(cuda):

@@ -14,6 +14,8 @@
 #   zpmc         tools/zipf_pmc.sh: wave-state, LDS and HBM counters of the cfg-3 path
 #   k5phases     tools/micro/k5_phases (diagnostic build: K5a / K5b phase stamps), assign and accumulate
 #   k5dist       the same (assign) on Zipf keys, uniform keys and a uniform pool matched to Zipf's distinct count
+#   stamps       tools/step_stamps.py (ab/stamps/libpskv.so, -DPSKV_STEP_STAMPS): K2g / K1 workgroup phase times of
+#                rank 0 and 1 of N = 8 and of the N = 1 headline step
 #   k5ab         ab/diag_{base,new}/k5_phases (assign, accumulate), then abz: base vs new K5 build phase stamps and times
 #   abz          tools/ab_lib.sh with AB_PROG=zipf: ab/libpskv_base.so vs ab/libpskv_new.so on cfg 3, 3 rounds each
 #   sizes        tools/size_probe.py: K2g / K1 time against window count (fixed cost per launch)
@@ -109,6 +111,10 @@ for step in "$@"; do
     zpmc) timeout -k 10 600 bash "$R/tools/zipf_pmc.sh" "$(basename "$OUT")/zpmc" > "$OUT/zpmc.log" 2>&1 ;;
     k5phases) timeout -k 10 200 "$R/tools/micro/k5_phases" 0 > "$OUT/k5_phases_assign.log" 2>&1 &&
         timeout -k 10 200 "$R/tools/micro/k5_phases" 1 > "$OUT/k5_phases_accumulate.log" 2>&1 ;;
+    stamps) for spec in 0/8 1/8 0/1; do
+          PSKV_LIB_PATH=$R/ab/stamps/libpskv.so timeout -k 10 200 python3 "$R/tools/step_stamps.py" $spec 20 \
+            > "$OUT/stamps_${spec/\//of}.log" 2>&1 || exit 1
+        done ;;
     k5ab) for v in base new; do for m in 0 1; do
           timeout -k 10 200 "$R/ab/diag_$v/k5_phases" $m > "$OUT/k5_phases_${v}_m$m.log" 2>&1 || exit 1
         done; done &&
