@@ -1256,6 +1256,75 @@ __device__ __forceinline__ uint32_t lds_insert(uint32_t* hk, uint32_t* sent,
   return own;
 }
 
+// Hybrid insert (A/B candidate, PSKV_K5A_INSERT=2): the first CAS of every
+// key position issued back to back as in lds_insert, then ONE retry stream per
+// lane over its collided positions (one CAS per step; a placed key hands the
+// next step to the lane's next collided key) instead of a probe loop per
+// position -- the wave pays the worst lane's total of retries, not the sum
+// over positions of each position's worst lane.
+template <int PER, int SLOTS>
+__device__ __forceinline__ uint32_t lds_insert_hybrid(uint32_t* hk, uint32_t* sent,
+                                                      const uint32_t (&key)[PER], uint32_t valid_mask,
+                                                      uint32_t (&slot)[PER]) {
+  uint32_t old[PER];
+  uint32_t own = 0, pend = 0;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    slot[q] = kEmpty32;
+    old[q] = 0;
+    if (!(valid_mask >> q & 1u)) continue;
+    if (key[q] == kEmpty32) {
+      slot[q] = SLOTS;
+      own |= atomicCAS(sent, 0u, 1u) == 0u ? (1u << q) : 0u;
+      old[q] = key[q];
+    } else {
+      slot[q] = fmix32(key[q]) & (SLOTS - 1);
+      old[q] = atomicCAS(&hk[slot[q]], kEmpty32, key[q]);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    if (!(valid_mask >> q & 1u) || key[q] == kEmpty32) continue;
+    if (old[q] == kEmpty32)
+      own |= 1u << q;
+    else if (old[q] != key[q])
+      pend |= 1u << q;
+  }
+  // the retry stream: cq = the lowest collided position, h its next slot
+  auto pick = [&](uint32_t cq, const uint32_t (&a)[PER]) {
+    uint32_t x = a[0];
+#pragma unroll
+    for (int i = 1; i < PER; ++i) {
+      asm volatile("" : "+v"(x));  // keep the select chain (an index by cq would go to scratch)
+      x = cq == (uint32_t)i ? a[i] : x;
+    }
+    return x;
+  };
+  uint32_t cq = (uint32_t)__builtin_ctz(pend | (1u << PER));
+  uint32_t ck = pick(cq, key);
+  uint32_t h = (pick(cq, slot) + 1u) & (SLOTS - 1);
+  while (pend) {
+    const uint32_t o = atomicCAS(&hk[h], kEmpty32, ck);
+    if (o == kEmpty32 || o == ck) {
+#pragma unroll
+      for (int i = 0; i < PER; ++i) slot[i] = cq == (uint32_t)i ? h : slot[i];
+      own |= o == kEmpty32 ? (1u << cq) : 0u;
+      pend &= pend - 1u;
+      cq = (uint32_t)__builtin_ctz(pend | (1u << PER));
+      ck = pick(cq, key);
+      h = (pick(cq, slot) + 1u) & (SLOTS - 1);
+    } else {
+      h = (h + 1) & (SLOTS - 1);
+    }
+  }
+  return own;
+}
+
+// K5a's insert for the A/B builds: 0 = lds_insert (default), 2 = lds_insert_hybrid
+#ifndef PSKV_K5A_INSERT
+#define PSKV_K5A_INSERT 0
+#endif
+
 // K5a k_rb_bin: persistent workgroups of BINB threads over super-chunks of
 // SC = 8 * BINB keys of one batch (4-byte values; 4 * BINB for 8-byte ones),
 // the next super-chunk's loads in flight.  BINB = 1024: one workgroup per CU
@@ -1399,7 +1468,11 @@ __global__ __launch_bounds__(BINB) void k_rb_bin(GroupArgs ga, DenseView d, RbMa
     // profiles/r05_probes/k5ab/.  Each step's dependent LDS round trip and
     // the ~50 VALU picking the lane's key and recording its slot cost more
     // than the probe instructions it saved.)
+#if PSKV_K5A_INSERT == 2
+    const uint32_t own = lds_insert_hybrid<KPT, SLOTS>(hk, &sent, kc, valid, slot);
+#else
     const uint32_t own = lds_insert<KPT, SLOTS>(hk, &sent, kc, valid, slot);
+#endif
 #pragma unroll
     for (int q = 0; q < KPT; ++q) {
       if (!(valid >> q & 1u)) continue;

@@ -32,6 +32,7 @@
 #   ranks8diag   bench.py as 8 ranks on one GPU: headline only, then with the Zipf measurement
 #   ranks8z      every rank of N = 8 alone with cfg 3 (emulated), then bench.py as 8 ranks on one GPU with cfg 3 at
 #                GPU_MAX_HW_QUEUES = 1 and 4 (bounded waits, Python stack dumps every 30 s)
+#   ranks8q      bench.py as RANKS8_N (8) ranks on one GPU with cfg 3 at GPU_MAX_HW_QUEUES in RANKS8_QUEUES (4)
 #   ranks48      bench.py as 4 and as 8 ranks on one GPU (gloo, shared device; --sets 4): the N = 4 / 8 code path
 #   zsweep       tools/zipf_probe.py: K5 bucket bits / resolve table / windows / K5a block at the head, 10 rounds
 #   k5tests      the K5 (unhinted Add) parity tests: Zipf, radix, random, accumulate, sentinel, ragged, full-size cfg 3
@@ -163,6 +164,13 @@ for step in "$@"; do
             PSKV_BENCH_SHARE_GPU=1 timeout -k 10 150 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
             --master-addr 127.0.0.1 --master-port $((29620 + q)) "$R/bench.py" --gpus 8 --steps 3 --warmup 1 --sets 2 \
             --no-extra > "$OUT/ranks8_q$q.json" 2> "$OUT/ranks8_q$q.err" || exit 1
+        done ;;
+    ranks8q) for q in ${RANKS8_QUEUES:-4}; do
+          GPU_MAX_HW_QUEUES=$q PSKV_SYNC_TIMEOUT_MS=40000 PSKV_BENCH_WATCHDOG=30 PSKV_BENCH_BACKEND=gloo \
+            PSKV_BENCH_SHARE_GPU=1 timeout -k 10 ${RANKS8_LIMIT:-150} python3 -m torch.distributed.run --nnodes=1 \
+            --nproc-per-node ${RANKS8_N:-8} --master-addr 127.0.0.1 --master-port $((29640 + q)) "$R/bench.py" \
+            --gpus ${RANKS8_N:-8} --steps 3 --warmup 1 --sets 2 --no-extra \
+            > "$OUT/ranks${RANKS8_N:-8}_q$q.json" 2> "$OUT/ranks${RANKS8_N:-8}_q$q.err" || exit 1
         done ;;
     ranks48) for n in 4 8; do
           PSKV_BENCH_BACKEND=gloo PSKV_BENCH_SHARE_GPU=1 timeout -k 10 500 python3 -m torch.distributed.run --nnodes=1 \
