@@ -1256,7 +1256,7 @@ __device__ __forceinline__ uint32_t lds_insert(uint32_t* hk, uint32_t* sent,
   return own;
 }
 
-// Hybrid insert (A/B candidate, PSKV_K5A_INSERT=2): the first CAS of every
+// Hybrid insert (K5a, round 5): the first CAS of every
 // key position issued back to back as in lds_insert, then ONE retry stream per
 // lane over its collided positions (one CAS per step; a placed key hands the
 // next step to the lane's next collided key) instead of a probe loop per
@@ -1319,11 +1319,6 @@ __device__ __forceinline__ uint32_t lds_insert_hybrid(uint32_t* hk, uint32_t* se
   }
   return own;
 }
-
-// K5a's insert for the A/B builds: 0 = lds_insert (default), 2 = lds_insert_hybrid
-#ifndef PSKV_K5A_INSERT
-#define PSKV_K5A_INSERT 0
-#endif
 
 // K5a k_rb_bin: persistent workgroups of BINB threads over super-chunks of
 // SC = 8 * BINB keys of one batch (4-byte values; 4 * BINB for 8-byte ones),
@@ -1468,11 +1463,11 @@ __global__ __launch_bounds__(BINB) void k_rb_bin(GroupArgs ga, DenseView d, RbMa
     // profiles/r05_probes/k5ab/.  Each step's dependent LDS round trip and
     // the ~50 VALU picking the lane's key and recording its slot cost more
     // than the probe instructions it saved.)
-#if PSKV_K5A_INSERT == 2
+    // (round 5) the hybrid insert: insert phase 15.5 K -> 13.7 K cycles per
+    // pass (assign; accumulate 18.3 K -> 17.1 K), K5 145.9 -> 142.8 us
+    // (accumulate 195.1 -> 191.7) over 3 interleaved rounds,
+    // profiles/r05_probes/k5ab_hybrid/
     const uint32_t own = lds_insert_hybrid<KPT, SLOTS>(hk, &sent, kc, valid, slot);
-#else
-    const uint32_t own = lds_insert<KPT, SLOTS>(hk, &sent, kc, valid, slot);
-#endif
 #pragma unroll
     for (int q = 0; q < KPT; ++q) {
       if (!(valid >> q & 1u)) continue;
