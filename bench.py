@@ -137,6 +137,27 @@ def barrier(world):
         dist.barrier()
 
 
+def in_turns(world, fn):
+    """Run fn() on every rank; in the shared-device rehearsal
+    (PSKV_BENCH_SHARE_GPU=1, several ranks on ONE GPU, never the driver's
+    run) one rank at a time.  Heavy torch setup (the cfg-3 Zipf draw over a
+    1e8-key CDF, torch.unique) issued by several processes at once on one
+    device was measured to stall for minutes, pskv code or not (DESIGN.md §8,
+    tools/proc_share_probe.py); one at a time it takes ~0.2 s a rank."""
+    if world == 1 or os.environ.get("PSKV_BENCH_SHARE_GPU") != "1":
+        return fn()
+    import torch
+    import torch.distributed as dist
+
+    out = None
+    for r in range(world):
+        if r == dist.get_rank():
+            out = fn()
+            torch.cuda.synchronize()
+        dist.barrier()
+    return out
+
+
 def _reduce_device(dev):
     import torch.distributed as dist
 
@@ -710,13 +731,15 @@ def zipf_sparse(rank, world, dev, lo, hi, B, steps, J=8):
     from parameter_server_amd import _lib, workload
 
     space = hi - lo
-    zb = workload.zipf_batches(J, space, batch=B, device=dev, perm_seed=7 + rank, seed=42 + 1000 * rank,
-                               lo=lo)
+
+    def draw():
+        zb_ = workload.zipf_batches(J, space, batch=B, device=dev, perm_seed=7 + rank, seed=42 + 1000 * rank,
+                                    lo=lo)
+        return zb_, int(torch.unique(zb_[0][0]).numel()), int(torch.unique(torch.cat([k for k, _ in zb_])).numel())
+
+    zb, uniq, u_all = in_turns(world, draw)
     zo = [torch.empty_like(v) for _, v in zb]
-    progress("cfg 3: batches built")
-    uniq = int(torch.unique(zb[0][0]).numel())
-    u_all = int(torch.unique(torch.cat([k for k, _ in zb])).numel())
-    progress("cfg 3: distinct keys counted")
+    progress("cfg 3: batches built, distinct keys counted")
     with ps.Shard(lo, hi, np.float32, device=dev.index) as sh:
         progress("cfg 3: shard created")
         sh.set_stream(torch.cuda.current_stream().cuda_stream)
@@ -775,7 +798,7 @@ def zipf_sparse(rank, world, dev, lo, hi, B, steps, J=8):
         kernels[n] = {"avg_ms": ms, "algorithmic_bytes": b, "GB/s": b / (ms * 1e-3) / 1e9,
                       "frac": b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
     progress("cfg 3: timed; random-access floor")
-    floor = random_access_floor(zb, lo, space, dev)
+    floor = in_turns(world, lambda: random_access_floor(zb, lo, space, dev))
     if floor is not None:
         k5_ms = kernels["k_rb_bin+k_rb_resolve (K5 Add)"]["avg_ms"]
         k1_ms = kernels["k_gather (K1 Get)"]["avg_ms"]
