@@ -204,7 +204,8 @@ int pskv_shard_info(pskv_shard* s, pskv_info* info);
 
 /* Tuning and path options of one shard, by name (DESIGN.md §5 lists them and
  * what each selects): GENERAL (0 = K4 stamps, 1 = auto, 2 = K5 always),
- * UNROLL, NT, NTP, EARLY (K2g early loads: 0 never, 1 always, 2 auto),
+ * UNROLL, GET_UNROLL (K1's keys per lane: 0 = by launch size, 4, 8), NT, NTP,
+ * EARLY (K2g early loads: 0 never, 1 always, 2 auto),
  * PAGEABLE_DMA, DMA_MIN_BYTES, DMA_MIN_BYTES_GET,
  * DMA_MIN_BYTES_PINNED, ZC_MAX_BYTES, FRAME_ZC_MAX_BYTES, INLINE,
  * INLINE_ADD_CHUNKS, INLINE_GET_CHUNKS, ISPIN, SERVE, SERVE_IDLE_US,

@@ -260,6 +260,7 @@ struct pskv_shard {
   // against 111.4 us; 2048 / 1024: 116.5 / 117.3; profiles/r04_probes/k2g_tune/)
   uint32_t tune_tile_grid = 65536;
   int tune_unroll = 8;   // PSKV_UNROLL: 4 or 8 (8: measured +5 % on the dense Add)
+  int tune_get_unroll = 0;  // PSKV_GET_UNROLL: K1's keys per lane, 4 or 8, 0 = by launch size
   bool tune_nt = true;   // PSKV_NT: non-temporal streams (measured +12-15 % on K1 / K2g)
   // PSKV_NTP: non-temporal parameter stores in the dense Add (K2g).  On
   // since round 4: cached stores leave the Add's parameter lines dirty in the
@@ -343,7 +344,19 @@ struct pskv_shard {
 
 namespace {
 
-int gather_unroll(const pskv_shard* s) { return s->tune_unroll; }
+// K1's keys per lane (8 x 4 or 4 x 4, i.e. 8 Ki- or 4 Ki-key chunks) for a
+// launch of `elems` keys.  Option GET_UNROLL: 4 or 8, or 0 = by size (round 5):
+// a launch of under kGetSmallKeys keys takes 4 x 4 -- a cfg-4 rank's Get at
+// N = 8 (~8 M keys) ran K1 in 17.5 against 18.4 us with the smaller chunks
+// (ranks 0 and 1 emulated, twice each, profiles/r05_probes/emu_u48/), where
+// the dense Add's K2g lost with them (22.0 against 21.2 us), so the two are
+// chosen apart; UNROLL = 4 still forces 4 x 4 on both.
+constexpr uint64_t kGetSmallKeys = 24ull << 20;
+int gather_unroll(const pskv_shard* s, uint64_t elems) {
+  if (s->tune_get_unroll) return s->tune_get_unroll;
+  if (s->tune_unroll == 4) return 4;
+  return elems < kGetSmallKeys ? 4 : 8;
+}
 
 int use_device(pskv_shard* s) {
   PSKV_HIP(hipSetDevice(s->device));
@@ -1593,11 +1606,12 @@ int zero_copy_get_views(pskv_shard* s, const std::vector<pskv_batch>& hv) {
   for (auto& b : hv) vec &= aligned16(b.keys) & aligned16(b.vals);
   for (auto& g : split_groups(hv)) {
     GroupArgs ga;
-    const uint32_t nwg = build_group(hv, g.first, g.second, stream_chunk(gather_unroll(s)), &ga);
     uint64_t elems = 0;
     for (size_t i = g.first; i < g.second; ++i) elems += hv[i].n;
+    const int gu = gather_unroll(s, elems);
+    const uint32_t nwg = build_group(hv, g.first, g.second, stream_chunk(gu), &ga);
     LaunchTimer t(s, PSKV_K_GATHER, elems);
-    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, ga, nwg, s->dview(), s->ovf, s->stream));
+    PSKV_HIP(launch_gather(s->vb, vec, gu, s->tune_nt, ga, nwg, s->dview(), s->ovf, s->stream));
     t.done();
   }
   if (int rc = wait_stream(s, s->stream, "shard stream (Get into page-locked memory)")) return rc;
@@ -1624,11 +1638,12 @@ int zero_copy_get(pskv_shard* s, const std::vector<pskv_batch>& v, bool vec) {
   }
   for (auto& g : split_groups(hv)) {
     GroupArgs ga;
-    const uint32_t nwg = build_group(hv, g.first, g.second, stream_chunk(gather_unroll(s)), &ga);
     uint64_t elems = 0;
     for (size_t i = g.first; i < g.second; ++i) elems += hv[i].n;
+    const int gu = gather_unroll(s, elems);
+    const uint32_t nwg = build_group(hv, g.first, g.second, stream_chunk(gu), &ga);
     LaunchTimer t(s, PSKV_K_GATHER, elems);
-    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, ga, nwg, s->dview(), s->ovf, s->stream));
+    PSKV_HIP(launch_gather(s->vb, vec, gu, s->tune_nt, ga, nwg, s->dview(), s->ovf, s->stream));
     t.done();
   }
   if (int rc = wait_stream(s, s->stream, "shard stream (zero-copy Get)")) return rc;
@@ -1689,11 +1704,12 @@ int pinned_get(pskv_shard* s, const std::vector<pskv_batch>& v) {
       PSKV_HIP(hipMemcpyAsync(const_cast<uint32_t*>(dv[i].keys), v[i].keys, v[i].n * 4, hipMemcpyHostToDevice,
                               s->stream));
     GroupArgs ga;
-    const uint32_t nwg = build_group(dv, b, e, stream_chunk(gather_unroll(s)), &ga);
     uint64_t elems = 0;
     for (size_t i = b; i < e; ++i) elems += dv[i].n;
+    const int gu = gather_unroll(s, elems);
+    const uint32_t nwg = build_group(dv, b, e, stream_chunk(gu), &ga);
     LaunchTimer t(s, PSKV_K_GATHER, elems);
-    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, ga, nwg, s->dview(),
+    PSKV_HIP(launch_gather(s->vb, vec, gu, s->tune_nt, ga, nwg, s->dview(),
                            s->ovf, s->stream));
     t.done();
     PSKV_HIP(hipEventRecord(s->out_events[w], s->stream));
@@ -1783,11 +1799,12 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
   for (auto& b : dv) vec &= aligned16(b.keys) & aligned16(b.vals);
   for (auto& g : split_groups(dv)) {
     GroupArgs ga;
-    const uint32_t nwg = build_group(dv, g.first, g.second, stream_chunk(gather_unroll(s)), &ga);
     uint64_t elems = 0;
     for (size_t i = g.first; i < g.second; ++i) elems += dv[i].n;
+    const int gu = gather_unroll(s, elems);
+    const uint32_t nwg = build_group(dv, g.first, g.second, stream_chunk(gu), &ga);
     LaunchTimer t(s, PSKV_K_GATHER, elems);
-    PSKV_HIP(launch_gather(s->vb, vec, gather_unroll(s), s->tune_nt, ga, nwg, s->dview(), s->ovf,
+    PSKV_HIP(launch_gather(s->vb, vec, gu, s->tune_nt, ga, nwg, s->dview(), s->ovf,
                            s->stream));
     t.done();
   }
@@ -1881,6 +1898,7 @@ const Option kOptions[] = {
     // the environment form also takes "stamps" / "auto" / "radix"
     PSKV_OPT("GENERAL", 0, 2, general_path, int),
     PSKV_OPT("UNROLL", 4, 8, tune_unroll, int),              // 4 or 8 (others: 8)
+    PSKV_OPT("GET_UNROLL", 0, 8, tune_get_unroll, int),      // 0 (by size), 4 or 8
     PSKV_OPT("NT", 0, 1, tune_nt, bool),
     PSKV_OPT("NTP", 0, 1, tune_ntp, bool),
     PSKV_OPT("EARLY", 0, 2, tune_early, int),
@@ -1916,6 +1934,8 @@ const Option* find_option(const char* name) {
 int set_option(pskv_shard* s, const Option& o, int64_t v) {
   if (v < o.lo || v > o.hi) return fail(PSKV_EINVAL, std::string("option ") + o.name + ": value out of range");
   if (std::strcmp(o.name, "UNROLL") == 0 && v != 4 && v != 8) return fail(PSKV_EINVAL, "option UNROLL: 4 or 8");
+  if (std::strcmp(o.name, "GET_UNROLL") == 0 && v != 0 && v != 4 && v != 8)
+    return fail(PSKV_EINVAL, "option GET_UNROLL: 0, 4 or 8");
   if (std::strcmp(o.name, "TILE_SHIFT") == 0 && v != 0 && v < 10) return fail(PSKV_EINVAL, "option TILE_SHIFT: 0 or 10..20");
   if (std::strcmp(o.name, "RB_APPLY_LOG2") == 0 && v != 0 && v != 13 && v != 14)
     return fail(PSKV_EINVAL, "option RB_APPLY_LOG2: 0, 13 or 14");
