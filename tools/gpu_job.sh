@@ -9,6 +9,7 @@
 #   emu8all      bench.py as each of the 8 ranks of N = 8 in turn (every rank's cfg-4 share alone)
 #   emu_curve    every rank of N = 2 and N = 4 emulated in turn (with emu8all: the estimated scaling curve)
 #   emutrace     rocprofv3 kernel trace of rank 0 of 8 (kernel durations and gaps of a small share)
+#   smalllat     tools/micro/small_latency (built with g++ against libpskv.so): per-call host Add / Get latency
 #   emu_u48      ranks 0 and 1 of N = 8 emulated at UNROLL 8 / 4 (8 / 4 Ki-key chunks for K2g and K1), twice
 #   emu_unroll   rank 0 of 8 at 4 x 4 keys per lane (PSKV_UNROLL=4) and at the default 8
 #   ztrace       rocprofv3 kernel trace of zipf_probe at K5a 1024 and 512 threads (K5a / K5b split)
@@ -110,6 +111,7 @@ for step in "$@"; do
           PSKV_BENCH_EMULATE=$r/8 PSKV_UNROLL=$u timeout -k 10 200 python3 "$R/bench.py" --steps 50 --no-zipf \
             --no-cpu-baseline --no-extra > "$OUT/emu8_${r}_u${u}_$rep.json" 2> "$OUT/emu8_${r}_u${u}_$rep.err" || exit 1
         done; done; done ;;
+    smalllat) timeout -k 10 300 "$R/tools/micro/small_latency" > "$OUT/small_latency.log" 2>&1 ;;
     ztrace) for v in 1024 512; do
           PSKV_RB_BIN_BLOCK=$v PROBE_ROUNDS=5 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/ztrace_$v" \
             -o run -- python3 "$R/tools/zipf_probe.py" > "$OUT/ztrace_$v.log" 2>&1 || exit 1
