@@ -40,6 +40,7 @@
 #include <string>
 #include <vector>
 
+#include "ps/callback_runner.hpp"
 #include "ps/consistency.hpp"
 #include "ps/hip_storage.hpp"
 #include "ps/consistent_hashing_partition_manager.hpp"
@@ -719,6 +720,101 @@ int known_answers(MakeStorage make, const char* label) {
     expect(p0.size() == 2 && p1.size() == 1, "buffer pops");
     expect(b.Size(0) == 0 && b.Size(1) == 0, "buffer empty after the pops");
     done("PendingBuffer PushAndPop");
+  }
+  {  // server_thread_test.cpp:35-120: one FIFO thread dispatches by flag
+    struct FakeModel : AbstractModel {
+      void Clock(Message&) override { ++clocks; }
+      void Add(Message&) override { ++adds; }
+      void Get(Message&) override { ++gets; }
+      int GetProgress(int) override { return -1; }
+      void ResetWorker(Message&) override {}
+      int clocks = 0, adds = 0, gets = 0;
+    };
+    {
+      ServerThread st(0);
+      st.RegisterModel(0, std::unique_ptr<AbstractModel>(new FakeModel()));
+      expect(st.GetModel(0) != nullptr, "server thread: registered model");
+      done("ServerThread RegisterModel");
+    }
+    const Flag flags[3] = {Flag::kClock, Flag::kAdd, Flag::kGet};
+    const int pushes[3] = {2, 1, 3};  // Clock x2, Add x1, Get x3 (:46-119)
+    const char* names[3] = {"ServerThread Clock", "ServerThread Add", "ServerThread Get"};
+    for (int c = 0; c < 3; ++c) {
+      ServerThread st(0);
+      st.RegisterModel(0, std::unique_ptr<AbstractModel>(new FakeModel()));
+      auto* p = static_cast<FakeModel*>(st.GetModel(0));
+      st.Start();
+      Message m;
+      m.meta.flag = flags[c];
+      m.meta.model_id = 0;
+      for (int i = 0; i < pushes[c]; ++i) st.GetWorkQueue()->Push(m);
+      Message ex;
+      ex.meta.flag = Flag::kExit;
+      st.GetWorkQueue()->Push(ex);
+      st.Stop();
+      const int got = c == 0 ? p->clocks : c == 1 ? p->adds : p->gets;
+      expect(got == pushes[c] && p->clocks + p->adds + p->gets == pushes[c], names[c]);
+      done(names[c]);
+    }
+  }
+  {  // callback_runner_test.cpp:19-108: replies handed to the receive handle,
+     // the finish handle after the last expected one, two app threads apart
+    auto reply_msg = [](std::vector<uint32_t> k, std::vector<float> v) {
+      Message m;
+      m.AddData(third_party::SArray<uint32_t>(k));
+      m.AddData(third_party::SArray<float>(v));
+      return m;
+    };
+    {
+      CallbackRunner runner;
+      std::map<uint32_t, float> reply;
+      bool finished = false;
+      runner.RegisterRecvHandle(0, 0, [&reply](Message& m) {
+        third_party::SArray<uint32_t> k(m.data[0]);
+        third_party::SArray<float> v(m.data[1]);
+        for (size_t i = 0; i < k.size(); ++i) reply.insert(std::make_pair(k[i], v[i]));
+      });
+      runner.RegisterRecvFinishHandle(0, 0, [&finished] { finished = true; });
+      runner.NewRequest(0, 0, 2);
+      Message r1 = reply_msg({3}, {0.1f}), r2 = reply_msg({4, 5, 6}, {0.4f, 0.2f, 0.3f});
+      runner.AddResponse(0, 0, r1);
+      runner.AddResponse(0, 0, r2);
+      runner.WaitRequest(0, 0);
+      const std::map<uint32_t, float> want{{3, 0.1f}, {4, 0.4f}, {5, 0.2f}, {6, 0.3f}};
+      expect(reply == want && finished, "callback runner: replies and finish");
+      done("CallbackRunner AddResponse");
+    }
+    {
+      CallbackRunner runner;
+      std::map<uint32_t, float> reply;
+      float sum = 0;
+      runner.RegisterRecvHandle(0, 0, [&reply](Message& m) {
+        third_party::SArray<uint32_t> k(m.data[0]);
+        third_party::SArray<float> v(m.data[1]);
+        for (size_t i = 0; i < k.size(); ++i) reply.insert(std::make_pair(k[i], v[i]));
+      });
+      runner.RegisterRecvFinishHandle(0, 0, [] {});
+      runner.NewRequest(0, 0, 2);
+      runner.RegisterRecvHandle(1, 0, [&sum](Message& m) {
+        third_party::SArray<float> v(m.data[1]);
+        for (size_t i = 0; i < v.size(); ++i) sum += v[i];
+      });
+      runner.RegisterRecvFinishHandle(1, 0, [] {});
+      runner.NewRequest(1, 0, 2);
+      Message r1 = reply_msg({3}, {0.1f}), r2 = reply_msg({4, 5, 6}, {0.4f, 0.2f, 0.3f});
+      runner.AddResponse(0, 0, r1);
+      runner.AddResponse(0, 0, r2);
+      runner.AddResponse(1, 0, r1);
+      runner.AddResponse(1, 0, r2);
+      runner.WaitRequest(0, 0);
+      const std::map<uint32_t, float> want{{3, 0.1f}, {4, 0.4f}, {5, 0.2f}, {6, 0.3f}};
+      expect(reply == want, "callback runner: worker 0 replies");
+      runner.WaitRequest(1, 0);
+      // the reference asserts EXPECT_EQ(sum, 1.0): 0.1f + 0.4f + 0.2f + 0.3f in
+      // this order is 1.0f exactly
+      expect(sum == 1.0f, "callback runner: worker 1 sum");
+      done("CallbackRunner AddResponseTwoWorkers");
+    }
   }
   std::printf("[%s] model known answers: %s\n", label, fails ? "FAIL" : "ok");
   return fails;

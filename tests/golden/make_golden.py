@@ -133,6 +133,23 @@ KNOWN = {
         {"name": "PendingBuffer PushAndPop", "cite": "server/util/pending_buffer_test.cpp:21-61",
          "ops": [["push", 0], ["push", 0], ["push", 1], ["size", 0, 2], ["size", 1, 1], ["pop", 0, 2],
                  ["pop", 1, 1]]},
+        # server/server_thread.cpp's dispatch (the path's caller)
+        {"name": "ServerThread RegisterModel", "cite": "server/server_thread_test.cpp:35-43",
+         "ops": [["register", 0], ["model_not_null", 0]]},
+        {"name": "ServerThread Clock", "cite": "server/server_thread_test.cpp:45-66",
+         "ops": [["push", "clock"], ["push", "clock"], ["exit"], ["count", "clock", 2]]},
+        {"name": "ServerThread Add", "cite": "server/server_thread_test.cpp:68-89",
+         "ops": [["push", "add"], ["exit"], ["count", "add", 1]]},
+        {"name": "ServerThread Get", "cite": "server/server_thread_test.cpp:91-114",
+         "ops": [["push", "get"], ["push", "get"], ["push", "get"], ["exit"], ["count", "get", 3]]},
+        # worker/callback_runner.cpp: where a worker's Get collects its replies
+        # (SURVEY §8 a12's producer side)
+        {"name": "CallbackRunner AddResponse", "cite": "worker/callback_runner_test.cpp:19-57",
+         "replies": [[[3], [0.1]], [[4, 5, 6], [0.4, 0.2, 0.3]]],
+         "expect": {"reply": {"3": 0.1, "4": 0.4, "5": 0.2, "6": 0.3}, "finished": True}},
+        {"name": "CallbackRunner AddResponseTwoWorkers", "cite": "worker/callback_runner_test.cpp:59-108",
+         "replies": [[[3], [0.1]], [[4, 5, 6], [0.4, 0.2, 0.3]]],
+         "expect": {"worker0_reply": {"3": 0.1, "4": 0.4, "5": 0.2, "6": 0.3}, "worker1_sum": 1.0}},
     ],
     "slice_cases": [
         {"cite": "base/range_partition_manager_test.cpp:19-33", "ranges": [[2, 4], [4, 7], [7, 10]],
