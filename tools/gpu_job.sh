@@ -10,6 +10,7 @@
 #   emu_curve    every rank of N = 2 and N = 4 emulated in turn (with emu8all: the estimated scaling curve)
 #   emutrace     rocprofv3 kernel trace of rank 0 of 8 (kernel durations and gaps of a small share)
 #   smalllat     tools/micro/small_latency (built with g++ against libpskv.so): per-call host Add / Get latency
+#   ablat        small_latency under ab/libpskv_{AB_VARIANTS}.so, twice each (the in-tree library restored after)
 #   emu_u48      ranks 0 and 1 of N = 8 emulated at UNROLL 8 / 4 (8 / 4 Ki-key chunks for K2g and K1), twice
 #   emu_unroll   rank 0 of 8 at 4 x 4 keys per lane (PSKV_UNROLL=4) and at the default 8
 #   ztrace       rocprofv3 kernel trace of zipf_probe at K5a 1024 and 512 threads (K5a / K5b split)
@@ -112,6 +113,11 @@ for step in "$@"; do
             --no-cpu-baseline --no-extra > "$OUT/emu8_${r}_u${u}_$rep.json" 2> "$OUT/emu8_${r}_u${u}_$rep.err" || exit 1
         done; done; done ;;
     smalllat) timeout -k 10 300 "$R/tools/micro/small_latency" > "$OUT/small_latency.log" 2>&1 ;;
+    ablat) L=$R/parameter_server_amd/libpskv.so; cp "$L" "$OUT/.keep.so" &&
+        for rep in 1 2; do for v in ${AB_VARIANTS:-base new}; do
+          cp "$R/ab/libpskv_$v.so" "$L" &&
+          timeout -k 10 300 "$R/tools/micro/small_latency" > "$OUT/small_latency_${v}_$rep.log" 2>&1 || { cp "$OUT/.keep.so" "$L"; exit 1; }
+        done; done; cp "$OUT/.keep.so" "$L"; rm -f "$OUT/.keep.so" ;;
     ztrace) for v in 1024 512; do
           PSKV_RB_BIN_BLOCK=$v PROBE_ROUNDS=5 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/ztrace_$v" \
             -o run -- python3 "$R/tools/zipf_probe.py" > "$OUT/ztrace_$v.log" 2>&1 || exit 1
