@@ -428,6 +428,10 @@ std::string wait_report(const pskv_shard* s, const char* what, const void* handl
 }
 
 int wait_event(pskv_shard* s, hipEvent_t ev, const char* what, const void* handle) {
+  if (!s->tune_sync_timeout_ms) {  // unbounded: the runtime's own blocking wait
+    const hipError_t e = hipEventSynchronize(ev);
+    return e == hipSuccess ? PSKV_OK : fail(PSKV_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+  }
   using Clock = std::chrono::steady_clock;
   const auto t0 = Clock::now();
   for (uint64_t it = 0;; ++it) {
@@ -449,6 +453,10 @@ int wait_event(pskv_shard* s, hipEvent_t ev, const char* what, const void* handl
 // The marker event keeps the default system-scope release, as the stream
 // synchronisation it replaces: host reads of pinned results see the writes.
 int wait_stream(pskv_shard* s, hipStream_t st, const char* what) {
+  if (!s->tune_sync_timeout_ms) {  // unbounded: the runtime's own blocking wait
+    const hipError_t e = hipStreamSynchronize(st);
+    return e == hipSuccess ? PSKV_OK : fail(PSKV_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+  }
   if (!s->sync_ev) PSKV_HIP(hipEventCreateWithFlags(&s->sync_ev, hipEventDisableTiming));
   PSKV_HIP(hipEventRecord(s->sync_ev, st));
   return wait_event(s, s->sync_ev, what, st);

@@ -113,6 +113,10 @@ for step in "$@"; do
             --no-cpu-baseline --no-extra > "$OUT/emu8_${r}_u${u}_$rep.json" 2> "$OUT/emu8_${r}_u${u}_$rep.err" || exit 1
         done; done; done ;;
     smalllat) timeout -k 10 300 "$R/tools/micro/small_latency" > "$OUT/small_latency.log" 2>&1 ;;
+    smalllat_sync) for rep in 1 2; do for t in 120000 0; do
+          SL_VARIANTS=0,6 PSKV_SYNC_TIMEOUT_MS=$t timeout -k 10 300 "$R/tools/micro/small_latency" \
+            > "$OUT/small_latency_t${t}_$rep.log" 2>&1 || exit 1
+        done; done ;;
     ablat) L=$R/parameter_server_amd/libpskv.so; cp "$L" "$OUT/.keep.so" &&
         for rep in 1 2; do for v in ${AB_VARIANTS:-base new}; do
           cp "$R/ab/libpskv_$v.so" "$L" &&

@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <string>
 #include <vector>
 
 #include "pskv.h"
@@ -71,6 +72,11 @@ int main() {
   constexpr int kVariants = 8;
   for (int pass = 0; pass < 2; ++pass)  // pass 0 warms the runtime up (its pageable-copy paths); pass 1 prints
   for (int var = 0; var < kVariants; ++var) {
+    // SL_VARIANTS="0,6": only those variants (quicker A/B runs)
+    if (const char* only = std::getenv("SL_VARIANTS")) {
+      const std::string list = std::string(",") + only + ",";
+      if (list.find("," + std::to_string(var) + ",") == std::string::npos) continue;
+    }
     const bool framed = var == 5 || var == 6;
     setenv("PSKV_SERVE", var == 7 ? "1" : "0", 1);  // K9: the resident request server
     const int flags = var == 6 ? PSKV_HOST | PSKV_HOST_FRAME : PSKV_HOST;
