@@ -201,3 +201,43 @@ def test_serve_start_waits_for_slow_stream_work(cuda, oracle_mod, serve):
         waited = time.perf_counter() - t0
     assert_bits_equal(got, ref.get(q), "after the slow dependency")
     assert waited > 2.0, f"the dependency did not delay the served calls ({waited:.2f} s): the test lost its point"
+
+
+def test_serve_wait_is_bounded(cuda, oracle_mod, serve):
+    """The request server's waits are bounded too (SYNC_TIMEOUT_MS):
+    a served Get queued behind ~3 s of earlier work on the shard's stream
+    fails with PSKV_ESTATE naming the server's dependency once the 500 ms
+    bound has passed, where it used to spin for as long as the dependency
+    ran; with the bound lifted the same shard serves the Get, bit-exact."""
+    import torch
+
+    import parameter_server_amd as ps
+    from parameter_server_amd import PskvError, _lib
+
+    rng = np.random.default_rng(37)
+    ref = oracle_mod.MapStorageRef(np.float32)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    torch.cuda._sleep(50_000_000)
+    e1.record()
+    torch.cuda.synchronize()
+    cycles_per_ms = 50_000_000 / max(e0.elapsed_time(e1), 1e-3)
+    with ps.Shard(0, 10_000, np.float32, options=dict(serve, SERVE_IDLE_US=1000, SYNC_TIMEOUT_MS=500)) as sh:
+        k = rng.integers(0, 10_000, size=100).astype(np.uint32)
+        v = rng.standard_normal(k.size).astype(np.float32)
+        sh.add(k, v)
+        ref.add(k, v)
+        assert_bits_equal(sh.get(k), ref.get(k), "before")
+        time.sleep(0.05)  # the server idles out
+        torch.cuda._sleep(int(3000 * cycles_per_ms))  # ~3 s of earlier work on the legacy stream
+        k2 = rng.integers(0, 10_000, size=100).astype(np.uint32)
+        v2 = rng.standard_normal(k2.size).astype(np.float32)
+        sh.add(k2, v2)  # relaunches the server behind the spin kernel
+        ref.add(k2, v2)
+        q = rng.integers(0, 10_000, size=300).astype(np.uint32)
+        with pytest.raises(PskvError) as ei:
+            sh.get(q)
+        assert ei.value.code == _lib.PSKV_ESTATE
+        assert "request-server" in str(ei.value) and "not complete after" in str(ei.value), str(ei.value)
+        sh.set_option("SYNC_TIMEOUT_MS", 0)
+        assert_bits_equal(sh.get(q), ref.get(q), "after the bound is lifted")
