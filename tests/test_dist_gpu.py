@@ -133,3 +133,54 @@ def test_cfg4_ranks_bit_exact(world):
     # every set's windows arrived whole over the ranks (split ones in two)
     assert res[0][4] == (2 * 64 + len(straddle_bases(world))) * 1_000_000
     assert all(r[2] > 0 and r[3] >= 4 and r[5] > 0 for r in res)
+
+
+_RCCL_PROBE = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+import torch
+import torch.distributed as dist
+
+import bench
+
+dev = torch.device("cuda:0")
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", device_id=dev)
+assert dist.get_backend() == "nccl"
+
+
+class Form:  # a step with real device work on torch's stream
+    def __init__(self):
+        self.x = torch.zeros(1 << 20, device=dev)
+
+    def step(self, i):
+        self.x.add_(1.0)
+
+
+f = Form()
+elapsed, own = bench.timed(f, 5, 2, dev)  # world 2: the collective path, on one rank
+assert elapsed == own > 0, (elapsed, own)
+assert float(f.x[0]) == 5.0
+assert bench.max_over_ranks(3.5, 2, dev) == 3.5
+assert bench.sum_over_ranks(2.25, 2, dev) == 2.25
+bench.barrier(2)
+dist.destroy_process_group()
+print("rccl ok")
+"""
+
+
+def test_rccl_synchronisation_one_rank(cuda):
+    """bench.py's N > 1 synchronisation over RCCL ("nccl" -- the backend of the
+    driver's multi-GPU run, which the gloo rehearsals above do not touch),
+    exercised on the one GPU a box has: a world-1 process group bound to
+    cuda:0 as dist_init binds it, the barrier-bracketed timed region, and the
+    float64 MAX / SUM all-reduces the ranks' timings and byte counts go
+    through (world passed as 2 so the collective path runs)."""
+    import subprocess
+    import sys
+
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
+               LOCAL_RANK="0")
+    r = subprocess.run(["timeout", "-k", "10", "120", sys.executable, "-c", _RCCL_PROBE, ROOT], capture_output=True,
+                       text=True, cwd=ROOT, env=env)
+    assert r.returncode == 0 and "rccl ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
