@@ -1855,7 +1855,11 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
         valid |= (uint32_t)q < len ? (1u << q) : 0u;
         key[q] = (uint32_t)q < len ? x[q].key : 0u;
       }
+#ifdef PSKV_K5B_HYBRID
+      lds_insert_hybrid<RPT, SLOTS>(ak, &sent, key, valid, slot);
+#else
       lds_insert<RPT, SLOTS>(ak, &sent, key, valid, slot);
+#endif
 #pragma unroll
       for (int q = 0; q < RPT; ++q) {
         if (!(valid >> q & 1u)) continue;

@@ -38,6 +38,7 @@
 #   ranks8q      bench.py as RANKS8_N (8) ranks on one GPU with cfg 3 at GPU_MAX_HW_QUEUES in RANKS8_QUEUES (4)
 #   ranks48      bench.py as 4 and as 8 ranks on one GPU (gloo, shared device; --sets 4): the N = 4 / 8 code path
 #   zsweep       tools/zipf_probe.py: K5 bucket bits / resolve table / windows / K5a block at the head, 10 rounds
+#   wsweep       tools/zipf_probe.py: K5 bucket window bits 11-14 on Zipf keys at 1e8 / 1.25e8 / 5e8 keys and on dense unhinted windows
 #   k5tests      the K5 (unhinted Add) parity tests: Zipf, radix, random, accumulate, sentinel, ragged, full-size cfg 3
 #   abk1         bench A/B of ab/libpskv_{base,k1occ6,k1occ4}.so (K1 held to 8 / 6 / 4 workgroups per CU), headline and rank 0 of 8
 #   fuzz         tests/test_fuzz.py over FUZZ_SCENARIOS (1500) new seeds from FUZZ_SEED0 (3500), single and concurrent
@@ -194,7 +195,11 @@ for step in "$@"; do
             --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29600 + n)) "$R/bench.py" --gpus $n --steps 5 \
             --warmup 2 --sets 4 > "$OUT/ranks$n.json" 2> "$OUT/ranks$n.err" || exit 1
         done ;;
-    zsweep) PROBE_ROUNDS=10 timeout -k 10 500 python3 "$R/tools/zipf_probe.py" "" "PSKV_RB_TB=10" "PSKV_RB_APPLY_LOG2=13" \
+    wsweep) for sp in 1e8 1.25e8 5e8; do PROBE_SPACE=$sp PROBE_ROUNDS=10 timeout -k 10 300 python3 -u "$R/tools/zipf_probe.py" "" \
+          "PSKV_RB_WBITS=12" "PSKV_RB_WBITS=13" "PSKV_RB_WBITS=14" > "$OUT/wsweep_$sp.log" 2>&1 || exit 1; done &&
+        PROBE_WORKLOAD=dense PROBE_ROUNDS=10 timeout -k 10 300 python3 -u "$R/tools/zipf_probe.py" "" "PSKV_RB_WBITS=12" \
+          "PSKV_RB_WBITS=13" > "$OUT/wsweep_dense.log" 2>&1 ;;
+    zsweep) PROBE_ROUNDS=10 timeout -k 10 500 python3 -u "$R/tools/zipf_probe.py" "" "PSKV_RB_TB=10" "PSKV_RB_APPLY_LOG2=13" \
           "PSKV_RB_WBITS=12" "PSKV_RB_WBITS=10" "PSKV_RB_BIN_BLOCK=512" > "$OUT/zsweep.log" 2>&1 ;;
     k5tests) timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread \
           "$R/tests/test_gpu_parity.py" "$R/tests/test_fuzz.py" -m gpu \
