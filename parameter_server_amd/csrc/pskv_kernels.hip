@@ -1575,7 +1575,9 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
   // f64 sums take 8 B per slot: half the slots in the same LDS
   constexpr int SLOTS = (MODE == 1 && sizeof(AT) == 8) ? (1 << LOGS) / 2 : (1 << LOGS);
   constexpr uint32_t CAP = (uint32_t)SLOTS / 8 * 7;  // entries per round (load <= 7/8)
-  constexpr int RPT = 10;                             // run entries held in registers (10: no spills for 4-byte values)
+  // run entries held in registers: 10 for 4-byte values; 16-byte entries
+  // (8-byte values) take 6, since 10 spilled (52-68 bytes of scratch a lane)
+  constexpr int RPT = sizeof(BT) == 8 ? 6 : 10;
   constexpr uint32_t LONG = 4 * RPT;                  // longer runs: the strided path
   static_assert(LONG <= 64, "a run's winners fit one 64-bit mask");
   using Ent = RbEnt<sizeof(BT)>;

@@ -3,6 +3,8 @@ assign and accumulate, plus the same keys through the Get alone (the random
 read floor).  Interleaved variants in one process (env knobs per shard).
 
   python tools/zipf_probe.py ["KNOB=V,..."] ...
+  (PROBE_DTYPE=f64: 8-byte values; PROBE_J, PROBE_ROUNDS, PROBE_SPACE,
+  PROBE_WORKLOAD=dense)
 """
 import os
 import statistics
@@ -25,10 +27,12 @@ def main():
     rounds = int(os.environ.get("PROBE_ROUNDS", "5"))
     space, B = int(float(os.environ.get("PROBE_SPACE", "1e8"))), 1_000_000
     dev = torch.device("cuda:0")
+    f64 = os.environ.get("PROBE_DTYPE", "f32") == "f64"  # 8-byte values
+    ndt, tdt = (np.float64, torch.float64) if f64 else (np.float32, torch.float32)
     if os.environ.get("PROBE_WORKLOAD", "zipf") == "dense":
-        zb = workload.dense_batches(J, space, batch=B, device=dev)
+        zb = workload.dense_batches(J, space, batch=B, device=dev, dtype=tdt)
     else:
-        zb = workload.zipf_batches(J, space, batch=B, device=dev)
+        zb = workload.zipf_batches(J, space, batch=B, device=dev, dtype=tdt)
     zo = [torch.empty_like(v) for _, v in zb]
     u_all = int(torch.unique(torch.cat([k for k, _ in zb])).numel())
     print(f"{os.environ.get('PROBE_WORKLOAD', 'zipf')}: {J} x {B} keys, distinct per step {u_all}, per batch {int(torch.unique(zb[0][0]).numel())}")
@@ -38,7 +42,7 @@ def main():
             env = dict(kv.split("=") for kv in v.split(",") if kv)
             old = {k: os.environ.get(k) for k in env}
             os.environ.update(env)
-            sh = ps.Shard(0, space, np.float32, mode=mode)
+            sh = ps.Shard(0, space, ndt, mode=mode)
             for k, o in old.items():
                 os.environ.pop(k) if o is None else os.environ.__setitem__(k, o)
             adds = sh.prepare(zb)
