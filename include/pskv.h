@@ -178,8 +178,11 @@ int pskv_get_grouped(pskv_shard* s, const pskv_batch* batches, uint64_t nb, int 
  * for both; PSKV_SORTED_HINT applies to the Adds): the BSP model's flush of
  * its deferred Adds followed by the Gets that flush releases
  * (server/consistency/bsp_model.cpp:14-31), or one worker round's push then
- * pull.  Identical results to the two calls.  (A single fused launch for the
- * pair was built and measured slower than the two launches) */
+ * pull.  Identical results to the two calls.  Device batches, assign mode,
+ * 4-byte values: the Add's conditional replay (K4r) rides on the Get's first
+ * K1 launch (K1r), one launch fewer than the two calls (option FOLD_REPLAY).
+ * (A single fused launch for the pair was built and measured slower than the
+ * two launches) */
 int pskv_add_get_grouped(pskv_shard* s, const pskv_batch* adds, uint64_t na, const pskv_batch* gets,
                          uint64_t ng, int flags);
 
@@ -210,7 +213,9 @@ int pskv_shard_info(pskv_shard* s, pskv_info* info);
  * DMA_MIN_BYTES_PINNED, ZC_MAX_BYTES, FRAME_ZC_MAX_BYTES, INLINE,
  * INLINE_ADD_CHUNKS, INLINE_GET_CHUNKS, ISPIN, SERVE, SERVE_IDLE_US,
  * TILE_SHIFT, TILE_GRID, RB_WBITS, RB_NBD, RB_TB, RB_APPLY_LOG2, RB_BIN_BLOCK,
- * SYNC_TIMEOUT_MS (the bound of every host wait, pskv_sync).
+ * SYNC_TIMEOUT_MS (the bound of every host wait, pskv_sync), FOLD_REPLAY
+ * (pskv_add_get_grouped: the Add's conditional replay rides on the Get's
+ * first K1 launch, K1r, instead of a K4r launch of its own; 1 = on).
  * Every option changes speed only, never results.  Some apply only together
  * with others (a value is accepted and echoed either way):
  *   EARLY = 1     K2g with UNROLL 8 and NT 1 (otherwise the default loads)

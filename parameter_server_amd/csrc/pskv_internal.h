@@ -56,6 +56,16 @@ struct GroupArgs {
 };
 static_assert(sizeof(GroupArgs) <= 1800, "a group plus the other arguments fit the 4 KiB kernarg segment");
 
+// The batches of an Add group whose conditional replay rides on the next Get's
+// K1 launch (K1r, pskv_add_get_grouped): a second group in the same kernarg
+// segment, without the workgroup prefix the replay does not read.
+struct ReplayGroup {
+  int nb;
+  DevBatch b[kMaxBatches];
+};
+static_assert(sizeof(GroupArgs) + sizeof(ReplayGroup) <= 3500,
+              "K1r's two groups plus its other arguments fit the 4 KiB kernarg segment");
+
 // K8: a whole small message inside the kernel arguments (<= 4 KiB kernarg).
 struct InlineAdd {
   uint32_t n;
@@ -136,6 +146,12 @@ hipError_t launch_ovf_rehash(int vb, const Ovf& from, uint64_t from_cap, const O
 // when *cond == epoch: a sorted-path hint was broken); assign or accumulate.
 hipError_t launch_replay(int dtype, int mode, const GroupArgs& ga, const DenseView& d, const Ovf& o,
                          const uint32_t* cond, uint32_t epoch, hipStream_t st);
+// K1r: K1 with an assign group's conditional replay folded in (the launch K4r
+// would cost): when *cond == epoch, workgroup 0 replays `rg` and then gathers
+// every chunk of `ga` itself while the other workgroups leave; otherwise K1.
+hipError_t launch_gather_replay(int vb, bool vec, int unroll, bool nt, const GroupArgs& ga, uint32_t nwg,
+                                const DenseView& d, const Ovf& o, const ReplayGroup& rg,
+                                const uint32_t* cond, uint32_t epoch, hipStream_t st);
 // K5 key buckets: windows of 2^wbits keys of the owned range, window w in
 // bucket w % nbd (1 <= nbd < 2^12, windows < 2^21: wbits >= 11 or a range
 // below 2^32); magic = ceil(2^32 / nbd); span = keys per bucket at most

@@ -293,10 +293,11 @@ __device__ __forceinline__ void gather2(const DenseView& d, const Ovf& o, const 
   }
 }
 
+// One K1 chunk (CH = 1024 * U keys of one batch): chunk `wg` of the group.
 template <typename VT, bool VEC, int U, bool NT>
-__global__ __launch_bounds__(kBlock) void k_gather(GroupArgs ga, DenseView d, Ovf o) {
+__device__ __forceinline__ void gather_chunk(const GroupArgs& ga, const DenseView& d, const Ovf& o,
+                                             uint32_t wg) {
   constexpr int CH = kBlock * 4 * U;
-  const uint32_t wg = blockIdx.x;
   const int j = batch_of(ga, wg);
   const uint32_t* __restrict__ keys = ga.b[j].keys;
   VT* __restrict__ out = reinterpret_cast<VT*>(const_cast<void*>(ga.b[j].vals));
@@ -361,6 +362,11 @@ __global__ __launch_bounds__(kBlock) void k_gather(GroupArgs ga, DenseView d, Ov
       }
     }
   }
+}
+
+template <typename VT, bool VEC, int U, bool NT>
+__global__ __launch_bounds__(kBlock) void k_gather(GroupArgs ga, DenseView d, Ovf o) {
+  gather_chunk<VT, VEC, U, NT>(ga, d, o, blockIdx.x);
 }
 
 // ----------------------------------------------------- K2 sorted assign
@@ -1945,23 +1951,24 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
 // kernel boundaries per step) — not the speed of a repair that only a broken
 // hint triggers (~1 GB/s: 64 M keys take ~0.3 s).
 constexpr int kReplayBlock = 1024;
-constexpr int kReplayChunk = 4 * kReplayBlock;
-constexpr int kReplaySlots = 2 * kReplayChunk;
 
-template <typename VT, int MODE>
-__device__ __forceinline__ void replay_group(const GroupArgs& ga, const DenseView& d, const Ovf& o) {
-  constexpr int PER = kReplayChunk / kReplayBlock;
-  __shared__ uint32_t hk[kReplaySlots];
-  __shared__ uint32_t hidx[MODE == 0 ? kReplaySlots + 1 : 1];  // assign: 1 + largest local index
-  __shared__ VT hsum[MODE == 1 ? kReplaySlots + 1 : 1];        // accumulate: the pass's sums
+// BLOCK threads (K4r: 1024; K1r: 256), 4 * BLOCK elements per pass; G is
+// GroupArgs or ReplayGroup (only nb and b[] are read).
+template <typename VT, int MODE, int BLOCK = kReplayBlock, typename G = GroupArgs>
+__device__ __forceinline__ void replay_group(const G& ga, const DenseView& d, const Ovf& o) {
+  constexpr int CHUNK = 4 * BLOCK, SLOTS = 2 * CHUNK;
+  constexpr int PER = CHUNK / BLOCK;
+  __shared__ uint32_t hk[SLOTS];
+  __shared__ uint32_t hidx[MODE == 0 ? SLOTS + 1 : 1];  // assign: 1 + largest local index
+  __shared__ VT hsum[MODE == 1 ? SLOTS + 1 : 1];        // accumulate: the pass's sums
   __shared__ uint32_t sent;
   const int tid = threadIdx.x;
   for (int j = 0; j < ga.nb; ++j) {
     const uint32_t* __restrict__ keys = ga.b[j].keys;
     const VT* __restrict__ vals = reinterpret_cast<const VT*>(ga.b[j].vals);
     const uint64_t n = ga.b[j].n;
-    for (uint64_t base = 0; base < n; base += kReplayChunk) {
-      for (int s = tid; s < kReplaySlots; s += kReplayBlock) {
+    for (uint64_t base = 0; base < n; base += CHUNK) {
+      for (int s = tid; s < SLOTS; s += BLOCK) {
         hk[s] = kEmpty32;
         if (MODE == 0)
           hidx[s] = 0u;
@@ -1971,27 +1978,27 @@ __device__ __forceinline__ void replay_group(const GroupArgs& ga, const DenseVie
       if (tid == 0) {
         sent = 0u;
         if (MODE == 0)
-          hidx[kReplaySlots] = 0u;
+          hidx[SLOTS] = 0u;
         else
-          hsum[kReplaySlots] = VT(0);
+          hsum[SLOTS] = VT(0);
       }
       __syncthreads();  // also orders the previous pass's stores before this pass's
       uint32_t key[PER], slot[PER], valid = 0;
       VT v[PER];
 #pragma unroll
       for (int q = 0; q < PER; ++q) {
-        const uint64_t i = base + (uint64_t)(q * kReplayBlock + tid);
+        const uint64_t i = base + (uint64_t)(q * BLOCK + tid);
         const bool in = i < n;
         valid |= in ? (1u << q) : 0u;
         key[q] = in ? keys[i] : 0u;
         v[q] = in ? vals[i] : VT(0);
       }
-      const uint32_t own = lds_insert<PER, kReplaySlots>(hk, &sent, key, valid, slot);
+      const uint32_t own = lds_insert<PER, SLOTS>(hk, &sent, key, valid, slot);
 #pragma unroll
       for (int q = 0; q < PER; ++q) {
         if (!(valid >> q & 1u)) continue;
         if (MODE == 0)
-          atomicMax(&hidx[slot[q]], (uint32_t)(q * kReplayBlock + tid) + 1u);
+          atomicMax(&hidx[slot[q]], (uint32_t)(q * BLOCK + tid) + 1u);
         else
           lds_add(&hsum[slot[q]], v[q]);
       }
@@ -2001,7 +2008,7 @@ __device__ __forceinline__ void replay_group(const GroupArgs& ga, const DenseVie
         if (!(valid >> q & 1u)) continue;
         const uint32_t off = key[q] - d.key_begin;
         if (MODE == 0) {
-          if (hidx[slot[q]] != (uint32_t)(q * kReplayBlock + tid) + 1u) continue;  // a later occurrence wins
+          if (hidx[slot[q]] != (uint32_t)(q * BLOCK + tid) + 1u) continue;  // a later occurrence wins
           if ((uint64_t)off < d.range) {
             reinterpret_cast<VT*>(d.param)[off] = v[q];
           } else {
@@ -2030,6 +2037,29 @@ __global__ __launch_bounds__(kReplayBlock) void k_replay(GroupArgs ga, DenseView
                                                          const uint32_t* cond, uint32_t epoch) {
   if (*cond != epoch) return;  // the hint held (the usual case)
   replay_group<VT, MODE>(ga, d, o);
+}
+
+// K1r: K1 carrying the conditional replay of the assign group just before it
+// (pskv_add_get_grouped: the Add's last launch group, then the Get's first) --
+// the idle K4r launch between K2g and K1 cost ~1 us of a rank's ~40 us step
+// and ~3 us of the headline's 200 (profiles/r04_probes/no_replay/).  Almost
+// always the hint held and every workgroup gathers its chunk as K1 does.  When
+// the Add's verification tagged `cond`, no parameter may be read before the
+// replay has rewritten the group's keys, and workgroups of one launch cannot
+// safely wait for one another, so workgroup 0 does all of it -- the replay
+// (256 threads, 1 Ki elements per pass) and then every chunk of the Get in
+// turn -- while the others leave at once.  Slow (a broken hint already pays a
+// one-workgroup replay), never a wait between workgroups.
+template <typename VT, bool VEC, int U, bool NT>
+__global__ __launch_bounds__(kBlock) void k_gather_r(GroupArgs ga, DenseView d, Ovf o, ReplayGroup rg,
+                                                     const uint32_t* cond, uint32_t epoch) {
+  if (*cond == epoch) {  // uniform
+    if (blockIdx.x != 0) return;
+    replay_group<VT, 0, kBlock>(rg, d, o);  // ends with a barrier: its stores precede the loads below
+    for (uint32_t w = 0; w < gridDim.x; ++w) gather_chunk<VT, VEC, U, NT>(ga, d, o, w);
+    return;
+  }
+  gather_chunk<VT, VEC, U, NT>(ga, d, o, blockIdx.x);
 }
 
 // ------------------------------------------- K6/K7 dense accumulate
@@ -2549,6 +2579,41 @@ hipError_t launch_gather(int vb, bool vec, int unroll, bool nt, const GroupArgs&
       gather_dispatch<unsigned long long, true>(unroll, nt, nwg, ga, d, o, st);
     else
       gather_dispatch<unsigned long long, false>(unroll, nt, nwg, ga, d, o, st);
+  }
+  return hipGetLastError();
+}
+
+template <typename VT, bool VEC>
+static void gather_replay_dispatch(int unroll, bool nt, uint32_t nwg, const GroupArgs& ga, const DenseView& d,
+                                   const Ovf& o, const ReplayGroup& rg, const uint32_t* cond, uint32_t epoch,
+                                   hipStream_t st) {
+  if (unroll == 8) {
+    if (nt)
+      k_gather_r<VT, VEC, 8, true><<<nwg, kBlock, 0, st>>>(ga, d, o, rg, cond, epoch);
+    else
+      k_gather_r<VT, VEC, 8, false><<<nwg, kBlock, 0, st>>>(ga, d, o, rg, cond, epoch);
+  } else {
+    if (nt)
+      k_gather_r<VT, VEC, 4, true><<<nwg, kBlock, 0, st>>>(ga, d, o, rg, cond, epoch);
+    else
+      k_gather_r<VT, VEC, 4, false><<<nwg, kBlock, 0, st>>>(ga, d, o, rg, cond, epoch);
+  }
+}
+
+hipError_t launch_gather_replay(int vb, bool vec, int unroll, bool nt, const GroupArgs& ga, uint32_t nwg,
+                                const DenseView& d, const Ovf& o, const ReplayGroup& rg,
+                                const uint32_t* cond, uint32_t epoch, hipStream_t st) {
+  if (nwg == 0) return hipErrorInvalidValue;  // the replay must run: the caller launches K4r instead
+  if (vb == 4) {
+    if (vec)
+      gather_replay_dispatch<uint32_t, true>(unroll, nt, nwg, ga, d, o, rg, cond, epoch, st);
+    else
+      gather_replay_dispatch<uint32_t, false>(unroll, nt, nwg, ga, d, o, rg, cond, epoch, st);
+  } else {
+    if (vec)
+      gather_replay_dispatch<unsigned long long, true>(unroll, nt, nwg, ga, d, o, rg, cond, epoch, st);
+    else
+      gather_replay_dispatch<unsigned long long, false>(unroll, nt, nwg, ga, d, o, rg, cond, epoch, st);
   }
   return hipGetLastError();
 }

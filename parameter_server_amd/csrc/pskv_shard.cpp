@@ -338,6 +338,15 @@ struct pskv_shard {
   uint64_t launches = 0;          // kernels this shard queued
   hipEvent_t sync_ev = nullptr;   // marks the end of a stream for a bounded wait
   uint32_t* stat_host = nullptr;  // page-locked read-back of the overflow table's {count, err}
+  // pskv_add_get_grouped (round 5): the Add's last conditional replay (K4r)
+  // held back and folded into the Get's first K1 launch (K1r) instead of a
+  // launch of its own; option FOLD_REPLAY
+  int tune_fold_replay = 1;
+  bool defer_replay = false;  // inside add_get: replay() holds the group instead of launching
+  bool pend_replay = false;   // a held replay: pend_rg, pend_epoch, pend_elems
+  ReplayGroup pend_rg{};
+  uint32_t pend_epoch = 0;
+  uint64_t pend_elems = 0;
 
   DenseView dview() const { return DenseView{dense, key_begin, range}; }
 };
@@ -947,14 +956,40 @@ int general_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_
   return PSKV_OK;
 }
 
+// A held replay (see replay) launched as K4r, its own launch.
+int flush_replay(pskv_shard* s) {
+  if (!s->pend_replay) return PSKV_OK;
+  s->pend_replay = false;
+  GroupArgs ga;
+  ga.nb = s->pend_rg.nb;
+  for (int i = 0; i < ga.nb; ++i) ga.b[i] = s->pend_rg.b[i];
+  LaunchTimer t(s, PSKV_K_REPLAY, s->pend_elems);
+  PSKV_HIP(launch_replay(s->dtype, s->mode, ga, s->dview(), s->ovf, s->flag, s->pend_epoch, s->stream));
+  t.done();
+  s->n_general++;
+  return PSKV_OK;
+}
+
 // The safety net behind a verifying sorted-path launch group: K4r replays the
 // group in call order iff the verification tagged s->flag with `epoch` (one
 // single-workgroup launch that exits at once otherwise).
+// Inside pskv_add_get_grouped (s->defer_replay) the replay of an assign group
+// with 4-byte values is held instead (pend_*): the Get's first K1 launch takes
+// it (K1r), or flush_replay launches it as K4r before anything else is queued.
 int replay(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_t e, uint32_t epoch) {
   GroupArgs ga;
   (void)build_group(v, b, e, kGeneralChunk, &ga);
   uint64_t elems = 0;
   for (size_t i = b; i < e; ++i) elems += v[i].n;
+  if (s->defer_replay && s->mode == PSKV_ASSIGN && s->vb == 4) {
+    if (int rc = flush_replay(s)) return rc;  // (add_impl flushed it already: the order holds either way)
+    s->pend_rg.nb = ga.nb;
+    for (int i = 0; i < ga.nb; ++i) s->pend_rg.b[i] = ga.b[i];
+    s->pend_epoch = epoch;
+    s->pend_elems = elems;
+    s->pend_replay = true;
+    return PSKV_OK;
+  }
   LaunchTimer t(s, PSKV_K_REPLAY, elems);
   PSKV_HIP(launch_replay(s->dtype, s->mode, ga, s->dview(), s->ovf, s->flag, epoch, s->stream));
   t.done();
@@ -1559,6 +1594,8 @@ int add_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
     bool vec = true;
     for (auto& b : v) vec &= aligned16(b.keys) & aligned16(b.vals);
     for (auto& g : split_groups(v)) {
+      // a replay held by the previous group goes before this group's launches
+      if ((rc = flush_replay(s))) return rc;
       const uint32_t epoch = next_epoch(s);
       if (s->mode == PSKV_ACCUMULATE) {
         if (!device && host_dense) {
@@ -1812,8 +1849,15 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
     const int gu = gather_unroll(s, elems);
     const uint32_t nwg = build_group(dv, g.first, g.second, stream_chunk(gu), &ga);
     LaunchTimer t(s, PSKV_K_GATHER, elems);
-    PSKV_HIP(launch_gather(s->vb, vec, gu, s->tune_nt, ga, nwg, s->dview(), s->ovf,
-                           s->stream));
+    if (s->pend_replay && nwg > 0) {
+      // the Add's held replay rides on this first K1 (pskv_add_get_grouped)
+      s->pend_replay = false;
+      PSKV_HIP(launch_gather_replay(s->vb, vec, gu, s->tune_nt, ga, nwg, s->dview(), s->ovf, s->pend_rg,
+                                    s->flag, s->pend_epoch, s->stream));
+    } else {
+      PSKV_HIP(launch_gather(s->vb, vec, gu, s->tune_nt, ga, nwg, s->dview(), s->ovf,
+                             s->stream));
+    }
     t.done();
   }
   if (!device) {
@@ -1878,9 +1922,17 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
 // kernel was removed; the call stays, as the two paths.
 int add_get_impl(pskv_shard* s, const std::vector<pskv_batch>& adds, const std::vector<pskv_batch>& gets,
                  int flags) {
+  // Device batches, assign, 4-byte values: the Add's last conditional replay
+  // is held and rides on the Get's first K1 launch (K1r) -- one launch fewer
+  // per call.  The Get's device path queues nothing before that K1; whatever
+  // is still held after it (an empty Get, a failure) is launched as K4r here,
+  // with nothing queued in between, so stream order is the sequential one.
+  s->defer_replay = s->tune_fold_replay && (flags & PSKV_DEVICE) && s->mode == PSKV_ASSIGN && s->vb == 4;
   int rc = add_impl(s, adds, flags);
-  if (rc) return rc;
-  return get_impl(s, gets, flags & ~PSKV_SORTED_HINT);
+  s->defer_replay = false;
+  if (!rc) rc = get_impl(s, gets, flags & ~PSKV_SORTED_HINT);
+  const int rf = flush_replay(s);
+  return rc ? rc : rf;
 }
 
 // ------------------------------------------------------------- options
@@ -1907,6 +1959,7 @@ const Option kOptions[] = {
     PSKV_OPT("GENERAL", 0, 2, general_path, int),
     PSKV_OPT("UNROLL", 4, 8, tune_unroll, int),              // 4 or 8 (others: 8)
     PSKV_OPT("GET_UNROLL", 0, 8, tune_get_unroll, int),      // 0 (by size), 4 or 8
+    PSKV_OPT("FOLD_REPLAY", 0, 1, tune_fold_replay, int),   // add_get: K4r folded into K1 (K1r)
     PSKV_OPT("NT", 0, 1, tune_nt, bool),
     PSKV_OPT("NTP", 0, 1, tune_ntp, bool),
     PSKV_OPT("EARLY", 0, 2, tune_early, int),

@@ -8,7 +8,9 @@ windows at every key phase (keys several windows cover: the LAST one wins),
 scattered pulls (overflow keys, never-written keys, the sentinel, partial
 chunks), sorted push groups that are not windows (K2g's tile mode), wrong
 sorted hints and window look-alikes (the replay), more than 64 batches on
-either side.  (These shapes were written for round 4's fused launch, K10,
+either side, with the Add's conditional replay folded into the Get's first
+K1 launch (K1r, round 5; FOLD_REPLAY=1, the default) and as its own launch
+(K4r, FOLD_REPLAY=0).  (These shapes were written for round 4's fused launch, K10,
 which answered covered pull keys from the pushed values; it measured slower
 than the two launches and was removed — the cases stay as the call's tests.)"""
 import numpy as np
@@ -27,7 +29,12 @@ def _dev(a, cuda):
     return torch.from_numpy(np.ascontiguousarray(a).view(np.int32 if a.dtype == np.uint32 else a.dtype)).to(cuda)
 
 
-def _run(cuda, oracle_mod, pre, pushes, pulls, hint=True):
+@pytest.fixture(params=[1, 0], ids=["fold", "k4r"])
+def fold(request):
+    return request.param
+
+
+def _run(cuda, oracle_mod, pre, pushes, pulls, hint=True, fold=1):
     """Apply `pre` (setup Adds, separate calls), then one add_get_grouped of
     `pushes` / `pulls` on a fresh float32 shard; return the pulled values and
     the oracle's."""
@@ -36,7 +43,7 @@ def _run(cuda, oracle_mod, pre, pushes, pulls, hint=True):
     import parameter_server_amd as ps
 
     ref = oracle_mod.MapStorageRef(np.float32)
-    with ps.Shard(KB, KE, np.float32, overflow_slots=1 << 16) as sh:
+    with ps.Shard(KB, KE, np.float32, overflow_slots=1 << 16, options={"FOLD_REPLAY": fold}) as sh:
         for k, v in pre:
             sh.add(k, v)
             ref.add(k, v)
@@ -67,14 +74,14 @@ def _vals(rng, n):
     return (rng.standard_normal(n) * 10).astype(np.float32)
 
 
-def _check(cuda, oracle_mod, pre, pushes, pulls, hint=True):
-    got, want, after, after_ref = _run(cuda, oracle_mod, pre, pushes, pulls, hint)
+def _check(cuda, oracle_mod, pre, pushes, pulls, hint=True, fold=1):
+    got, want, after, after_ref = _run(cuda, oracle_mod, pre, pushes, pulls, hint, fold)
     for j, (g, w) in enumerate(zip(got, want)):
         assert_bits_equal(g, w, f"pull batch {j}")
     assert_bits_equal(after, after_ref, "shard after the call")
 
 
-def test_add_get_disjoint_pulls(cuda, oracle_mod):
+def test_add_get_disjoint_pulls(cuda, oracle_mod, fold):
     """The benchmarked shape: window pushes, pulls of windows no push touches."""
     rng = np.random.default_rng(1)
     pre = [(np.arange(KB, KE, dtype=np.uint32), _vals(rng, KE - KB))]
@@ -86,7 +93,7 @@ def test_add_get_disjoint_pulls(cuda, oracle_mod):
         q = np.arange(b, b + 40_000, dtype=np.uint32)
         if not np.isin(q, pushed).any():
             pulls.append(q)
-    _check(cuda, oracle_mod, pre, pushes, pulls)
+    _check(cuda, oracle_mod, pre, pushes, pulls, fold=fold)
 
 
 @pytest.mark.parametrize("phase", [0, 1, 3])
@@ -126,7 +133,7 @@ def test_add_get_scattered_pulls_overflow_sentinel(cuda, oracle_mod):
     _check(cuda, oracle_mod, pre, pushes, pulls)
 
 
-def test_add_get_tile_mode_grid_barrier(cuda, oracle_mod):
+def test_add_get_tile_mode_grid_barrier(cuda, oracle_mod, fold):
     """A push group of sorted batches that are not windows (duplicates, gaps):
     the Add runs K2g's tile mode; the Get must see every tile's writes."""
     rng = np.random.default_rng(7)
@@ -137,10 +144,10 @@ def test_add_get_tile_mode_grid_barrier(cuda, oracle_mod):
         pushes.append((k, _vals(rng, n)))
     keys = np.concatenate([k for k, _ in pushes])
     pulls = [np.sort(keys[::3]), keys[::5].copy(), np.arange(KB, KB + 100_000, dtype=np.uint32)]
-    _check(cuda, oracle_mod, pre, pushes, pulls)
+    _check(cuda, oracle_mod, pre, pushes, pulls, fold=fold)
 
 
-def test_add_get_wrong_hint_and_lookalike_repaired(cuda, oracle_mod):
+def test_add_get_wrong_hint_and_lookalike_repaired(cuda, oracle_mod, fold):
     """A wrong sorted hint (an unsorted batch) and a window look-alike (spans
     n - 1 keys but repeats one): K2g tags the group, K4r replays it before the
     Get runs — the pulls of the pushed keys see the sequential last-write-wins
@@ -154,10 +161,10 @@ def test_add_get_wrong_hint_and_lookalike_repaired(cuda, oracle_mod):
     pushes = [(w, _vals(rng, w.size)), (look, _vals(rng, look.size)), (bad, _vals(rng, bad.size)),
               (w[5000:9000].copy(), _vals(rng, 4000))]
     pulls = [np.arange(KB, KB + 400_000, dtype=np.uint32), look.copy(), bad[::3].copy()]
-    _check(cuda, oracle_mod, pre, pushes, pulls)
+    _check(cuda, oracle_mod, pre, pushes, pulls, fold=fold)
 
 
-def test_add_get_many_batches_and_empty(cuda, oracle_mod):
+def test_add_get_many_batches_and_empty(cuda, oracle_mod, fold):
     """70 push windows and 70 pull batches (two launch groups each side), some
     empty, in order."""
     rng = np.random.default_rng(13)
@@ -166,7 +173,7 @@ def test_add_get_many_batches_and_empty(cuda, oracle_mod):
     pulls = [np.arange(b, b + 5_000, dtype=np.uint32) for b in rng.integers(KB, KE - 5_000, size=70)]
     pulls[10] = np.zeros(0, np.uint32)
     pulls[69] = np.concatenate([k for k, _ in pushes[60:]])  # the last Add group's own keys
-    _check(cuda, oracle_mod, [], pushes, pulls)
+    _check(cuda, oracle_mod, [], pushes, pulls, fold=fold)
 
 
 def test_add_get_host_batches_and_unhinted(cuda, oracle_mod):
@@ -187,3 +194,41 @@ def test_add_get_host_batches_and_unhinted(cuda, oracle_mod):
         for k, v in pushes:
             ref.add(k, v)
     assert_bits_equal(outs[0], ref.get(pulls[0]), "host batches")
+
+
+def test_add_get_replay_rides_on_the_get(cuda, oracle_mod):
+    """FOLD_REPLAY (round 5): a hinted add_get launches no K4r of its own -- the
+    Add's conditional replay is K1r's (one launch fewer per call) -- and with
+    the option off it does; an Add in two launch groups launches the first
+    group's replay as K4r in either case, before the second group's K2g.  The
+    results are the oracle's either way (a broken hint in the LAST group
+    exercises the folded replay, workgroup 0 replaying then gathering every
+    chunk)."""
+    import torch
+
+    import parameter_server_amd as ps
+    from parameter_server_amd import _lib
+
+    rng = np.random.default_rng(31)
+    for fold, groups in ((1, 1), (0, 1), (1, 2), (0, 2)):
+        pushes = [(k, _vals(rng, k.size)) for k in _windows(rng, 64 * groups, 4_000, phase_max=1)]
+        bad = rng.permutation(np.arange(KB + 500_000, KB + 520_000, dtype=np.uint32))
+        pushes[-1] = (bad, _vals(rng, bad.size))  # the last group's hint is broken
+        pulls = [np.arange(KB + 490_000, KB + 530_000, dtype=np.uint32), np.concatenate([k for k, _ in pushes[:5]])]
+        ref = oracle_mod.MapStorageRef(np.float32)
+        with ps.Shard(KB, KE, np.float32, options={"FOLD_REPLAY": fold}) as sh:
+            adds = [(_dev(k, cuda), _dev(v, cuda)) for k, v in pushes]
+            outs = [torch.empty(q.size, dtype=torch.float32, device=cuda) for q in pulls]
+            sh.set_timing(True, [_lib.PSKV_K_REPLAY, _lib.PSKV_K_GATHER])
+            sh.add_get_grouped(adds, [(_dev(q, cuda), o) for q, o in zip(pulls, outs)], sorted_hint=True)
+            torch.cuda.synchronize()
+            reps = sh.kernel_time(_lib.PSKV_K_REPLAY)["launches"]
+            gathers = sh.kernel_time(_lib.PSKV_K_GATHER)["launches"]
+            sh.set_timing(False)
+            got = [o.cpu().numpy() for o in outs]
+        for k, v in pushes:
+            ref.add(k, v)
+        for j, (g, q) in enumerate(zip(got, pulls)):
+            assert_bits_equal(g, ref.get(q), f"fold {fold}, {groups} group(s), pull {j}")
+        assert gathers == 1
+        assert reps == (groups - 1 if fold else groups), (fold, groups, reps)

@@ -36,7 +36,7 @@ N_GROUPS = int(os.environ.get("FUZZ_GROUPS", "4"))  # concurrent groups of 6 sha
 KNOBS = [{}, {}, {}, {"SERVE": 1}, {"GENERAL": "stamps"}, {"INLINE": 0},
          {"UNROLL": 4}, {"PAGEABLE_DMA": 1}, {"ZC_MAX_BYTES": 0},
          {"RB_APPLY_LOG2": 13}, {"RB_BIN_BLOCK": 512}, {"GET_UNROLL": 8}, {"GET_UNROLL": 4}, {"EARLY": 1}, {"EARLY": 0}, {"NTP": 0},
-         {"TILE_GRID": 1024}, {"NT": 0}]
+         {"TILE_GRID": 1024}, {"NT": 0}, {"FOLD_REPLAY": 0}]
 SIZES = [0, 1, 5, 100, 256, 257, 1024, 2049, 5000, 40_000, 300_000]
 U32 = 1 << 32
 

@@ -1521,7 +1521,7 @@ def test_shard_options_api(cuda, monkeypatch, capfd):
     names = ["GENERAL", "UNROLL", "GET_UNROLL", "NT", "NTP", "EARLY", "PAGEABLE_DMA", "DMA_MIN_BYTES", "DMA_MIN_BYTES_GET",
              "DMA_MIN_BYTES_PINNED", "ZC_MAX_BYTES", "FRAME_ZC_MAX_BYTES", "INLINE", "INLINE_ADD_CHUNKS",
              "INLINE_GET_CHUNKS", "ISPIN", "SERVE", "SERVE_IDLE_US", "TILE_SHIFT", "TILE_GRID", "RB_WBITS",
-             "RB_NBD", "RB_TB", "RB_APPLY_LOG2", "RB_BIN_BLOCK", "SYNC_TIMEOUT_MS"]
+             "RB_NBD", "RB_TB", "RB_APPLY_LOG2", "RB_BIN_BLOCK", "SYNC_TIMEOUT_MS", "FOLD_REPLAY"]
     with ps.Shard(0, 1000, np.float32) as sh:
         for n in names:
             sh.set_option(n, sh.get_option(n))  # every default is a valid value
@@ -1532,7 +1532,7 @@ def test_shard_options_api(cuda, monkeypatch, capfd):
         sh.set_option("ZC_MAX_BYTES", 12345)
         assert sh.get_option("ZC_MAX_BYTES") == 12345
         for n, bad in (("UNROLL", 5), ("GET_UNROLL", 6), ("RB_APPLY_LOG2", 12), ("TILE_SHIFT", 3), ("INLINE", 2),
-                        ("RB_BIN_BLOCK", 768), ("NOPE", 1), ("GET_DEDUP", 1), ("RB_INSERT", 1), ("GET_NTP", 1), ("FUSE", 1)):
+                        ("RB_BIN_BLOCK", 768), ("FOLD_REPLAY", 2), ("NOPE", 1), ("GET_DEDUP", 1), ("RB_INSERT", 1), ("GET_NTP", 1), ("FUSE", 1)):
             before = sh.get_option(n) if n in names else None
             with pytest.raises(PskvError) as ei:
                 sh.set_option(n, bad)
