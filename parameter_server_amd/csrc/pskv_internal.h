@@ -149,9 +149,11 @@ hipError_t launch_replay(int dtype, int mode, const GroupArgs& ga, const DenseVi
 // K1r: K1 with an assign group's conditional replay folded in (the launch K4r
 // would cost): when *cond == epoch, workgroup 0 replays `rg` and then gathers
 // every chunk of `ga` itself while the other workgroups leave; otherwise K1.
+// tab: kK1rTableWords words of device scratch (the replay's table, K1r has no LDS).
+constexpr uint32_t kK1rTableWords = 4100;
 hipError_t launch_gather_replay(int vb, bool vec, int unroll, bool nt, const GroupArgs& ga, uint32_t nwg,
                                 const DenseView& d, const Ovf& o, const ReplayGroup& rg,
-                                const uint32_t* cond, uint32_t epoch, hipStream_t st);
+                                const uint32_t* cond, uint32_t epoch, uint32_t* tab, hipStream_t st);
 // K5 key buckets: windows of 2^wbits keys of the owned range, window w in
 // bucket w % nbd (1 <= nbd < 2^12, windows < 2^21: wbits >= 11 or a range
 // below 2^32); magic = ceil(2^32 / nbd); span = keys per bucket at most

@@ -294,9 +294,15 @@ __device__ __forceinline__ void gather2(const DenseView& d, const Ovf& o, const 
 }
 
 // One K1 chunk (CH = 1024 * U keys of one batch): chunk `wg` of the group.
-template <typename VT, bool VEC, int U, bool NT>
+// go() is asked once, after the chunk's key loads are issued and before any
+// parameter is read: false abandons the chunk (K1r's tag check, whose scalar
+// load then waits behind the key loads instead of in front of them).
+struct GoAlways {
+  __device__ bool operator()() const { return true; }
+};
+template <typename VT, bool VEC, int U, bool NT, typename Go = GoAlways>
 __device__ __forceinline__ void gather_chunk(const GroupArgs& ga, const DenseView& d, const Ovf& o,
-                                             uint32_t wg) {
+                                             uint32_t wg, Go go = Go()) {
   constexpr int CH = kBlock * 4 * U;
   const int j = batch_of(ga, wg);
   const uint32_t* __restrict__ keys = ga.b[j].keys;
@@ -314,6 +320,7 @@ __device__ __forceinline__ void gather_chunk(const GroupArgs& ga, const DenseVie
       uint32_t k[UU][2];
 #pragma unroll
       for (int u = 0; u < UU; ++u) ld8_keys<NT>(keys + base + (uint64_t)(u * kBlock + tid) * 2, k[u]);
+      if (!go()) return;
       VT v[UU][2];
 #pragma unroll
       for (int u = 0; u < UU; ++u) gather2(d, o, k[u], v[u]);
@@ -328,6 +335,7 @@ __device__ __forceinline__ void gather_chunk(const GroupArgs& ga, const DenseVie
 #pragma unroll
     for (int u = 0; u < U; ++u)
       Vec4<uint32_t>::load<NT>(keys + base + (uint64_t)(u * kBlock + tid) * 4, k[u]);
+    if (!go()) return;
 #ifdef PSKV_STEP_STAMPS
     ready(k[0]);
     STEP_STAMP(1, 1);
@@ -344,6 +352,7 @@ __device__ __forceinline__ void gather_chunk(const GroupArgs& ga, const DenseVie
     // then their gathers, then the stores — one dependent round trip per
     // eight elements instead of per element (it matters when the keys sit in
     // host memory: the zero-copy Get runs K1 over pinned staging)
+    if (!go()) return;
     const uint64_t end = n < base + CH ? n : base + CH;
     for (uint64_t i0 = base + tid; i0 < end; i0 += 8ull * kBlock) {
       uint32_t kk[8];
@@ -1953,15 +1962,22 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
 constexpr int kReplayBlock = 1024;
 
 // BLOCK threads (K4r: 1024; K1r: 256), 4 * BLOCK elements per pass; G is
-// GroupArgs or ReplayGroup (only nb and b[] are read).
+// GroupArgs or ReplayGroup (only nb and b[] are read).  The pass's table --
+// hk[SLOTS], assign: hidx[SLOTS + 1] (1 + largest local index), accumulate:
+// hsum[SLOTS + 1] (the pass's sums), the sentinel's word -- is K4r's LDS, or
+// for K1r a small global scratch (its atomics resolve in this XCD's L2; the
+// barriers order them within the workgroup), so that K1r, which almost never
+// replays, allocates no LDS.
+template <int BLOCK>
+constexpr int replay_slots() {
+  return 8 * BLOCK;
+}
 template <typename VT, int MODE, int BLOCK = kReplayBlock, typename G = GroupArgs>
-__device__ __forceinline__ void replay_group(const G& ga, const DenseView& d, const Ovf& o) {
-  constexpr int CHUNK = 4 * BLOCK, SLOTS = 2 * CHUNK;
+__device__ __forceinline__ void replay_group(const G& ga, const DenseView& d, const Ovf& o, uint32_t* hk,
+                                             uint32_t* hidx, VT* hsum, uint32_t* sent_p) {
+  constexpr int CHUNK = 4 * BLOCK, SLOTS = replay_slots<BLOCK>();
   constexpr int PER = CHUNK / BLOCK;
-  __shared__ uint32_t hk[SLOTS];
-  __shared__ uint32_t hidx[MODE == 0 ? SLOTS + 1 : 1];  // assign: 1 + largest local index
-  __shared__ VT hsum[MODE == 1 ? SLOTS + 1 : 1];        // accumulate: the pass's sums
-  __shared__ uint32_t sent;
+  uint32_t& sent = *sent_p;
   const int tid = threadIdx.x;
   for (int j = 0; j < ga.nb; ++j) {
     const uint32_t* __restrict__ keys = ga.b[j].keys;
@@ -2008,7 +2024,12 @@ __device__ __forceinline__ void replay_group(const G& ga, const DenseView& d, co
         if (!(valid >> q & 1u)) continue;
         const uint32_t off = key[q] - d.key_begin;
         if (MODE == 0) {
-          if (hidx[slot[q]] != (uint32_t)(q * BLOCK + tid) + 1u) continue;  // a later occurrence wins
+          // (an atomic load: in K1r's global table the maxima were resolved in L2,
+          // and a plain load could hit a line this CU's L1 holds from an
+          // earlier pass)
+          if (__hip_atomic_load(&hidx[slot[q]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+              (uint32_t)(q * BLOCK + tid) + 1u)
+            continue;  // a later occurrence wins
           if ((uint64_t)off < d.range) {
             reinterpret_cast<VT*>(d.param)[off] = v[q];
           } else {
@@ -2035,8 +2056,13 @@ __device__ __forceinline__ void replay_group(const G& ga, const DenseView& d, co
 template <typename VT, int MODE>
 __global__ __launch_bounds__(kReplayBlock) void k_replay(GroupArgs ga, DenseView d, Ovf o,
                                                          const uint32_t* cond, uint32_t epoch) {
+  constexpr int SLOTS = replay_slots<kReplayBlock>();
+  __shared__ uint32_t hk[SLOTS];
+  __shared__ uint32_t hidx[MODE == 0 ? SLOTS + 1 : 1];
+  __shared__ VT hsum[MODE == 1 ? SLOTS + 1 : 1];
+  __shared__ uint32_t sent;
   if (*cond != epoch) return;  // the hint held (the usual case)
-  replay_group<VT, MODE>(ga, d, o);
+  replay_group<VT, MODE>(ga, d, o, hk, hidx, hsum, &sent);
 }
 
 // K1r: K1 carrying the conditional replay of the assign group just before it
@@ -2052,14 +2078,21 @@ __global__ __launch_bounds__(kReplayBlock) void k_replay(GroupArgs ga, DenseView
 // one-workgroup replay), never a wait between workgroups.
 template <typename VT, bool VEC, int U, bool NT>
 __global__ __launch_bounds__(kBlock) void k_gather_r(GroupArgs ga, DenseView d, Ovf o, ReplayGroup rg,
-                                                     const uint32_t* cond, uint32_t epoch) {
-  if (*cond == epoch) {  // uniform
-    if (blockIdx.x != 0) return;
-    replay_group<VT, 0, kBlock>(rg, d, o);  // ends with a barrier: its stores precede the loads below
+                                                     const uint32_t* cond, uint32_t epoch, uint32_t* tab) {
+  const uint32_t tag = *cond;  // waited for after this chunk's key loads are issued
+  bool tagged = false;
+  gather_chunk<VT, VEC, U, NT>(ga, d, o, blockIdx.x, [&]() {
+    tagged = tag == epoch;  // uniform
+    return !tagged;
+  });
+  if (tagged && blockIdx.x == 0) {
+    // the table in global scratch (kK1rTableWords words): hk, hidx, the sentinel word
+    constexpr int SLOTS = replay_slots<kBlock>();
+    static_assert(2 * SLOTS + 2 <= (int)kK1rTableWords, "K1r's replay table fits its scratch");
+    replay_group<VT, 0, kBlock>(rg, d, o, tab, tab + SLOTS, static_cast<VT*>(nullptr), tab + 2 * SLOTS + 1);
+    // (ends with a barrier: its stores precede the loads below)
     for (uint32_t w = 0; w < gridDim.x; ++w) gather_chunk<VT, VEC, U, NT>(ga, d, o, w);
-    return;
   }
-  gather_chunk<VT, VEC, U, NT>(ga, d, o, blockIdx.x);
 }
 
 // ------------------------------------------- K6/K7 dense accumulate
@@ -2586,34 +2619,34 @@ hipError_t launch_gather(int vb, bool vec, int unroll, bool nt, const GroupArgs&
 template <typename VT, bool VEC>
 static void gather_replay_dispatch(int unroll, bool nt, uint32_t nwg, const GroupArgs& ga, const DenseView& d,
                                    const Ovf& o, const ReplayGroup& rg, const uint32_t* cond, uint32_t epoch,
-                                   hipStream_t st) {
+                                   uint32_t* tab, hipStream_t st) {
   if (unroll == 8) {
     if (nt)
-      k_gather_r<VT, VEC, 8, true><<<nwg, kBlock, 0, st>>>(ga, d, o, rg, cond, epoch);
+      k_gather_r<VT, VEC, 8, true><<<nwg, kBlock, 0, st>>>(ga, d, o, rg, cond, epoch, tab);
     else
-      k_gather_r<VT, VEC, 8, false><<<nwg, kBlock, 0, st>>>(ga, d, o, rg, cond, epoch);
+      k_gather_r<VT, VEC, 8, false><<<nwg, kBlock, 0, st>>>(ga, d, o, rg, cond, epoch, tab);
   } else {
     if (nt)
-      k_gather_r<VT, VEC, 4, true><<<nwg, kBlock, 0, st>>>(ga, d, o, rg, cond, epoch);
+      k_gather_r<VT, VEC, 4, true><<<nwg, kBlock, 0, st>>>(ga, d, o, rg, cond, epoch, tab);
     else
-      k_gather_r<VT, VEC, 4, false><<<nwg, kBlock, 0, st>>>(ga, d, o, rg, cond, epoch);
+      k_gather_r<VT, VEC, 4, false><<<nwg, kBlock, 0, st>>>(ga, d, o, rg, cond, epoch, tab);
   }
 }
 
 hipError_t launch_gather_replay(int vb, bool vec, int unroll, bool nt, const GroupArgs& ga, uint32_t nwg,
                                 const DenseView& d, const Ovf& o, const ReplayGroup& rg,
-                                const uint32_t* cond, uint32_t epoch, hipStream_t st) {
+                                const uint32_t* cond, uint32_t epoch, uint32_t* tab, hipStream_t st) {
   if (nwg == 0) return hipErrorInvalidValue;  // the replay must run: the caller launches K4r instead
   if (vb == 4) {
     if (vec)
-      gather_replay_dispatch<uint32_t, true>(unroll, nt, nwg, ga, d, o, rg, cond, epoch, st);
+      gather_replay_dispatch<uint32_t, true>(unroll, nt, nwg, ga, d, o, rg, cond, epoch, tab, st);
     else
-      gather_replay_dispatch<uint32_t, false>(unroll, nt, nwg, ga, d, o, rg, cond, epoch, st);
+      gather_replay_dispatch<uint32_t, false>(unroll, nt, nwg, ga, d, o, rg, cond, epoch, tab, st);
   } else {
     if (vec)
-      gather_replay_dispatch<unsigned long long, true>(unroll, nt, nwg, ga, d, o, rg, cond, epoch, st);
+      gather_replay_dispatch<unsigned long long, true>(unroll, nt, nwg, ga, d, o, rg, cond, epoch, tab, st);
     else
-      gather_replay_dispatch<unsigned long long, false>(unroll, nt, nwg, ga, d, o, rg, cond, epoch, st);
+      gather_replay_dispatch<unsigned long long, false>(unroll, nt, nwg, ga, d, o, rg, cond, epoch, tab, st);
   }
   return hipGetLastError();
 }

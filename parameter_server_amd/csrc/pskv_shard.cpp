@@ -1853,7 +1853,7 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
       // the Add's held replay rides on this first K1 (pskv_add_get_grouped)
       s->pend_replay = false;
       PSKV_HIP(launch_gather_replay(s->vb, vec, gu, s->tune_nt, ga, nwg, s->dview(), s->ovf, s->pend_rg,
-                                    s->flag, s->pend_epoch, s->stream));
+                                    s->flag, s->pend_epoch, s->flag + 16, s->stream));
     } else {
       PSKV_HIP(launch_gather(s->vb, vec, gu, s->tune_nt, ga, nwg, s->dview(), s->ovf,
                              s->stream));
@@ -2131,7 +2131,9 @@ int pskv_shard_create_ex(int device, uint32_t key_begin, uint64_t key_end, int d
   if (hipMemsetAsync(s->dense, 0, s->range * (size_t)vb, s->stream) != hipSuccess)
     return bail(fail(PSKV_EHIP, "hipMemsetAsync failed"));
   // flag[0]: the sorted path's verification tag
-  if (hipMalloc(&s->flag, 16) != hipSuccess) return bail(fail(PSKV_ENOMEM, "flag allocation failed"));
+  // the verification tag (16 bytes), then K1r's replay table (add_get's folded replay)
+  if (hipMalloc(&s->flag, 64 + kK1rTableWords * sizeof(uint32_t)) != hipSuccess)
+    return bail(fail(PSKV_ENOMEM, "flag allocation failed"));
   if (hipMemsetAsync(s->flag, 0, 16, s->stream) != hipSuccess)
     return bail(fail(PSKV_EHIP, "hipMemsetAsync failed"));
   s->ocap = next_pow2(std::max<uint64_t>(overflow_slots ? overflow_slots : kDefaultOverflowSlots, 64));
