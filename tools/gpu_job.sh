@@ -39,6 +39,7 @@
 #   ranks48      bench.py as 4 and as 8 ranks on one GPU (gloo, shared device; --sets 4): the N = 4 / 8 code path
 #   zsweep       tools/zipf_probe.py: K5 bucket bits / resolve table / windows / K5a block at the head, 10 rounds
 #   foldab       FOLD_REPLAY 1 / 0 interleaved, 3 rounds: the headline (--no-cold) and rank 0 of N = 8 emulated
+#   foldcold     FOLD_REPLAY 1 / 0 interleaved, 3 rounds, on the cold form (bench.py --cold-only)
 #   wsweep       tools/zipf_probe.py: K5 bucket window bits 11-14 on Zipf keys at 1e8 / 1.25e8 / 5e8 keys and on dense unhinted windows
 #   k5tests      the K5 (unhinted Add) parity tests: Zipf, radix, random, accumulate, sentinel, ragged, full-size cfg 3
 #   abk1         bench A/B of ab/libpskv_{base,k1occ6,k1occ4}.so (K1 held to 8 / 6 / 4 workgroups per CU), headline and rank 0 of 8
@@ -92,6 +93,10 @@ for step in "$@"; do
     tests_all) timeout -k 10 900 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread "$R/tests" -m gpu \
         > "$OUT/tests_all.log" 2>&1 ;;
     align) timeout -k 10 200 python3 "$R/tools/align_probe.py" 0,1,2,3 20 > "$OUT/align.log" 2>&1 ;;
+    foldcold) mkdir -p "$OUT/foldcold" && for i in 1 2 3; do for f in 1 0; do
+          PSKV_FOLD_REPLAY=$f timeout -k 10 200 python3 "$R/bench.py" --steps 50 --cold-only \
+            > "$OUT/foldcold/c_f${f}_$i.json" 2> "$OUT/foldcold/c_f${f}_$i.err" || exit 1
+        done; done ;;
     foldab) mkdir -p "$OUT/foldab" && for i in 1 2 3; do for f in 1 0; do
           PSKV_FOLD_REPLAY=$f timeout -k 10 200 python3 "$R/bench.py" --steps 100 --no-zipf --no-cpu-baseline \
             --no-extra --no-cold > "$OUT/foldab/h_f${f}_$i.json" 2> "$OUT/foldab/h_f${f}_$i.err" || exit 1
