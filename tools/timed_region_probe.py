@@ -57,6 +57,22 @@ def main():
             form.step(i)
         host = (time.perf_counter() - t0) / 20 * 1e6
         torch.cuda.synchronize()
+        # the call's host path in parts: the Add alone, the Get alone, one-batch forms
+        parts = {}
+        one_add = sh.prepare(sets[0]["batches"][:1])
+        one_get = sh.prepare([(sets[0]["pull_keys"][0], form.outs[0][0])], is_get=True)
+        for name, fn in (("add_grouped (all batches)", lambda i: sh.add_grouped(form.adds[i % R], sorted_hint=True)),
+                         ("get_grouped (all batches)", lambda i: sh.get_grouped(form.gets[i % R])),
+                         ("add_grouped (1 batch)", lambda i: sh.add_grouped(one_add, sorted_hint=True)),
+                         ("get_grouped (1 batch)", lambda i: sh.get_grouped(one_get)),
+                         ("a library call that queues nothing (pskv_get_option)", lambda i: sh.get_option("NT")),
+                         ("nothing", lambda i: None)):
+            torch.cuda._sleep(20_000_000)
+            t0 = time.perf_counter()
+            for i in range(20):
+                fn(i)
+            parts[name] = (time.perf_counter() - t0) / 20 * 1e6
+            torch.cuda.synchronize()
         idle = []
         for _ in range(50):
             t0 = time.perf_counter()
@@ -66,6 +82,8 @@ def main():
         for k in (1, 2, 5, 10, 20, 50, 200):
             res[k] = statistics.median(region(k, 7 * j) / k for j in range(7))
         print(f"{emu}: host_call_us {host:.1f}, sync_idle_us {statistics.median(idle):.1f}")
+        for n, v in parts.items():
+            print(f"  host us per call, {n}: {v:.1f}")
         for k, v in res.items():
             print(f"  K = {k:3d}: {v:7.2f} us per step (fixed cost if the step is the K = 200 figure: "
                   f"{(v - res[200]) * k:6.1f} us per region)", flush=True)
