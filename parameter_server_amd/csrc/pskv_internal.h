@@ -179,7 +179,7 @@ hipError_t launch_rb_add(int dtype, int mode, const GroupArgs& ga, uint32_t nsc,
                          int apply_log2, int bin_block, uint16_t* loff, void* tmp,
                          hipStream_t st);
 uint32_t rb_superchunk(int vb, int bin_block);
-constexpr size_t kRbTmpPad = 256;  // bytes past the last entry K5b may read (up to 10 entries of its run loads)
+constexpr size_t kRbTmpPad = 16;  // bytes past the last entry K5b may read (paired loads)
 // K8: one small host message carried in the kernarg segment (one workgroup).
 // Get writes its n values to `out` (page-locked host memory or device memory);
 // with `done` non-null it then stores `seq` there (system-scope release) for a

@@ -1746,29 +1746,6 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
   // length reads one entry past its end: the next run's, or the scratch
   // buffer's tail pad (launch_rb_add's caller allocates kRbTmpPad bytes more).
   auto load_run = [&](uint32_t a, uint32_t e, Ent (&x)[RPT]) {
-#ifdef PSKV_K5B_READY_BEFORE_STORES
-    // every load issued, whatever the run's length (no branch around a load,
-    // so none waits where it is issued): entries past the run are read from
-    // the next run or the buffer's tail pad and ignored; a thread without a
-    // run reads region 0
-    const size_t b0 = has_run ? (size_t)st0 + a : 0;
-    (void)e;
-    if constexpr (sizeof(Ent) == 8) {
-#pragma unroll
-      for (int q = 0; q < RPT; q += 2) {
-        uint32_t w[4];
-        ld16a4<false>(reinterpret_cast<const uint32_t*>(tmp + b0 + q), w);
-        x[q].key = w[0];
-        x[q].val = w[1];
-        x[q + 1].key = w[2];
-        x[q + 1].val = w[3];
-      }
-    } else {
-#pragma unroll
-      for (int q = 0; q < RPT; ++q) x[q] = tmp[b0 + q];
-    }
-    return;
-#endif
     if constexpr (sizeof(Ent) == 8) {
       static_assert(RPT % 2 == 0, "whole pairs");
 #pragma unroll
@@ -1797,24 +1774,11 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
       *reinterpret_cast<u32x4*>(&best[i]) = u32x4{0u, 0u, 0u, 0u};
   };
   uint32_t ra, re, na, ne_;
-  Ent xn[RPT];
-  // Everything the next iteration's top reads (its run xn, the bounds na /
-  // ne_ after it) complete BEFORE this bucket's scattered stores are issued:
-  // the memory counter is in order and counts stores, so a wait for those
-  // loads placed after the stores (at the loop top) waits for the stores'
-  // acknowledgements too.
-  auto next_ready = [&]() {
-#ifdef PSKV_K5B_READY_BEFORE_STORES
-#pragma unroll
-    for (int q = 0; q < RPT; ++q) asm volatile("" ::"v"(xn[q].key), "v"(xn[q].val));
-    asm volatile("" ::"v"(na), "v"(ne_));
-#endif
-  };
   bounds(b, ra, re);
   if (!bounds_ok(b)) ra = re = 0;
   bounds(b + per_xcd, na, ne_);
+  Ent xn[RPT];
   load_run(ra, re, xn);
-  next_ready();  // complete on entry as on the back edge: no wait at the loop top
   uint32_t it = 0;
   for (uint32_t pass = 0; b < b_hi; b += per_xcd, it = it == 2u ? 0u : it + 1u, ++pass) {
     K5_STAMP(1, pass, 0);
@@ -1886,7 +1850,6 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
         if (h + 1 < halves) __syncthreads();  // the table is read before the next pass
       }
       K5_STAMP(1, pass, 2);
-      next_ready();
 #pragma unroll
       for (int q = 0; q < RPT; ++q)
         if (win >> q & 1u) store_winner(b, x[q].key, (BT)x[q].val);
@@ -1926,7 +1889,6 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
         insert_one(y.key, pos - 1u, (BT)y.val);
       }
       __syncthreads();
-      next_ready();
       if (MODE == 0) {
 #pragma unroll
         for (int q = 0; q < RPT; ++q)
