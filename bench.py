@@ -318,7 +318,7 @@ class Form:
 
     def step(self, i):
         # the grouped Add then the grouped Get, in one call
-        # (pskv_add_get_grouped: the K2g launch + its conditional replay, then K1)
+        # (pskv_add_get_grouped: the K2g launch, then K1 carrying its conditional replay -- K1r)
         self.shard.add_get_grouped(self.adds[i % self.R], self.gets[i % self.R], sorted_hint=self.hint)
 
     def bytes(self, steps):
