@@ -108,11 +108,11 @@ for step in "$@"; do
          PSKV_BENCH_EMULATE=0/2 timeout -k 10 200 python3 "$R/bench.py" --steps 20 --no-zipf --no-cpu-baseline --no-extra \
            > "$OUT/emu02.json" 2> "$OUT/emu02.err" ;;
     emu8all) for r in 0 1 2 3 4 5 6 7; do
-          PSKV_BENCH_EMULATE=$r/8 timeout -k 10 200 python3 "$R/bench.py" --steps 50 --no-zipf --no-cpu-baseline \
+          PSKV_BENCH_EMULATE=$r/8 timeout -k 10 200 python3 "$R/bench.py" --steps ${EMU_STEPS:-50} --no-zipf --no-cpu-baseline \
             --no-extra > "$OUT/emu8_$r.json" 2> "$OUT/emu8_$r.err" || exit 1
         done ;;
     emu_curve) for n in 2 4; do for r in $(seq 0 $((n - 1))); do
-          PSKV_BENCH_EMULATE=$r/$n timeout -k 10 200 python3 "$R/bench.py" --steps 50 --no-zipf --no-cpu-baseline \
+          PSKV_BENCH_EMULATE=$r/$n timeout -k 10 200 python3 "$R/bench.py" --steps ${EMU_STEPS:-50} --no-zipf --no-cpu-baseline \
             --no-extra > "$OUT/emu${n}_$r.json" 2> "$OUT/emu${n}_$r.err" || exit 1
         done; done ;;
     emutrace) PSKV_BENCH_EMULATE=0/8 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/emutrace" -o run \
