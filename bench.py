@@ -40,7 +40,8 @@ Bytes per step (counting what the step must move):
 Prints ONE JSON line on rank 0 with roofline (per-kernel rates from HIP events
 on the launch stream, the dominant kernel's as `frac`, and the cold form's) and
 cpu_baseline (the oracle restatement of the reference storages timed on this
-host, N = 1 only).
+host by rank 0: one thread with one storage at N = 1, beside 8 server threads
+with 8 storages; at N > 1 the 8-thread sample is the value).
 """
 from __future__ import annotations
 
@@ -421,10 +422,14 @@ def run_form(form, steps, warmup, world, dev):
 # ------------------------------------------------------------ CPU baseline
 
 
-def cpu_baseline(bases, B, n_batches, vector_sizes):
-    """The oracle (C++ restatement of server/map_storage.hpp, 1 thread) on a
-    bounded sample of the same workload; VectorStorage (cfg 1) at several sizes
-    with the a*n^2 fit extrapolated to config 1's 1e6 keys."""
+def cpu_baseline(bases, B, n_batches, vector_sizes, servers=1):
+    """The oracle (C++ restatement of server/map_storage.hpp) on a bounded
+    sample of the same workload: one thread with one storage, and 8 server
+    threads with one storage each (the reference runs one storage
+    per server thread); VectorStorage (cfg 1) at several sizes with the a*n^2
+    fit extrapolated to config 1's 1e6 keys (skipped with no sizes).
+    servers = 8 (the N > 1 line) reports the 8-thread sample as the baseline
+    value, the 1-thread one beside it."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test infrastructure: the CPU baseline leg
 
@@ -439,7 +444,8 @@ def cpu_baseline(bases, B, n_batches, vector_sizes):
     for k in ks:
         m.get(k)
     t_map = time.perf_counter() - t0
-    vector = vector_storage_fit(oracle, vector_sizes)
+    m.close()
+    vector = vector_storage_fit(oracle, vector_sizes) if vector_sizes else None
     # 8 server threads with 8 storages (the reference runs one
     # storage per server thread); ctypes drops the GIL inside the oracle calls
     import threading
@@ -469,20 +475,30 @@ def cpu_baseline(bases, B, n_batches, vector_sizes):
     u = B * len(set(int(b) for b in bases[:n_batches]))
     add_b, get_b = step_bytes(B * len(ks), u, B * len(ks))
     u_mt = B * len(set(int(b) for b in bases[:mt_batches]))
-    return {
+    for sh in shards:
+        sh.close()
+    one = {
         "value": (add_b + get_b) / t_map / 1e9,
         "unit": "GB/s",
         "cores": 1,
         "kind": "port",
         "sample": f"MapStorage restatement (std::map, 1 thread), {len(ks)} x {B} contiguous float keys of the "
                   f"same workload (window set 0), Add then Get, {t_map:.2f} s",
-        "vector_storage": vector,
-        "eight_threads": {
-            "value": sum(step_bytes(B * mt_batches, u_mt, B * mt_batches)) * T / t_mt / 1e9, "unit": "GB/s",
-            "cores": T, "seconds": t_mt,
-            "sample": f"{T} threads x one MapStorage restatement each, {mt_batches} x {B} keys per thread"},
-        "host_cpu": _cpu_model(),
     }
+    eight = {
+        "value": sum(step_bytes(B * mt_batches, u_mt, B * mt_batches)) * T / t_mt / 1e9, "unit": "GB/s",
+        "cores": T, "kind": "port", "seconds": t_mt,
+        "sample": f"{T} server threads x one MapStorage restatement each (the reference's one storage per server "
+                  f"thread), {mt_batches} x {B} contiguous float keys of window set 0 per thread, Add then Get, "
+                  f"{t_mt:.2f} s"}
+    if servers == 1:
+        rec = dict(one, eight_threads=eight)
+    else:
+        rec = dict(eight, one_thread=one)
+    if vector is not None:
+        rec["vector_storage"] = vector
+    rec["host_cpu"] = _cpu_model()
+    return rec
 
 
 def vector_storage_fit(oracle, sizes):
@@ -526,9 +542,6 @@ def vector_storage_fit(oracle, sizes):
             "fit_seconds": {"a_n2": a, "form": "t = a * n^2, least squares"},
             "extrapolated_1e6_seconds": t1e6,
             "value": 24.0 * 1e6 / t1e6 / 1e9, "unit": "GB/s",
-            "measured_1e6": {"seconds": 215.0, "GB/s": 24.0 * 1e6 / 215.0 / 1e9,
-                             "source": "bench.py --vector-only --vector-sizes 1000000 on an MI355X box's host "
-                                       "(AMD EPYC 9575F), profiles/r03_vector_storage_1e6.log"},
             "sample": "VectorStorage restatement (append + O(stored x queried) last-match scan), config 1's "
                       "contiguous float keys at the sizes listed, 1 thread; value = the a*n^2 fit at 1e6 keys"}
 
@@ -1176,12 +1189,18 @@ def main(argv=None):
             del wf, wsets
     shard.set_stream(None)
     shard.close()
-    if rank == 0 and pworld == 1 and not args.no_cpu_baseline:
-        sizes = [int(x) for x in args.vector_sizes.split(",") if x]
+    if rank == 0 and not args.no_cpu_baseline:
         progress("cpu baseline")
-        result["cpu_baseline"] = cpu_baseline([f for _, f, _ in sets[0]["slices"]], B, args.cpu_batches, sizes)
-        if zipf_res is not None:  # cfg 3's own CPU baseline: the same Zipf batches
-            result["cpu_baseline"]["zipf"] = _zipf_cpu_sample(zb[:2], B)
+        if pworld == 1:
+            sizes = [int(x) for x in args.vector_sizes.split(",") if x]
+            result["cpu_baseline"] = cpu_baseline([f for _, f, _ in sets[0]["slices"]], B, args.cpu_batches, sizes)
+            if zipf_res is not None:  # cfg 3's own CPU baseline: the same Zipf batches
+                result["cpu_baseline"]["zipf"] = _zipf_cpu_sample(zb[:2], B)
+        else:
+            # cfg 4's baseline: 8 server threads with 8 storages on
+            # this host, over the producers' windows of set 0, after every timed
+            # region (the other ranks wait at the closing barrier meanwhile)
+            result["cpu_baseline"] = cpu_baseline(list(sets[0]["bases"]), B, 16, [], servers=8)
     if zipf_res is not None:
         del zb
     if pworld == 1 and not args.no_extra:

@@ -192,7 +192,12 @@ int pskv_add_get_grouped(pskv_shard* s, const pskv_batch* adds, uint64_t na, con
  * SYNC_TIMEOUT_MS (default 120000; 0 = unbounded): work that does not complete
  * in time fails the call with PSKV_ESTATE, and pskv_last_error() names the
  * stream or event waited for, the device and the last kernel the shard
- * queued.  Nothing is cancelled or restarted. */
+ * queued.  Nothing is cancelled or restarted: after a call fails with
+ * PSKV_ESTATE its queued work may still read the call's host inputs (a direct
+ * DMA from the caller's buffers) or write its host outputs (a Get's values
+ * into page-locked memory), so the caller keeps those buffers alive and
+ * unmodified until a later pskv_sync succeeds.  (The library's own staging is
+ * held back the same way: the next call waits for it, bounded.) */
 int pskv_sync(pskv_shard* s);
 /* Zero every value (dense array and overflow table). */
 int pskv_clear(pskv_shard* s);

@@ -716,6 +716,15 @@ int read_overflow_stat(pskv_shard* s, uint32_t* count, uint32_t* err) {
   return PSKV_OK;
 }
 
+// A call that gives up on a wait (PSKV_ESTATE) or fails after queueing work
+// that still reads or writes the pinned staging buffer (H2D from it, D2H or K1
+// stores into it): mark the buffer busy until the stream's current end, so the
+// next host call waits (bounded) before its CPU copy touches the buffer or a
+// regrowth frees it.
+void hold_hstage(pskv_shard* s) {
+  if (hipEventRecord(s->hstage_free, s->stream) == hipSuccess) s->hstage_pending = true;
+}
+
 int ensure_hstage(pskv_shard* s, size_t bytes) {
   if (s->hstage_pending) {
     if (int rc = wait_event(s, s->hstage_free, "pinned staging release event", s->hstage_free)) return rc;
@@ -959,12 +968,12 @@ int general_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_
 // A held replay (see replay) launched as K4r, its own launch.
 int flush_replay(pskv_shard* s) {
   if (!s->pend_replay) return PSKV_OK;
-  s->pend_replay = false;
   GroupArgs ga;
   ga.nb = s->pend_rg.nb;
   for (int i = 0; i < ga.nb; ++i) ga.b[i] = s->pend_rg.b[i];
   LaunchTimer t(s, PSKV_K_REPLAY, s->pend_elems);
   PSKV_HIP(launch_replay(s->dtype, s->mode, ga, s->dview(), s->ovf, s->flag, s->pend_epoch, s->stream));
+  s->pend_replay = false;  // (held until its launch is queued)
   t.done();
   s->n_general++;
   return PSKV_OK;
@@ -1164,7 +1173,11 @@ int pipelined_h2d(pskv_shard* s, std::vector<Piece>& pieces, char* h, char* d) {
     run_pieces(pieces, i, j, [&](Piece& p) { copy_piece(p, s->key_begin, s->range); });
     char* lo = pieces[i].dst;
     char* hi = pieces[j - 1].dst + pieces[j - 1].bytes;
-    PSKV_HIP(hipMemcpyAsync(d + (lo - h), lo, (size_t)(hi - lo), hipMemcpyHostToDevice, s->stream));
+    const hipError_t e = hipMemcpyAsync(d + (lo - h), lo, (size_t)(hi - lo), hipMemcpyHostToDevice, s->stream);
+    if (e != hipSuccess) {
+      if (i) hold_hstage(s);  // the windows queued before still read the staging
+      PSKV_HIP(e);
+    }
     i = j;
   }
   return PSKV_OK;
@@ -1688,10 +1701,17 @@ int zero_copy_get(pskv_shard* s, const std::vector<pskv_batch>& v, bool vec) {
     const int gu = gather_unroll(s, elems);
     const uint32_t nwg = build_group(hv, g.first, g.second, stream_chunk(gu), &ga);
     LaunchTimer t(s, PSKV_K_GATHER, elems);
-    PSKV_HIP(launch_gather(s->vb, vec, gu, s->tune_nt, ga, nwg, s->dview(), s->ovf, s->stream));
+    const hipError_t e = launch_gather(s->vb, vec, gu, s->tune_nt, ga, nwg, s->dview(), s->ovf, s->stream);
+    if (e != hipSuccess) {
+      hold_hstage(s);  // earlier groups' K1 still read / write the staging
+      PSKV_HIP(e);
+    }
     t.done();
   }
-  if (int rc = wait_stream(s, s->stream, "shard stream (zero-copy Get)")) return rc;
+  if (int rc = wait_stream(s, s->stream, "shard stream (zero-copy Get)")) {
+    hold_hstage(s);  // its K1 may still write into the staging
+    return rc;
+  }
   for (size_t i = 0; i < v.size(); ++i) std::memcpy(v[i].vals, hv[i].vals, v[i].n * (size_t)s->vb);
   return PSKV_OK;
 }
@@ -1849,14 +1869,19 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
     const int gu = gather_unroll(s, elems);
     const uint32_t nwg = build_group(dv, g.first, g.second, stream_chunk(gu), &ga);
     LaunchTimer t(s, PSKV_K_GATHER, elems);
+    hipError_t e;
     if (s->pend_replay && nwg > 0) {
-      // the Add's held replay rides on this first K1 (pskv_add_get_grouped)
-      s->pend_replay = false;
-      PSKV_HIP(launch_gather_replay(s->vb, vec, gu, s->tune_nt, ga, nwg, s->dview(), s->ovf, s->pend_rg,
-                                    s->flag, s->pend_epoch, s->flag + 16, s->stream));
+      // the Add's held replay rides on this first K1 (pskv_add_get_grouped);
+      // it stays held (for add_get_impl's trailing K4r) unless this launch is queued
+      e = launch_gather_replay(s->vb, vec, gu, s->tune_nt, ga, nwg, s->dview(), s->ovf, s->pend_rg,
+                               s->flag, s->pend_epoch, s->flag + 16, s->stream);
+      if (e == hipSuccess) s->pend_replay = false;
     } else {
-      PSKV_HIP(launch_gather(s->vb, vec, gu, s->tune_nt, ga, nwg, s->dview(), s->ovf,
-                             s->stream));
+      e = launch_gather(s->vb, vec, gu, s->tune_nt, ga, nwg, s->dview(), s->ovf, s->stream);
+    }
+    if (e != hipSuccess) {
+      if (!device) hold_hstage(s);  // the keys' H2D from the staging is queued
+      PSKV_HIP(e);
     }
     t.done();
   }
@@ -1894,12 +1919,19 @@ int get_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
     for (size_t w = 0; w < wins.size(); ++w) {
       const char* lo = pieces[wins[w].first].src;
       const char* hi = pieces[wins[w].second - 1].src + pieces[wins[w].second - 1].bytes;
-      PSKV_HIP(hipMemcpyAsync(const_cast<char*>(lo), d + (lo - h), (size_t)(hi - lo),
-                              hipMemcpyDeviceToHost, s->stream));
-      PSKV_HIP(hipEventRecord(s->win_events[w], s->stream));
+      hipError_t e = hipMemcpyAsync(const_cast<char*>(lo), d + (lo - h), (size_t)(hi - lo),
+                                    hipMemcpyDeviceToHost, s->stream);
+      if (e == hipSuccess) e = hipEventRecord(s->win_events[w], s->stream);
+      if (e != hipSuccess) {
+        hold_hstage(s);  // earlier windows' D2H still write into the staging
+        PSKV_HIP(e);
+      }
     }
     for (size_t w = 0; w < wins.size(); ++w) {
-      if (int rc = wait_event(s, s->win_events[w], "D2H window event (Get to host)", s->win_events[w])) return rc;
+      if (int rc = wait_event(s, s->win_events[w], "D2H window event (Get to host)", s->win_events[w])) {
+        hold_hstage(s);  // the queued D2H copies still write into the staging
+        return rc;
+      }
       run_pieces(pieces, wins[w].first, wins[w].second,
                  [&](Piece& p) { copy_piece(p, s->key_begin, s->range); });
     }
@@ -2170,13 +2202,16 @@ int pskv_shard_destroy(pskv_shard* s) {
   if (s->out_stream) drain(s->out_stream, "D2H output stream (destroy)");
   if (s->own_stream) drain(s->own_stream, "shard stream (destroy)");
   if (s->stream && s->stream != s->own_stream) drain(s->stream, "caller stream (destroy)");
-  if (s->counted) g_queues.add_shard(s->device, -1);
-  if (s->out_stream) g_queues.add_stream(s->device, -1);
   if (!stuck.empty()) {
+    // the leaked streams keep their hardware queues: they stay counted in
+    // g_queues (pskv_queues.h), so later shards on this device do not plan
+    // with queues that are still held
     std::fprintf(stderr, "pskv: shard destroy: %s; its device memory and streams are not freed\n", stuck.c_str());
     delete s;
     return fail(PSKV_ESTATE, "pskv_shard_destroy: " + stuck);
   }
+  if (s->counted) g_queues.add_shard(s->device, -1);
+  if (s->out_stream) g_queues.add_stream(s->device, -1);
   if (s->srv) (void)hipHostFree(s->srv);
   if (s->srv_stream) (void)hipStreamDestroy(s->srv_stream);
   if (s->srv_dep) (void)hipEventDestroy(s->srv_dep);

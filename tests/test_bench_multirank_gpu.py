@@ -53,3 +53,7 @@ def test_bench_ranks_one_gpu(cuda, world):
     assert "cold" not in res["roofline"]  # the cold form is an N = 1 figure
     assert res["zipf_sparse"]["n_gpus"] == world  # cfg 3 on every rank
     assert res["extra"]["weak_scaled"]["GB/s"] > 0
+    # cfg 4's CPU baseline: 8 server threads x 8 MapStorage restatements
+    cb = res["cpu_baseline"]
+    assert cb["cores"] == 8 and cb["value"] > 0 and cb["kind"] == "port"
+    assert cb["one_thread"]["cores"] == 1 and cb["one_thread"]["value"] > 0

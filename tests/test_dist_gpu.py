@@ -39,56 +39,14 @@ def _rank(rank, world, port, q):
 
         import bench
         import oracle
-        import parameter_server_amd as ps
 
         oracle.build()
         r_, w_, local = bench.dist_init(bench.parse([]))
         assert (r_, w_, local) == (rank, world, 0)
         dev = torch.device("cuda:0")
-        J, B, R = 64, 1_000_000, 3
-        sets = [bench.make_set(rank, world, J, B, dev, r) for r in range(2)]
-        # a third set whose windows surely straddle every range boundary (and
-        # overlap each other across it): the range map splits each in two
-        bases = straddle_bases(world)
-        sets.append(bench.make_set(rank, world, len(bases), B, dev, 2, bases=bases))
-        own_edges = sum(1 for m in edges(world) if m in (rank * (10 ** 9 // world), (rank + 1) * (10 ** 9 // world)))
-        assert len(sets[2]["slices"]) == 4 * own_edges and all(n < B for _, _, n in sets[2]["slices"])
-        _, lo, hi, _, _ = bench.plan_rank(rank, world, J, B)
-        assert hi - lo == 1_000_000_000 // world
-        ref = np.zeros(hi - lo, np.float32)
-        host = [[(f, v.cpu().numpy()) for (_, f, _), (_, v) in zip(s["slices"], s["batches"])] for s in sets]
-        with ps.Shard(lo, hi, np.float32, device=0) as sh:
-            sh.set_stream(torch.cuda.current_stream().cuda_stream)
-            form = bench.Form(sh, sets, dev)
-            steps = 2 * R
-            # stepwise: every pull against the oracle state after the step's Add
-            for i in range(steps):
-                for f, v in host[i % R]:
-                    oracle.dense_last_wins(ref, lo, np.arange(f, f + v.size, dtype=np.uint32), v)
-                form.step(i)
-                torch.cuda.synchronize()
-                t = i % R
-                assert bench.overlap_keys(sets[t]) == 0
-                for (_, f, n), o in zip(form.pull_slices[t], form.outs[t]):
-                    got = o.cpu().numpy()
-                    if not np.array_equal(got.view(np.uint32), ref[f - lo:f - lo + n].view(np.uint32)):
-                        raise AssertionError(f"rank {rank} step {i}: pull of key {f} differs from the oracle")
-            # the timed region as bench.py runs it, then the oracle catches up
-            elapsed, own = bench.timed(form, steps, world, dev)
-            assert elapsed >= own > 0
-            for i in range(steps):
-                for f, v in host[i % R]:
-                    oracle.dense_last_wins(ref, lo, np.arange(f, f + v.size, dtype=np.uint32), v)
-            dense = sh.dense_view().cpu().numpy()
-            sh.set_stream(None)
-            sh.sync()
-        if not np.array_equal(dense.view(np.uint32), ref.view(np.uint32)):
-            bad = np.nonzero(dense.view(np.uint32) != ref.view(np.uint32))[0]
-            raise AssertionError(f"rank {rank}: {bad.size} keys differ, first at {lo + bad[:4]}")
-        n_slices = sum(len(s["slices"]) for s in sets)
-        split = sum(1 for s in sets for _, _, n in s["slices"] if n < B)
-        total = bench.sum_over_ranks(float(sum(n for s in sets for _, _, n in s["slices"])), world, dev)
-        q.put((rank, "ok", n_slices, split, total, int(np.count_nonzero(ref))))
+        n_slices, split, keys, nz = _run_share(rank, world, world, dev)
+        total = bench.sum_over_ranks(float(keys), world, dev)
+        q.put((rank, "ok", n_slices, split, total, nz))
         bench.barrier(world)
         import torch.distributed as dist
 
@@ -98,6 +56,88 @@ def _rank(rank, world, port, q):
 
         q.put((rank, "error", traceback.format_exc(), 0, 0, 0))
         raise
+
+
+def _run_share(rank, world, sync_world, dev):
+    """Rank `rank`'s share of the `world`-GPU cfg-4 plan on `dev`: two drawn
+    window sets of 64 producers plus one whose windows straddle every range
+    boundary, 2 x 3 steps through bench.Form.step checked pull by pull against
+    the oracle, then the same steps through bench.timed, then the WHOLE dense
+    array against the oracle.  `sync_world` is the process group's size (1: the
+    share runs alone, no collective).  Returns (slices, split slices, keys
+    routed here, nonzero keys of the final state)."""
+    import torch
+
+    import bench
+    import oracle
+    import parameter_server_amd as ps
+
+    J, B, R = 64, 1_000_000, 3
+    sets = [bench.make_set(rank, world, J, B, dev, r) for r in range(2)]
+    # a third set whose windows surely straddle every range boundary (and
+    # overlap each other across it): the range map splits each in two
+    bases = straddle_bases(world)
+    sets.append(bench.make_set(rank, world, len(bases), B, dev, 2, bases=bases))
+    own_edges = sum(1 for m in edges(world) if m in (rank * (10 ** 9 // world), (rank + 1) * (10 ** 9 // world)))
+    assert len(sets[2]["slices"]) == 4 * own_edges and all(n < B for _, _, n in sets[2]["slices"])
+    _, lo, hi, _, _ = bench.plan_rank(rank, world, J, B)
+    assert hi - lo == 1_000_000_000 // world
+    ref = np.zeros(hi - lo, np.float32)
+    host = [[(f, v.cpu().numpy()) for (_, f, _), (_, v) in zip(s["slices"], s["batches"])] for s in sets]
+    with ps.Shard(lo, hi, np.float32, device=dev.index or 0) as sh:
+        sh.set_stream(torch.cuda.current_stream().cuda_stream)
+        form = bench.Form(sh, sets, dev)
+        steps = 2 * R
+        # stepwise: every pull against the oracle state after the step's Add
+        for i in range(steps):
+            for f, v in host[i % R]:
+                oracle.dense_last_wins(ref, lo, np.arange(f, f + v.size, dtype=np.uint32), v)
+            form.step(i)
+            torch.cuda.synchronize()
+            t = i % R
+            assert bench.overlap_keys(sets[t]) == 0
+            for (_, f, n), o in zip(form.pull_slices[t], form.outs[t]):
+                got = o.cpu().numpy()
+                if not np.array_equal(got.view(np.uint32), ref[f - lo:f - lo + n].view(np.uint32)):
+                    raise AssertionError(f"rank {rank}/{world} step {i}: pull of key {f} differs from the oracle")
+        # the timed region as bench.py runs it, then the oracle catches up
+        elapsed, own = bench.timed(form, steps, sync_world, dev)
+        assert elapsed >= own > 0
+        for i in range(steps):
+            for f, v in host[i % R]:
+                oracle.dense_last_wins(ref, lo, np.arange(f, f + v.size, dtype=np.uint32), v)
+        dense = sh.dense_view().cpu().numpy()
+        sh.set_stream(None)
+        sh.sync()
+        del form
+    if not np.array_equal(dense.view(np.uint32), ref.view(np.uint32)):
+        bad = np.nonzero(dense.view(np.uint32) != ref.view(np.uint32))[0]
+        raise AssertionError(f"rank {rank}/{world}: {bad.size} keys differ, first at {lo + bad[:4]}")
+    n_slices = sum(len(s["slices"]) for s in sets)
+    split = sum(1 for s in sets for _, _, n in s["slices"] if n < B)
+    keys = sum(n for s in sets for _, _, n in s["slices"])
+    nz = int(np.count_nonzero(ref))
+    del sets, ref, dense
+    torch.cuda.empty_cache()
+    return n_slices, split, keys, nz
+
+
+@pytest.mark.parametrize("world", [8])
+def test_cfg4_rank_shares_bit_exact(cuda, oracle_mod, world):
+    """The N = 8 cfg-4 plan the driver's 8-GPU run executes, one rank's share at
+    a time on cuda:0 in this process (eight processes on one GPU is the
+    shared-device rehearsal DESIGN.md §8 records as stalling in torch's
+    device-wide sorts): every rank's 1.25e8-key range shard, its slices of the
+    64-producer window sets, the straddling windows at all 7 boundaries, every
+    pull and the whole final array bit-exact against the oracle
+    (base/range_partition_manager.hpp:19-46, server/map_storage.hpp:17-27)."""
+    res = [_run_share(r, world, 1, cuda) for r in range(world)]
+    # every set's windows arrived whole over the ranks (straddling ones in two)
+    assert sum(r[2] for r in res) == (2 * 64 + len(straddle_bases(world))) * 1_000_000
+    assert all(r[0] > 0 and r[3] > 0 for r in res)
+    # split slices: the outer ranks hold one boundary (4 straddling windows),
+    # the inner ranks two
+    assert res[0][1] >= 4 and res[-1][1] >= 4 and all(r[1] >= 8 for r in res[1:-1])
 
 
 def edges(world):

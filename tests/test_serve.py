@@ -245,3 +245,44 @@ def test_serve_wait_is_bounded(cuda, oracle_mod, serve):
         torch.cuda.synchronize()
         sh.set_option("SYNC_TIMEOUT_MS", 0)
         assert_bits_equal(sh.get(q), ref.get(q), "after the earlier work drained")
+
+
+def test_timed_out_get_holds_staging(cuda, oracle_mod):
+    """A staged host Get that gives up on its D2H wait (SYNC_TIMEOUT_MS) leaves
+    its H2D, K1 and D2H queued on the pinned staging buffer; the next host Get
+    must not write its keys there until that work has drained.
+    The second Get is larger, so its keys cover the first one's value region
+    in the staging: without the hold the first Get's late D2H lands on them
+    before they are DMA'd, and the second Get answers other keys."""
+    import torch
+
+    import parameter_server_amd as ps
+    from parameter_server_amd import PskvError, _lib
+
+    rng = np.random.default_rng(53)
+    ref = oracle_mod.MapStorageRef(np.float32)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    torch.cuda._sleep(50_000_000)
+    e1.record()
+    torch.cuda.synchronize()
+    cycles_per_ms = 50_000_000 / max(e0.elapsed_time(e1), 1e-3)
+    # staged Gets only: no inline (K8), no zero copy, no direct pageable DMA
+    opts = dict(INLINE=0, ZC_MAX_BYTES=0, PAGEABLE_DMA=0, SYNC_TIMEOUT_MS=500)
+    n = 1_000_000
+    with ps.Shard(0, n, np.float32, options=opts) as sh:
+        k = np.arange(n, dtype=np.uint32)
+        v = rng.standard_normal(n).astype(np.float32)
+        sh.add(k, v)
+        ref.add(k, v)
+        sh.sync()
+        q1 = rng.integers(0, n, size=20_000).astype(np.uint32)
+        q2 = rng.integers(0, n, size=200_000).astype(np.uint32)
+        torch.cuda._sleep(int(2000 * cycles_per_ms))  # ~2 s of earlier work on the legacy stream
+        with pytest.raises(PskvError) as ei:
+            sh.get(q1)
+        assert ei.value.code == _lib.PSKV_ESTATE and "not complete after" in str(ei.value), str(ei.value)
+        sh.set_option("SYNC_TIMEOUT_MS", 0)
+        got = sh.get(q2)  # waits for the held staging, then stages its own keys
+        assert_bits_equal(got, ref.get(q2), "Get after a timed-out Get")
+        assert_bits_equal(sh.get(q1), ref.get(q1), "the timed-out Get, again")
