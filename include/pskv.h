@@ -32,14 +32,16 @@
  *
  * Keys outside [key_begin, key_end) are legal (the reference's last range
  * server receives every out-of-range key, range_partition_manager.hpp:26-27):
- * they live in a device-side overflow hash table with the same semantics.
- * Host inputs are counted while they are checked, and the table grows before
- * the kernels run, so host calls (the reference's case) never run out of room.
- * For PSKV_DEVICE inputs the keys are not read on the host: the table grows at
- * pskv_sync (to keep its load <= 1/2), and one device call may add at most
- * (capacity - stored) new out-of-range keys; beyond that keys are dropped and
- * the next pskv_sync returns PSKV_ESTATE.  Size the table for the largest
- * out-of-range burst a device caller expects (pskv_shard_create_ex).
+ * they live in a device-side overflow hash table with the same semantics, and
+ * there is no limit on how many (as the reference's std::map has none).  Every
+ * out-of-range insert, from host or device inputs, is made by ONE workgroup
+ * that first reserves room: when the table would pass 3/4 load it asks the
+ * library's grow service (a host thread) for larger arrays and rehashes into
+ * them on the device, in stream order, so device callers need no host step
+ * and no sizing (round 6; DESIGN.md §4 "Overflow growth").  pskv_sync trims
+ * the load back to <= 1/2.  Keys are dropped -- and the next pskv_sync returns
+ * PSKV_ESTATE -- only if a growth request is not answered within
+ * SYNC_TIMEOUT_MS or its allocation fails (device memory exhausted).
  *
  * Threading: one shard handle is used by one host thread at a time (the
  * reference calls a storage only from its ServerThread, server_thread.cpp:20-50);

@@ -4,10 +4,10 @@
 // HBM layout of one shard (DESIGN.md "Data layout in HBM"):
 //   dense[range]        value array, one slot per owned key, zero-initialised
 //   owner[range]        u64 last-writer stamps (epoch<<32 | group index), general path only
-//   ovf.keys[cap]       u64 overflow hash keys, EMPTY = ~0
-//   ovf.vals[cap]       overflow values
-//   ovf.owner[cap]      overflow stamps
-//   ovf.stat[2]         {occupied slots, sticky error bits}
+//   ctl                 OvfCtl: the overflow table's current arrays, {occupied
+//                       slots, sticky error bits}, the growth mailbox
+//   keys[cap]           u64 overflow hash keys, EMPTY = ~0
+//   vals[cap]           overflow values
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stddef.h>
@@ -110,12 +110,41 @@ struct DenseView {
   uint64_t range;  // number of owned keys, <= 2^32
 };
 
-struct Ovf {
+// The overflow table: open addressing over u64 key slots (EMPTY = ~0) for the
+// keys outside the dense range (the last range server's fall-through keys,
+// range_partition_manager.hpp:26-27).  Its arrays can be replaced while work
+// is queued -- a single-workgroup inserter grows the table on the device
+// (ovf_reserve, DESIGN.md §4 "Overflow growth") -- so kernels reach them
+// through the shard's control block, whose address is fixed for the shard's
+// life, and load them when they meet an out-of-range key.
+struct OvfTab {
   unsigned long long* keys;
   void* vals;
-  unsigned long long* owner;
-  uint32_t* stat;
   uint64_t mask;  // capacity - 1 (capacity is a power of two)
+};
+// Growth requests of device-side inserters: one per shard, in coherent
+// page-locked host memory; the library's grow service (pskv_shard.cpp) answers
+// each with fresh arrays of the asked capacity, the requesting workgroup fills
+// and rehashes them itself and switches the control block over.
+struct OvfMbox {
+  uint32_t req_seq;   // device: number of the last request
+  uint32_t pad0;
+  uint64_t req_cap;   // device: slots asked for (a power of two)
+  uint64_t wait_ticks;  // host: bound of a request's wait (device wall-clock ticks)
+  uint64_t pad1[5];
+  uint32_t resp_seq;  // host: number of the last request answered
+  uint32_t resp_ok;   // host: 1 = resp_tab holds uninitialised arrays of req_cap slots
+  OvfTab resp_tab;
+  uint64_t pad2[4];
+};
+static_assert(sizeof(OvfMbox) == 128, "device and host words on separate 64-byte lines");
+struct OvfCtl {  // device memory
+  OvfTab t;          // the current table
+  uint32_t stat[2];  // {occupied slots, sticky error bits}
+  OvfMbox* mbox;     // growth requests
+};
+struct Ovf {  // kernel argument
+  OvfCtl* c;
 };
 
 // Launch wrappers (pskv_kernels.hip).  vb = value bytes (4 or 8), vec = all
@@ -134,18 +163,24 @@ hipError_t launch_assign_group(int vb, bool vec, int unroll, bool nt, bool ntp, 
                                const GroupArgs& ga,
                                const DenseView& d, uint32_t tile_shift, uint64_t ntiles,
                                uint32_t grid, uint32_t* flag, uint32_t epoch, hipStream_t st);
+// K4a: in-range keys only; an out-of-range key tags *oor with `epoch` for the
+// oor_only replay behind K4.
 hipError_t launch_general_mark(int dtype, int mode, const GroupArgs& ga, uint32_t nwg,
-                               const DenseView& d, const Ovf& o, unsigned long long* owner,
+                               const DenseView& d, uint32_t* oor, unsigned long long* owner,
                                const uint32_t* cond, uint32_t epoch, hipStream_t st);
 hipError_t launch_general_commit(int vb, const GroupArgs& ga, uint32_t nwg, const DenseView& d,
-                                 const Ovf& o, const unsigned long long* owner,
+                                 const unsigned long long* owner,
                                  const uint32_t* cond, uint32_t epoch, hipStream_t st);
-hipError_t launch_ovf_rehash(int vb, const Ovf& from, uint64_t from_cap, const Ovf& to,
-                             hipStream_t st);
+// Host growth of the table (pskv_sync keeps its load <= 1/2): rehash the
+// current table (from_cap slots) into `to` (keys EMPTY, values 0), then
+// switch the control block over.
+hipError_t launch_ovf_rehash(int vb, const Ovf& o, uint64_t from_cap, const OvfTab& to, hipStream_t st);
 // K4r: conditional replay of a group in call order by ONE workgroup (runs only
 // when *cond == epoch: a sorted-path hint was broken); assign or accumulate.
+// oor_only: only the group's out-of-range keys (behind K4, which leaves them
+// to this single workgroup, the only kind of inserter that can grow the table).
 hipError_t launch_replay(int dtype, int mode, const GroupArgs& ga, const DenseView& d, const Ovf& o,
-                         const uint32_t* cond, uint32_t epoch, hipStream_t st);
+                         const uint32_t* cond, uint32_t epoch, hipStream_t st, bool oor_only = false);
 // K1r: K1 with an assign group's conditional replay folded in (the launch K4r
 // would cost): when *cond == epoch, workgroup 0 replays `rg` and then gathers
 // every chunk of `ga` itself while the other workgroups leave; otherwise K1.

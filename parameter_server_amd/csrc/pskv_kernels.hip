@@ -185,42 +185,200 @@ __device__ __forceinline__ int batch_of(const GroupArgs& ga, uint32_t wg) {
 // uint32 key is storable).  Keys are never deleted, so a non-EMPTY slot read
 // without an atomic is final; a stale EMPTY is resolved by the CAS.
 
-__device__ __forceinline__ long long ovf_find(const Ovf& o, uint32_t key) {
-  uint64_t h = fmix32(key) & o.mask;
-  for (uint64_t p = 0; p <= o.mask; ++p) {
-    const unsigned long long k = o.keys[h];
+template <typename T>
+__device__ __forceinline__ T sys_load(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <typename T>
+__device__ __forceinline__ T agent_load(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// (readfirstlane returns int: each half goes through uint32_t, or a low word
+// with its top bit set would sign-extend over the high word)
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
+// The table's current arrays, read from the control block (wave-uniform: kept
+// in scalar registers).  FRESH: agent-scope loads, for a kernel in which a
+// workgroup may have grown the table and switched the block over (the replays
+// K4r / K1r, K5b, K8, K9): they reach L2 past any line an earlier read left
+// in the CU.  Otherwise plain loads (the caches start clean at every launch).
+template <bool FRESH = true>
+__device__ __forceinline__ OvfTab ovf_tab(const Ovf& o) {
+  OvfTab t;
+  if (FRESH) {
+    t.keys = reinterpret_cast<unsigned long long*>(
+        uniform64(agent_load(reinterpret_cast<const uint64_t*>(&o.c->t.keys))));
+    t.vals = reinterpret_cast<void*>(uniform64(agent_load(reinterpret_cast<const uint64_t*>(&o.c->t.vals))));
+    t.mask = uniform64(agent_load(&o.c->t.mask));
+  } else {
+    t = o.c->t;
+  }
+  return t;
+}
+
+__device__ __forceinline__ long long ovf_find(const OvfTab& t, uint32_t key) {
+  uint64_t h = fmix32(key) & t.mask;
+  for (uint64_t p = 0; p <= t.mask; ++p) {
+    const unsigned long long k = t.keys[h];
     if (k == (unsigned long long)key) return (long long)h;
     if (k == kEmpty64) return -1;
-    h = (h + 1) & o.mask;
+    h = (h + 1) & t.mask;
   }
   return -1;
 }
 
-__device__ long long ovf_insert(const Ovf& o, uint32_t key) {
-  uint64_t h = fmix32(key) & o.mask;
-  for (uint64_t p = 0; p <= o.mask; ++p) {
-    const unsigned long long k = o.keys[h];
+// Insert (or find) `key`; counts a new key in stat[0].  A full table sets the
+// sticky error bit: only a caller that skipped ovf_reserve can get there (the
+// grow service did not answer within the wait bound, or its allocation failed).
+__device__ long long ovf_insert(const OvfTab& t, uint32_t* stat, uint32_t key) {
+  uint64_t h = fmix32(key) & t.mask;
+  for (uint64_t p = 0; p <= t.mask; ++p) {
+    const unsigned long long k = t.keys[h];
     if (k == (unsigned long long)key) return (long long)h;
     if (k == kEmpty64) {
-      const unsigned long long old = atomicCAS(&o.keys[h], kEmpty64, (unsigned long long)key);
+      const unsigned long long old = atomicCAS(&t.keys[h], kEmpty64, (unsigned long long)key);
       if (old == kEmpty64) {
-        atomicAdd(&o.stat[0], 1u);
+        atomicAdd(&stat[0], 1u);
         return (long long)h;
       }
       if (old == (unsigned long long)key) return (long long)h;
     }
-    h = (h + 1) & o.mask;
+    h = (h + 1) & t.mask;
   }
-  atomicOr(&o.stat[1], kErrOverflowFull);
+  atomicOr(&stat[1], kErrOverflowFull);
   return -1;
 }
+__device__ __forceinline__ long long ovf_insert(const Ovf& o, const OvfTab& t, uint32_t key) {
+  return ovf_insert(t, o.c->stat, key);
+}
 
-template <typename VT>
+// A key's slot in a table being filled by a rehash (room for every key, keys
+// distinct): no count, no error.
+__device__ __forceinline__ long long ovf_place(const OvfTab& t, uint32_t key) {
+  uint64_t h = fmix32(key) & t.mask;
+  for (;;) {
+    const unsigned long long old = atomicCAS(&t.keys[h], kEmpty64, (unsigned long long)key);
+    if (old == kEmpty64 || old == (unsigned long long)key) return (long long)h;
+    h = (h + 1) & t.mask;
+  }
+}
+
+// VB value bytes of slot i, copied (agent-scope loads: the values were stored
+// by this workgroup earlier in the kernel, possibly behind a stale CU line).
+template <int VB>
+__device__ __forceinline__ void ovf_copy_val(const OvfTab& from, uint64_t i, const OvfTab& to, long long s) {
+  if (VB == 8)
+    reinterpret_cast<unsigned long long*>(to.vals)[s] =
+        agent_load(reinterpret_cast<const unsigned long long*>(from.vals) + i);
+  else
+    reinterpret_cast<uint32_t*>(to.vals)[s] = agent_load(reinterpret_cast<const uint32_t*>(from.vals) + i);
+}
+
+// ---- growth on the device (round 6).  The reference's last range server
+// stores every key the slicer cannot place, however many
+// (range_partition_manager.hpp:26-27, map_storage.hpp:22-23).  A device-side
+// Add's keys are never read on the host, so the table cannot be sized before
+// the kernels run; instead every out-of-range insert happens in ONE workgroup
+// (the replays K4r / K1r, the out-of-range bucket of K5b, K8, K9), which
+// reserves room before each pass: when the pass could lift the load above 3/4,
+// thread 0 posts a request to the shard's mailbox (coherent host memory) and
+// polls for the answer; the library's grow service (a host thread) allocates
+// arrays of the asked size and answers; the workgroup fills them, rehashes the
+// table into them, switches the control block over and goes on.  Later
+// kernels read the block, so work queued before the growth uses the new table.
+// The wait is bounded (mailbox wait_ticks, from SYNC_TIMEOUT_MS): without an
+// answer the workgroup goes on with the old table, and an insert that finds it
+// full sets the sticky error (pskv_sync: PSKV_ESTATE), as before round 6.
+
+// Thread 0: ask the grow service for `cap` slots; true with the new arrays in *out.
+__device__ bool ovf_request(OvfMbox* m, uint64_t cap, OvfTab* out) {
+  if (m == nullptr) return false;
+  const uint32_t seq = sys_load(&m->req_seq) + 1u;
+  __hip_atomic_store(&m->req_cap, cap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&m->req_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  const unsigned long long t0 = wall_clock64(), lim = sys_load(&m->wait_ticks);
+  for (;;) {
+    if (__hip_atomic_load(&m->resp_seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == seq) break;
+    if (wall_clock64() - t0 > lim) return false;
+    __builtin_amdgcn_s_sleep(16);
+  }
+  if (sys_load(&m->resp_ok) == 0u) return false;
+  out->keys = reinterpret_cast<unsigned long long*>(sys_load(reinterpret_cast<const uint64_t*>(&m->resp_tab.keys)));
+  out->vals = reinterpret_cast<void*>(sys_load(reinterpret_cast<const uint64_t*>(&m->resp_tab.vals)));
+  out->mask = sys_load(&m->resp_tab.mask);
+  return out->keys != nullptr && out->vals != nullptr && out->mask + 1 == cap;
+}
+
+// Every thread of the workgroup, uniformly: make room for `extra` more keys
+// (load <= 3/4 after them), growing the table if needed.  Orders every earlier
+// insert of the workgroup before it (barrier).  VB: value bytes.
+template <int VB>
+__device__ void ovf_reserve(const Ovf& o, uint64_t extra) {
+  __shared__ OvfTab s_new;
+  __shared__ uint32_t s_go;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t go = 0;
+    const OvfTab t = ovf_tab(o);
+    const uint64_t cap = t.mask + 1;
+    const uint64_t cnt = agent_load(&o.c->stat[0]);
+    if (4 * (cnt + extra) > 3 * cap) {
+      uint64_t want = 2 * cap;
+      while (want < 2 * (cnt + extra)) want <<= 1;
+      OvfTab n;
+      if (ovf_request(o.c->mbox, want, &n)) {
+        s_new = n;
+        go = 1;
+      }
+    }
+    s_go = go;
+  }
+  __syncthreads();
+  if (!s_go) return;  // uniform
+  const OvfTab from = ovf_tab(o);
+  OvfTab to;  // (scalar registers: the caller's live values keep the vector ones)
+  to.keys = reinterpret_cast<unsigned long long*>(uniform64(reinterpret_cast<uint64_t>(s_new.keys)));
+  to.vals = reinterpret_cast<void*>(uniform64(reinterpret_cast<uint64_t>(s_new.vals)));
+  to.mask = uniform64(s_new.mask);
+  for (uint64_t i = threadIdx.x; i <= to.mask; i += blockDim.x) {
+    to.keys[i] = kEmpty64;
+    if (VB == 8)
+      reinterpret_cast<unsigned long long*>(to.vals)[i] = 0ull;
+    else
+      reinterpret_cast<uint32_t*>(to.vals)[i] = 0u;
+  }
+  __threadfence();
+  __syncthreads();
+  for (uint64_t i = threadIdx.x; i <= from.mask; i += blockDim.x) {
+    const unsigned long long k = agent_load(from.keys + i);
+    if (k == kEmpty64) continue;
+    ovf_copy_val<VB>(from, i, to, ovf_place(to, (uint32_t)k));
+  }
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(&o.c->t.keys), reinterpret_cast<uint64_t>(to.keys),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(&o.c->t.vals), reinterpret_cast<uint64_t>(to.vals),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&o.c->t.mask, to.mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __threadfence();
+  __syncthreads();
+}
+
+template <typename VT, bool FRESH = false>
 __device__ __forceinline__ VT load_one(const DenseView& d, const Ovf& o, uint32_t key) {
   const uint32_t off = key - d.key_begin;
   if ((uint64_t)off < d.range) return reinterpret_cast<const VT*>(d.param)[off];
-  const long long s = ovf_find(o, key);
-  return s >= 0 ? reinterpret_cast<const VT*>(o.vals)[s] : VT(0);
+  const OvfTab t = ovf_tab<FRESH>(o);
+  const long long s = ovf_find(t, key);
+  return s >= 0 ? reinterpret_cast<const VT*>(t.vals)[s] : VT(0);
 }
 
 // An empty asm that reads x: the compiler's wait-count pass must have x's loads
@@ -254,7 +412,7 @@ __device__ unsigned long long g_step_stamps[2][8192][4];
 // key; cfg 4's producer windows do); otherwise four scalar gathers.  (Round 3
 // loaded the two slots such a run straddles and selected: K1 ran 4-6 % slower
 // at phases 1-3 than at phase 0, `profiles/r03_probes/align_probe_own_range.log`.)
-template <typename VT, bool NTP = false>
+template <typename VT, bool NTP = false, bool FRESH = false>
 __device__ __forceinline__ void gather4(const DenseView& d, const Ovf& o, const uint32_t (&k)[4],
                                         VT (&v)[4]) {
   const uint32_t off0 = k[0] - d.key_begin;
@@ -269,12 +427,13 @@ __device__ __forceinline__ void gather4(const DenseView& d, const Ovf& o, const 
     for (int e = 0; e < 4; ++e) v[e] = (VT)t[e];
   } else {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = load_one<VT>(d, o, k[e]);
+    for (int e = 0; e < 4; ++e) v[e] = load_one<VT, FRESH>(d, o, k[e]);
   }
 }
 
 // Two keys of one lane, 8-byte values: one 16-byte load when they are two
 // consecutive in-range keys, from a dword-aligned address on an odd offset.
+template <bool FRESH = false>
 __device__ __forceinline__ void gather2(const DenseView& d, const Ovf& o, const uint32_t (&k)[2],
                                         unsigned long long (&v)[2]) {
   using T = unsigned long long;
@@ -288,8 +447,8 @@ __device__ __forceinline__ void gather2(const DenseView& d, const Ovf& o, const 
     v[0] = (T)t[0] | ((T)t[1] << 32);
     v[1] = (T)t[2] | ((T)t[3] << 32);
   } else {
-    v[0] = load_one<T>(d, o, k[0]);
-    v[1] = load_one<T>(d, o, k[1]);
+    v[0] = load_one<T, FRESH>(d, o, k[0]);
+    v[1] = load_one<T, FRESH>(d, o, k[1]);
   }
 }
 
@@ -300,7 +459,7 @@ __device__ __forceinline__ void gather2(const DenseView& d, const Ovf& o, const 
 struct GoAlways {
   __device__ bool operator()() const { return true; }
 };
-template <typename VT, bool VEC, int U, bool NT, typename Go = GoAlways>
+template <typename VT, bool VEC, int U, bool NT, typename Go = GoAlways, bool FRESH = false>
 __device__ __forceinline__ void gather_chunk(const GroupArgs& ga, const DenseView& d, const Ovf& o,
                                              uint32_t wg, Go go = Go()) {
   constexpr int CH = kBlock * 4 * U;
@@ -323,7 +482,7 @@ __device__ __forceinline__ void gather_chunk(const GroupArgs& ga, const DenseVie
       if (!go()) return;
       VT v[UU][2];
 #pragma unroll
-      for (int u = 0; u < UU; ++u) gather2(d, o, k[u], v[u]);
+      for (int u = 0; u < UU; ++u) gather2<FRESH>(d, o, k[u], v[u]);
 #pragma unroll
       for (int u = 0; u < UU; ++u) Vec2x8::store<NT>(out + base + (uint64_t)(u * kBlock + tid) * 2, v[u]);
       return;
@@ -342,7 +501,7 @@ __device__ __forceinline__ void gather_chunk(const GroupArgs& ga, const DenseVie
 #endif
     VT v[U][4];
 #pragma unroll
-    for (int u = 0; u < U; ++u) gather4<VT>(d, o, k[u], v[u]);
+    for (int u = 0; u < U; ++u) gather4<VT, false, FRESH>(d, o, k[u], v[u]);
 #pragma unroll
     for (int u = 0; u < U; ++u)
       Vec4<VT>::template store<NT>(out + base + (uint64_t)(u * kBlock + tid) * 4, v[u]);
@@ -363,7 +522,8 @@ __device__ __forceinline__ void gather_chunk(const GroupArgs& ga, const DenseVie
         kk[q] = i < end ? keys[i] : 0u;
       }
 #pragma unroll
-      for (int q = 0; q < 8; ++q) vv[q] = i0 + (uint64_t)q * kBlock < end ? load_one<VT>(d, o, kk[q]) : VT(0);
+      for (int q = 0; q < 8; ++q)
+        vv[q] = i0 + (uint64_t)q * kBlock < end ? load_one<VT, FRESH>(d, o, kk[q]) : VT(0);
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const uint64_t i = i0 + (uint64_t)q * kBlock;
@@ -960,32 +1120,33 @@ __device__ __forceinline__ void lds_add(T* p, T v) {
 // element per key, the last one in call order.  The stamp array is never reset:
 // epochs increase, so an old stamp always loses.
 
+// Out-of-range keys are not K4's: many workgroups insert at once here, and
+// only a single workgroup can grow the table mid-kernel, so K4a tags `oor`
+// and the oor_only replay behind K4 applies those keys in call order (assign:
+// last wins; accumulate: sums), with room reserved as it goes.  Dense and
+// overflow keys are disjoint, so the split changes no result.
 template <typename AT>
-__device__ __forceinline__ void global_accumulate(const DenseView& d, const Ovf& o, uint32_t k,
-                                                  AT v) {
+__device__ __forceinline__ void global_accumulate(const DenseView& d, uint32_t* oor, uint32_t epoch,
+                                                  uint32_t k, AT v) {
   const uint32_t off = k - d.key_begin;
-  if ((uint64_t)off < d.range) {
+  if ((uint64_t)off < d.range)
     atomicAdd(reinterpret_cast<AT*>(d.param) + off, v);
-  } else {
-    const long long s = ovf_insert(o, k);
-    if (s >= 0) atomicAdd(reinterpret_cast<AT*>(o.vals) + s, v);
-  }
+  else
+    __hip_atomic_store(oor, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ void global_stamp(const DenseView& d, const Ovf& o,
+__device__ __forceinline__ void global_stamp(const DenseView& d, uint32_t* oor, uint32_t epoch,
                                              unsigned long long* owner, uint32_t k,
                                              unsigned long long tag) {
   const uint32_t off = k - d.key_begin;
-  if ((uint64_t)off < d.range) {
+  if ((uint64_t)off < d.range)
     atomicMax(owner + off, tag);
-  } else {
-    const long long s = ovf_insert(o, k);
-    if (s >= 0) atomicMax(o.owner + s, tag);
-  }
+  else
+    __hip_atomic_store(oor, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <typename AT, int MODE>
-__global__ __launch_bounds__(kBlock) void k_general_mark(GroupArgs ga, DenseView d, Ovf o,
+__global__ __launch_bounds__(kBlock) void k_general_mark(GroupArgs ga, DenseView d, uint32_t* oor,
                                                          unsigned long long* owner,
                                                          const uint32_t* cond, uint32_t epoch) {
   if (cond != nullptr && *cond != epoch) return;  // repair launch, sorted path was right
@@ -1026,9 +1187,9 @@ __global__ __launch_bounds__(kBlock) void k_general_mark(GroupArgs ga, DenseView
         key[r] = k;
         if (k == kEmpty32) {  // the LDS sentinel itself: bypass the LDS table
           if (MODE == 0)
-            global_stamp(d, o, owner, k, ((unsigned long long)epoch << 32) | (gbase + li));
+            global_stamp(d, oor, epoch, owner, k, ((unsigned long long)epoch << 32) | (gbase + li));
           else
-            global_accumulate<AT>(d, o, k, vals[i]);
+            global_accumulate<AT>(d, oor, epoch, k, vals[i]);
         } else {
           uint32_t h = fmix32(k) & (kGeneralSlots - 1);
           for (;;) {
@@ -1054,16 +1215,16 @@ __global__ __launch_bounds__(kBlock) void k_general_mark(GroupArgs ga, DenseView
       const uint32_t h = slot[r];
       if (h == kEmpty32 || hfirst[h] != (uint32_t)(r * kBlock + tid)) continue;
       if (MODE == 0)
-        global_stamp(d, o, owner, key[r], ((unsigned long long)epoch << 32) | (gbase + hidx[h]));
+        global_stamp(d, oor, epoch, owner, key[r], ((unsigned long long)epoch << 32) | (gbase + hidx[h]));
       else
-        global_accumulate<AT>(d, o, key[r], hsum[h]);
+        global_accumulate<AT>(d, oor, epoch, key[r], hsum[h]);
     }
     __syncthreads();  // the table is re-initialised for the next chunk
   }
 }
 
 template <typename VT>
-__global__ __launch_bounds__(kBlock) void k_general_commit(GroupArgs ga, DenseView d, Ovf o,
+__global__ __launch_bounds__(kBlock) void k_general_commit(GroupArgs ga, DenseView d,
                                                            const unsigned long long* owner,
                                                            const uint32_t* cond, uint32_t epoch) {
   if (cond != nullptr && *cond != epoch) return;
@@ -1084,25 +1245,27 @@ __global__ __launch_bounds__(kBlock) void k_general_commit(GroupArgs ga, DenseVi
       const uint32_t k = keys[i];
       const unsigned long long tag = ((unsigned long long)epoch << 32) | (gbase + li);
       const uint32_t off = k - d.key_begin;
-      if ((uint64_t)off < d.range) {
-        if (owner[off] == tag) reinterpret_cast<VT*>(d.param)[off] = vals[i];
-      } else {
-        const long long s = ovf_find(o, k);
-        if (s >= 0 && o.owner[s] == tag) reinterpret_cast<VT*>(o.vals)[s] = vals[i];
-      }
+      if ((uint64_t)off < d.range && owner[off] == tag) reinterpret_cast<VT*>(d.param)[off] = vals[i];
+      // (out-of-range keys: the oor_only replay behind K4)
     }
   }
 }
 
+// Host growth (pskv_sync): the table in the control block, rehashed into `to`
+// (keys EMPTY, values 0, room for every key); then k_ovf_set switches over.
 template <typename VT>
-__global__ __launch_bounds__(kBlock) void k_ovf_rehash(Ovf from, uint64_t from_cap, Ovf to) {
-  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < from_cap;
+__global__ __launch_bounds__(kBlock) void k_ovf_rehash(Ovf o, uint64_t from_cap, OvfTab to) {
+  const OvfTab from = ovf_tab(o);
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < from_cap && i <= from.mask;
        i += (uint64_t)gridDim.x * kBlock) {
     const unsigned long long k = from.keys[i];
     if (k == kEmpty64) continue;
-    const long long s = ovf_insert(to, (uint32_t)k);
-    if (s >= 0) reinterpret_cast<VT*>(to.vals)[s] = reinterpret_cast<const VT*>(from.vals)[i];
+    reinterpret_cast<VT*>(to.vals)[ovf_place(to, (uint32_t)k)] = reinterpret_cast<const VT*>(from.vals)[i];
   }
+}
+
+__global__ void k_ovf_set(Ovf o, OvfTab to) {
+  if (threadIdx.x == 0) o.c->t = to;
 }
 
 // ------------------------------------------- K5 key-bucket general path
@@ -1647,13 +1810,16 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
     }
     return lo;
   };
+  // the overflow table, loaded (after the room for it is reserved) when this
+  // workgroup takes the out-of-range bucket
+  OvfTab ot{};
   auto store_winner = [&](uint32_t b, uint32_t key, BT vbits) {
     const AT v = from_bits<AT>(to_bits<BT>(vbits));
     if (b != nbd) {
       reinterpret_cast<AT*>(d.param)[key - d.key_begin] = v;
     } else {
-      const long long sl = ovf_insert(o, key);
-      if (sl >= 0) reinterpret_cast<AT*>(o.vals)[sl] = v;
+      const long long sl = ovf_insert(o, ot, key);
+      if (sl >= 0) reinterpret_cast<AT*>(ot.vals)[sl] = v;
     }
   };
   auto accumulate_all = [&](uint32_t b) {
@@ -1687,9 +1853,9 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
       const bool used = s == SLOTS ? sent != 0 : ak[s] != kEmpty32;
       if (!used) continue;
       const uint32_t key = s == SLOTS ? kEmpty32 : ak[s];
-      const long long sl = ovf_insert(o, key);
+      const long long sl = ovf_insert(o, ot, key);
       if (sl < 0) continue;
-      AT* p = reinterpret_cast<AT*>(o.vals) + sl;
+      AT* p = reinterpret_cast<AT*>(ot.vals) + sl;
       *p = add_wrap<AT>(*p, asum[s]);
     }
   };
@@ -1813,6 +1979,10 @@ __global__ __launch_bounds__(kApplyBlock) void k_rb_resolve(DenseView d, Ovf o, 
       s_max[z] = 0;
     }
     if (ne == 0) continue;  // uniform
+    if (b == nbd) {  // uniform: the out-of-range bucket, at most ne new keys
+      ovf_reserve<sizeof(AT)>(o, ne);
+      ot = ovf_tab(o);
+    }
     const bool direct = MODE == 0 && b != nbd && !long_run && halves <= 4;
     if (direct) {
       uint32_t rel[RPT];
@@ -1972,13 +2142,35 @@ template <int BLOCK>
 constexpr int replay_slots() {
   return 8 * BLOCK;
 }
-template <typename VT, int MODE, int BLOCK = kReplayBlock, typename G = GroupArgs>
+template <typename VT, int MODE, int BLOCK = kReplayBlock, typename G = GroupArgs, bool OOR_ONLY = false>
 __device__ __forceinline__ void replay_group(const G& ga, const DenseView& d, const Ovf& o, uint32_t* hk,
                                              uint32_t* hidx, VT* hsum, uint32_t* sent_p) {
   constexpr int CHUNK = 4 * BLOCK, SLOTS = replay_slots<BLOCK>();
   constexpr int PER = CHUNK / BLOCK;
   uint32_t& sent = *sent_p;
   const int tid = threadIdx.x;
+  // Room in the overflow table for the group's out-of-range keys, reserved once
+  // before the passes: a read of the group's keys counts their occurrences (a
+  // bound on the new keys; the replay runs at ~1 GB/s, the count is noise),
+  // summed in the sentinel word, which the first pass then clears.  (Once, not
+  // per pass: the reservation then holds no pass state live, and K1r keeps
+  // its register count.)
+  {
+    uint32_t c = 0;
+    for (int j = 0; j < ga.nb; ++j)
+      for (uint64_t i = (uint64_t)tid; i < ga.b[j].n; i += BLOCK)
+        c += (uint64_t)(uint32_t)(ga.b[j].keys[i] - d.key_begin) >= d.range ? 1u : 0u;
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) c += (uint32_t)__shfl_xor((int)c, w, 64);
+    if (tid == 0) __hip_atomic_store(&sent, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if ((tid & 63) == 0 && c != 0u) atomicAdd(&sent, c);
+    __syncthreads();
+    const uint32_t total = __hip_atomic_load(&sent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();  // every wave has read it before the first pass clears the word
+    if (total != 0u) ovf_reserve<sizeof(VT)>(o, total);  // uniform
+  }
+  const OvfTab ot = ovf_tab(o);
   for (int j = 0; j < ga.nb; ++j) {
     const uint32_t* __restrict__ keys = ga.b[j].keys;
     const VT* __restrict__ vals = reinterpret_cast<const VT*>(ga.b[j].vals);
@@ -2005,9 +2197,11 @@ __device__ __forceinline__ void replay_group(const G& ga, const DenseView& d, co
       for (int q = 0; q < PER; ++q) {
         const uint64_t i = base + (uint64_t)(q * BLOCK + tid);
         const bool in = i < n;
-        valid |= in ? (1u << q) : 0u;
         key[q] = in ? keys[i] : 0u;
-        v[q] = in ? vals[i] : VT(0);
+        // OOR_ONLY (behind K4): only the out-of-range keys; K4 applied the rest
+        const bool take = in && (!OOR_ONLY || (uint64_t)(uint32_t)(key[q] - d.key_begin) >= d.range);
+        valid |= take ? (1u << q) : 0u;
+        v[q] = take ? vals[i] : VT(0);
       }
       const uint32_t own = lds_insert<PER, SLOTS>(hk, &sent, key, valid, slot);
 #pragma unroll
@@ -2033,8 +2227,8 @@ __device__ __forceinline__ void replay_group(const G& ga, const DenseView& d, co
           if ((uint64_t)off < d.range) {
             reinterpret_cast<VT*>(d.param)[off] = v[q];
           } else {
-            const long long sl = ovf_insert(o, key[q]);
-            if (sl >= 0) reinterpret_cast<VT*>(o.vals)[sl] = v[q];
+            const long long sl = ovf_insert(o, ot, key[q]);
+            if (sl >= 0) reinterpret_cast<VT*>(ot.vals)[sl] = v[q];
           }
         } else {
           if (!(own >> q & 1u)) continue;  // the key's inserting lane adds the pass's sum
@@ -2042,8 +2236,8 @@ __device__ __forceinline__ void replay_group(const G& ga, const DenseView& d, co
           if ((uint64_t)off < d.range) {
             p = reinterpret_cast<VT*>(d.param) + off;
           } else {
-            const long long sl = ovf_insert(o, key[q]);
-            if (sl >= 0) p = reinterpret_cast<VT*>(o.vals) + sl;
+            const long long sl = ovf_insert(o, ot, key[q]);
+            if (sl >= 0) p = reinterpret_cast<VT*>(ot.vals) + sl;
           }
           if (p) *p = add_wrap<VT>(*p, hsum[slot[q]]);
         }
@@ -2053,7 +2247,7 @@ __device__ __forceinline__ void replay_group(const G& ga, const DenseView& d, co
   }
 }
 
-template <typename VT, int MODE>
+template <typename VT, int MODE, bool OOR_ONLY>
 __global__ __launch_bounds__(kReplayBlock) void k_replay(GroupArgs ga, DenseView d, Ovf o,
                                                          const uint32_t* cond, uint32_t epoch) {
   constexpr int SLOTS = replay_slots<kReplayBlock>();
@@ -2061,8 +2255,8 @@ __global__ __launch_bounds__(kReplayBlock) void k_replay(GroupArgs ga, DenseView
   __shared__ uint32_t hidx[MODE == 0 ? SLOTS + 1 : 1];
   __shared__ VT hsum[MODE == 1 ? SLOTS + 1 : 1];
   __shared__ uint32_t sent;
-  if (*cond != epoch) return;  // the hint held (the usual case)
-  replay_group<VT, MODE>(ga, d, o, hk, hidx, hsum, &sent);
+  if (*cond != epoch) return;  // the hint held / no out-of-range key (the usual case)
+  replay_group<VT, MODE, kReplayBlock, GroupArgs, OOR_ONLY>(ga, d, o, hk, hidx, hsum, &sent);
 }
 
 // K1r: K1 carrying the conditional replay of the assign group just before it
@@ -2091,7 +2285,8 @@ __global__ __launch_bounds__(kBlock) void k_gather_r(GroupArgs ga, DenseView d, 
     static_assert(2 * SLOTS + 2 <= (int)kK1rTableWords, "K1r's replay table fits its scratch");
     replay_group<VT, 0, kBlock>(rg, d, o, tab, tab + SLOTS, static_cast<VT*>(nullptr), tab + 2 * SLOTS + 1);
     // (ends with a barrier: its stores precede the loads below)
-    for (uint32_t w = 0; w < gridDim.x; ++w) gather_chunk<VT, VEC, U, NT>(ga, d, o, w);
+    // (FRESH: the replay may have grown the overflow table in this kernel)
+    for (uint32_t w = 0; w < gridDim.x; ++w) gather_chunk<VT, VEC, U, NT, GoAlways, true>(ga, d, o, w);
   }
 }
 
@@ -2307,32 +2502,40 @@ __global__ __launch_bounds__(kInlineMax) void k_inline_add(InlineAdd a, DenseVie
   const int n = (int)a.n;
   const uint32_t k = tid < n ? a.keys[tid] : 0u;
   using BT = typename std::conditional<sizeof(VT) == 8, unsigned long long, uint32_t>::type;
+  const uint32_t off = k - d.key_begin;
+  // room for the message's new out-of-range keys first (every thread: the
+  // reservation is a workgroup step)
+  const bool outside = tid < n && (uint64_t)off >= d.range;
+  const int n_out = __syncthreads_count(outside);
+  OvfTab ot{};
+  if (n_out) {
+    ovf_reserve<sizeof(VT)>(o, (uint64_t)n_out);
+    ot = ovf_tab(o);
+  }
   if (MODE == 0) {
     bool later = false;
 #pragma unroll 16
     for (int j = 0; j < n; ++j) later |= (j > tid) & (a.keys[j] == k);
     if (tid >= n || later) return;  // a later occurrence wins
     const BT v = (BT)a.vals[tid];
-    const uint32_t off = k - d.key_begin;
-    if ((uint64_t)off < d.range) {
+    if (!outside) {
       reinterpret_cast<BT*>(d.param)[off] = v;
     } else {
-      const long long slot = ovf_insert(o, k);
-      if (slot >= 0) reinterpret_cast<BT*>(o.vals)[slot] = v;
+      const long long slot = ovf_insert(o, ot, k);
+      if (slot >= 0) reinterpret_cast<BT*>(ot.vals)[slot] = v;
     }
   } else {
     bool earlier = false;
 #pragma unroll 16
     for (int j = 0; j < n; ++j) earlier |= (j < tid) & (a.keys[j] == k);
     if (tid >= n || earlier) return;  // the first occurrence sums them all
-    const uint32_t off = k - d.key_begin;
     VT* p;
-    if ((uint64_t)off < d.range) {
+    if (!outside) {
       p = reinterpret_cast<VT*>(d.param) + off;
     } else {
-      const long long slot = ovf_insert(o, k);
+      const long long slot = ovf_insert(o, ot, k);
       if (slot < 0) return;
-      p = reinterpret_cast<VT*>(o.vals) + slot;
+      p = reinterpret_cast<VT*>(ot.vals) + slot;
     }
     VT acc = *p;
 #pragma unroll 16
@@ -2392,11 +2595,6 @@ __global__ __launch_bounds__(64) void k_inline_get(InlineGet a, DenseView d, Ovf
 // thread-group-split mode a CU's vector memory operations reach L2 in order,
 // so workgroup-scope ordering needs no vmcnt wait — checked in the ISA.)
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-template <typename T>
-__device__ __forceinline__ T sys_load(const T* p) {
-  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 
 template <typename VT, int MODE>
 __global__ __launch_bounds__(kInlineMax) void k_serve(SrvRing* ring, DenseView d, Ovf o,
@@ -2505,6 +2703,13 @@ __global__ __launch_bounds__(kInlineMax) void k_serve(SrvRing* ring, DenseView d
         }
       }
       __syncthreads();
+      // room for the request's new out-of-range keys (a workgroup step)
+      const int n_out = __syncthreads_count(tid < n && (uint64_t)(uint32_t)(s_keys[tid] - d.key_begin) >= d.range);
+      OvfTab ot{};
+      if (n_out) {
+        ovf_reserve<sizeof(VT)>(o, (uint64_t)n_out);
+        ot = ovf_tab(o);
+      }
       if (tid < n) {
         const uint32_t k = s_keys[tid];
         const uint32_t off = k - d.key_begin;
@@ -2514,8 +2719,8 @@ __global__ __launch_bounds__(kInlineMax) void k_serve(SrvRing* ring, DenseView d
             if ((uint64_t)off < d.range) {
               reinterpret_cast<BT*>(d.param)[off] = v;
             } else {
-              const long long slot = ovf_insert(o, k);
-              if (slot >= 0) reinterpret_cast<BT*>(o.vals)[slot] = v;
+              const long long slot = ovf_insert(o, ot, k);
+              if (slot >= 0) reinterpret_cast<BT*>(ot.vals)[slot] = v;
             }
           }
         } else {
@@ -2530,8 +2735,8 @@ __global__ __launch_bounds__(kInlineMax) void k_serve(SrvRing* ring, DenseView d
             if ((uint64_t)off < d.range) {
               p = reinterpret_cast<VT*>(d.param) + off;
             } else {
-              const long long slot = ovf_insert(o, k);
-              if (slot >= 0) p = reinterpret_cast<VT*>(o.vals) + slot;
+              const long long slot = ovf_insert(o, ot, k);
+              if (slot >= 0) p = reinterpret_cast<VT*>(ot.vals) + slot;
             }
             if (p) {
               VT acc = *p;
@@ -2551,7 +2756,7 @@ __global__ __launch_bounds__(kInlineMax) void k_serve(SrvRing* ring, DenseView d
 #pragma unroll
       for (int q = 0; q < PER; ++q) {
         const int i = tid + kInlineMax * q;
-        v[q] = i < n ? load_one<BT>(d, o, s_keys[i]) : BT(0);
+        v[q] = i < n ? load_one<BT, true>(d, o, s_keys[i]) : BT(0);
       }
       BT* out = static_cast<BT*>(reply) + roff;
 #pragma unroll
@@ -2747,63 +2952,73 @@ static uint32_t general_grid(uint32_t nwg, const uint32_t* cond) {
 }
 
 hipError_t launch_general_mark(int dtype, int mode, const GroupArgs& ga, uint32_t nwg,
-                               const DenseView& d, const Ovf& o, unsigned long long* owner,
+                               const DenseView& d, uint32_t* oor, unsigned long long* owner,
                                const uint32_t* cond, uint32_t epoch, hipStream_t st) {
   if (nwg == 0) return hipSuccess;
   nwg = general_grid(nwg, cond);
   if (mode == 0) {
     // assign: value bits are never read here; the AT parameter only sizes unused LDS
-    k_general_mark<uint32_t, 0><<<nwg, kBlock, 0, st>>>(ga, d, o, owner, cond, epoch);
+    k_general_mark<uint32_t, 0><<<nwg, kBlock, 0, st>>>(ga, d, oor, owner, cond, epoch);
   } else if (dtype == 0) {
-    k_general_mark<int, 1><<<nwg, kBlock, 0, st>>>(ga, d, o, owner, cond, epoch);
+    k_general_mark<int, 1><<<nwg, kBlock, 0, st>>>(ga, d, oor, owner, cond, epoch);
   } else if (dtype == 1) {
-    k_general_mark<float, 1><<<nwg, kBlock, 0, st>>>(ga, d, o, owner, cond, epoch);
+    k_general_mark<float, 1><<<nwg, kBlock, 0, st>>>(ga, d, oor, owner, cond, epoch);
   } else {
-    k_general_mark<double, 1><<<nwg, kBlock, 0, st>>>(ga, d, o, owner, cond, epoch);
+    k_general_mark<double, 1><<<nwg, kBlock, 0, st>>>(ga, d, oor, owner, cond, epoch);
   }
   return hipGetLastError();
 }
 
 hipError_t launch_general_commit(int vb, const GroupArgs& ga, uint32_t nwg, const DenseView& d,
-                                 const Ovf& o, const unsigned long long* owner,
+                                 const unsigned long long* owner,
                                  const uint32_t* cond, uint32_t epoch, hipStream_t st) {
   if (nwg == 0) return hipSuccess;
   nwg = general_grid(nwg, cond);
   if (vb == 4)
-    k_general_commit<uint32_t><<<nwg, kBlock, 0, st>>>(ga, d, o, owner, cond, epoch);
+    k_general_commit<uint32_t><<<nwg, kBlock, 0, st>>>(ga, d, owner, cond, epoch);
   else
-    k_general_commit<unsigned long long><<<nwg, kBlock, 0, st>>>(ga, d, o, owner, cond, epoch);
+    k_general_commit<unsigned long long><<<nwg, kBlock, 0, st>>>(ga, d, owner, cond, epoch);
   return hipGetLastError();
 }
 
-hipError_t launch_replay(int dtype, int mode, const GroupArgs& ga, const DenseView& d, const Ovf& o,
-                         const uint32_t* cond, uint32_t epoch, hipStream_t st) {
-  if (ga.nb == 0) return hipSuccess;
+template <bool OOR_ONLY>
+static void replay_dispatch(int dtype, int mode, const GroupArgs& ga, const DenseView& d, const Ovf& o,
+                            const uint32_t* cond, uint32_t epoch, hipStream_t st) {
   if (mode == 0) {
     // assign moves value bits only: int32 and float share the 4-byte form
     if (dtype == 2)
-      k_replay<unsigned long long, 0><<<1, kReplayBlock, 0, st>>>(ga, d, o, cond, epoch);
+      k_replay<unsigned long long, 0, OOR_ONLY><<<1, kReplayBlock, 0, st>>>(ga, d, o, cond, epoch);
     else
-      k_replay<uint32_t, 0><<<1, kReplayBlock, 0, st>>>(ga, d, o, cond, epoch);
+      k_replay<uint32_t, 0, OOR_ONLY><<<1, kReplayBlock, 0, st>>>(ga, d, o, cond, epoch);
   } else if (dtype == 0) {
-    k_replay<int, 1><<<1, kReplayBlock, 0, st>>>(ga, d, o, cond, epoch);
+    k_replay<int, 1, OOR_ONLY><<<1, kReplayBlock, 0, st>>>(ga, d, o, cond, epoch);
   } else if (dtype == 1) {
-    k_replay<float, 1><<<1, kReplayBlock, 0, st>>>(ga, d, o, cond, epoch);
+    k_replay<float, 1, OOR_ONLY><<<1, kReplayBlock, 0, st>>>(ga, d, o, cond, epoch);
   } else {
-    k_replay<double, 1><<<1, kReplayBlock, 0, st>>>(ga, d, o, cond, epoch);
+    k_replay<double, 1, OOR_ONLY><<<1, kReplayBlock, 0, st>>>(ga, d, o, cond, epoch);
   }
+}
+
+hipError_t launch_replay(int dtype, int mode, const GroupArgs& ga, const DenseView& d, const Ovf& o,
+                         const uint32_t* cond, uint32_t epoch, hipStream_t st, bool oor_only) {
+  if (ga.nb == 0) return hipSuccess;
+  if (oor_only)
+    replay_dispatch<true>(dtype, mode, ga, d, o, cond, epoch, st);
+  else
+    replay_dispatch<false>(dtype, mode, ga, d, o, cond, epoch, st);
   return hipGetLastError();
 }
 
-hipError_t launch_ovf_rehash(int vb, const Ovf& from, uint64_t from_cap, const Ovf& to,
-                             hipStream_t st) {
+hipError_t launch_ovf_rehash(int vb, const Ovf& o, uint64_t from_cap, const OvfTab& to, hipStream_t st) {
   uint64_t g = (from_cap + kBlock - 1) / kBlock;
   if (g > 4096) g = 4096;
-  if (g == 0) return hipSuccess;
-  if (vb == 4)
-    k_ovf_rehash<uint32_t><<<(uint32_t)g, kBlock, 0, st>>>(from, from_cap, to);
-  else
-    k_ovf_rehash<unsigned long long><<<(uint32_t)g, kBlock, 0, st>>>(from, from_cap, to);
+  if (g != 0) {
+    if (vb == 4)
+      k_ovf_rehash<uint32_t><<<(uint32_t)g, kBlock, 0, st>>>(o, from_cap, to);
+    else
+      k_ovf_rehash<unsigned long long><<<(uint32_t)g, kBlock, 0, st>>>(o, from_cap, to);
+  }
+  k_ovf_set<<<1, 64, 0, st>>>(o, to);
   return hipGetLastError();
 }
 

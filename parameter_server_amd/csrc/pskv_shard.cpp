@@ -217,8 +217,17 @@ struct pskv_shard {
   uint64_t range = 0;
   void* dense = nullptr;
   unsigned long long* owner = nullptr;  // u64 stamps, allocated on first general-path use
-  // overflow table
+  // overflow table: the control block (device memory; the kernels' argument),
+  // its growth mailbox (coherent page-locked), the table as of the last
+  // adoption (read_overflow_stat) and every table array set allocated for this
+  // shard, by the host or by the grow service (freed once superseded and the
+  // stream is idle).  tab_m guards `tables` (the service appends to it).
   Ovf ovf{};
+  OvfMbox* mbox = nullptr;
+  OvfTab cur{};
+  std::mutex tab_m;
+  std::vector<OvfTab> tables;
+  uint32_t mbox_served = 0;  // grow service: number of the last request answered
   uint64_t ocap = 0;
   uint64_t ocount_known = 0;
   // device words: [0] verification tag
@@ -652,69 +661,186 @@ void srv_publish(pskv_shard* s) {
   __atomic_store_n(&s->srv->req_seq, q, __ATOMIC_RELEASE);
 }
 
-int alloc_overflow(Ovf* o, uint64_t cap, int vb, hipStream_t st) {
-  *o = Ovf{};
-  PSKV_HIP(hipMalloc(&o->keys, cap * sizeof(unsigned long long)));
-  PSKV_HIP(hipMalloc(&o->vals, cap * (size_t)vb));
-  PSKV_HIP(hipMalloc(&o->owner, cap * sizeof(unsigned long long)));
-  PSKV_HIP(hipMalloc(&o->stat, 2 * sizeof(uint32_t)));
-  PSKV_HIP(hipMemsetAsync(o->keys, 0xFF, cap * sizeof(unsigned long long), st));
-  PSKV_HIP(hipMemsetAsync(o->vals, 0, cap * (size_t)vb, st));
-  PSKV_HIP(hipMemsetAsync(o->owner, 0, cap * sizeof(unsigned long long), st));
-  PSKV_HIP(hipMemsetAsync(o->stat, 0, 2 * sizeof(uint32_t), st));
-  o->mask = cap - 1;
+// ------------------------------------------------------- overflow table
+// One array set of the table: keys EMPTY, values 0 (stream-ordered), tracked
+// in s->tables.
+int alloc_tab(pskv_shard* s, uint64_t cap, OvfTab* out) {
+  OvfTab t{};
+  if (hipMalloc(&t.keys, cap * sizeof(unsigned long long)) != hipSuccess ||
+      hipMalloc(&t.vals, cap * (size_t)s->vb) != hipSuccess) {
+    if (t.keys) (void)hipFree(t.keys);
+    return fail(PSKV_ENOMEM, "overflow table allocation failed");
+  }
+  t.mask = cap - 1;
+  {
+    std::lock_guard<std::mutex> g(s->tab_m);
+    s->tables.push_back(t);
+  }
+  PSKV_HIP(hipMemsetAsync(t.keys, 0xFF, cap * sizeof(unsigned long long), s->stream));
+  PSKV_HIP(hipMemsetAsync(t.vals, 0, cap * (size_t)s->vb, s->stream));
+  *out = t;
   return PSKV_OK;
 }
 
-void free_overflow(Ovf* o) {
-  if (o->keys) (void)hipFree(o->keys);
-  if (o->vals) (void)hipFree(o->vals);
-  if (o->owner) (void)hipFree(o->owner);
-  if (o->stat) (void)hipFree(o->stat);
-  *o = Ovf{};
+// Free every array set but the current one.  Only with the shard's stream
+// idle (no kernel can still hold a superseded table).
+void free_stale_tables(pskv_shard* s) {
+  std::lock_guard<std::mutex> g(s->tab_m);
+  std::vector<OvfTab> keep;
+  for (const auto& t : s->tables) {
+    if (t.keys == s->cur.keys) {
+      keep.push_back(t);
+      continue;
+    }
+    (void)hipFree(t.keys);
+    (void)hipFree(t.vals);
+  }
+  s->tables.swap(keep);
 }
 
-// Grow the overflow table to at least `need` occupied slots at load <= 1/2.
-int grow_overflow(pskv_shard* s, uint64_t need) {
-  if (int rc = srv_stop(s)) return rc;  // it holds the table by value
-  uint64_t cap = s->ocap;
-  while (cap < 2 * need) cap <<= 1;
-  if (cap == s->ocap) return PSKV_OK;
-  Ovf n{};
-  int rc = alloc_overflow(&n, cap, s->vb, s->stream);
-  if (rc) return rc;
-  PSKV_HIP(launch_ovf_rehash(s->vb, s->ovf, s->ocap, n, s->stream));
-  // carry the sticky error bits
-  PSKV_HIP(hipMemcpyAsync(n.stat + 1, s->ovf.stat + 1, sizeof(uint32_t), hipMemcpyDeviceToDevice,
-                          s->stream));
-  if (int rc = wait_stream(s, s->stream, "shard stream (overflow table growth)")) return rc;
-  free_overflow(&s->ovf);
-  s->ovf = n;
-  s->ocap = cap;
-  return PSKV_OK;
-}
-
-// Read {count, err} of the overflow table (synchronises the stream).
+// Read the control block back (synchronises the stream): {count, err}, and
+// adopt the table it names -- a device-side inserter may have grown it
+// (ovf_reserve) -- freeing the superseded arrays.
 int read_overflow_stat(pskv_shard* s, uint32_t* count, uint32_t* err) {
   if (int rc = srv_stop(s)) return rc;
   // into page-locked memory the shard owns: the copy is truly asynchronous (a
   // pageable destination would block inside the runtime, unbounded), and a
   // wait that times out leaves it writing into live memory, not a dead frame
+  static_assert(sizeof(OvfCtl) <= 64, "the control block fits the read-back buffer");
   if (!s->stat_host) {
     void* p = nullptr;
     if (hipHostMalloc(&p, 64, hipHostMallocDefault) != hipSuccess)
       return fail(PSKV_ENOMEM, "overflow-stat read-back buffer allocation failed");
     s->stat_host = static_cast<uint32_t*>(p);
   }
-  uint32_t* st = s->stat_host;
-  st[0] = st[1] = 0;
-  PSKV_HIP(hipMemcpyAsync(st, s->ovf.stat, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
+  OvfCtl* st = reinterpret_cast<OvfCtl*>(s->stat_host);
+  std::memset(st, 0, sizeof(OvfCtl));
+  PSKV_HIP(hipMemcpyAsync(st, s->ovf.c, sizeof(OvfCtl), hipMemcpyDeviceToHost, s->stream));
   if (int rc = wait_stream(s, s->stream, "shard stream (overflow count read-back)")) return rc;
-  *count = st[0];
-  *err = st[1];
-  s->ocount_known = st[0];
+  *count = st->stat[0];
+  *err = st->stat[1];
+  s->ocount_known = st->stat[0];
+  if (st->t.keys && st->t.keys != s->cur.keys) {
+    s->cur = st->t;
+    s->ocap = st->t.mask + 1;
+  }
+  free_stale_tables(s);
   return PSKV_OK;
 }
+
+// Grow the overflow table to at least `need` occupied slots at load <= 1/2
+// (after read_overflow_stat: the stream is idle and s->cur current).
+int grow_overflow(pskv_shard* s, uint64_t need) {
+  if (int rc = srv_stop(s)) return rc;
+  uint64_t cap = s->ocap;
+  while (cap < 2 * need) cap <<= 1;
+  if (cap == s->ocap) return PSKV_OK;
+  OvfTab n{};
+  if (int rc = alloc_tab(s, cap, &n)) return rc;
+  // rehash, then the control block names the new arrays (its counts and
+  // sticky bits stay where they are)
+  PSKV_HIP(launch_ovf_rehash(s->vb, s->ovf, s->ocap, n, s->stream));
+  if (int rc = wait_stream(s, s->stream, "shard stream (overflow table growth)")) return rc;
+  s->cur = n;
+  s->ocap = cap;
+  free_stale_tables(s);
+  return PSKV_OK;
+}
+
+// Device wait bound of a growth request (SYNC_TIMEOUT_MS in device wall-clock
+// ticks; 0 = unbounded host waits still bounds the device at 10 minutes, so a
+// grow service that is gone cannot hold a workgroup forever).
+void refresh_grow_wait(pskv_shard* s) {
+  if (!s->mbox) return;
+  const uint64_t ms = s->tune_sync_timeout_ms ? s->tune_sync_timeout_ms : 600000u;
+  const uint64_t ticks = ms * (uint64_t)std::max(s->wall_khz, 1);
+  __atomic_store_n(&s->mbox->wait_ticks, ticks, __ATOMIC_RELEASE);
+}
+
+// The grow service: ONE host thread per process that answers the growth
+// requests device-side inserters post to their shard's mailbox (ovf_reserve in
+// pskv_kernels.hip).  It polls every registered mailbox (100 us apart while
+// requests come, backing off to 1 ms after a quiet second), allocates arrays of
+// the asked capacity on the shard's device -- only allocation: the requesting
+// workgroup fills them and rehashes the table itself, so nothing here waits for
+// a queue the requester may be blocking -- records them in the shard's table
+// list, and answers.  A shard unregisters (under the service's lock) before its
+// mailbox goes.
+class GrowService {
+ public:
+  static GrowService& get() {
+    static GrowService g;
+    return g;
+  }
+  void add(pskv_shard* s) {
+    std::lock_guard<std::mutex> g(m_);
+    shards_.push_back(s);
+    if (!th_.joinable()) th_ = std::thread([this] { loop(); });
+    cv_.notify_all();
+  }
+  void remove(pskv_shard* s) {
+    std::lock_guard<std::mutex> g(m_);
+    shards_.erase(std::remove(shards_.begin(), shards_.end(), s), shards_.end());
+  }
+  ~GrowService() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    if (th_.joinable()) th_.join();
+  }
+
+ private:
+  GrowService() = default;
+  void serve(pskv_shard* s) {
+    OvfMbox* m = s->mbox;
+    const uint32_t seq = __atomic_load_n(&m->req_seq, __ATOMIC_ACQUIRE);
+    if (seq == s->mbox_served) return;
+    const uint64_t cap = __atomic_load_n(&m->req_cap, __ATOMIC_RELAXED);
+    OvfTab t{};
+    uint32_t ok = 0;
+    if (cap >= 2 && (cap & (cap - 1)) == 0 && hipSetDevice(s->device) == hipSuccess &&
+        hipMalloc(&t.keys, cap * sizeof(unsigned long long)) == hipSuccess) {
+      if (hipMalloc(&t.vals, cap * (size_t)s->vb) == hipSuccess) {
+        t.mask = cap - 1;
+        ok = 1;
+        std::lock_guard<std::mutex> g(s->tab_m);
+        s->tables.push_back(t);
+      } else {
+        (void)hipFree(t.keys);
+        t = OvfTab{};
+      }
+    }
+    (void)hipGetLastError();
+    m->resp_tab = t;
+    m->resp_ok = ok;
+    __atomic_store_n(&m->resp_seq, seq, __ATOMIC_RELEASE);
+    s->mbox_served = seq;
+    ++served_;
+  }
+  void loop() {
+    auto quiet_since = std::chrono::steady_clock::now();
+    std::unique_lock<std::mutex> lk(m_);
+    for (;;) {
+      cv_.wait(lk, [&] { return stop_ || !shards_.empty(); });
+      if (stop_) return;
+      const uint64_t before = served_;
+      for (pskv_shard* s : shards_) serve(s);
+      const auto now = std::chrono::steady_clock::now();
+      if (served_ != before) quiet_since = now;
+      const bool busy = now - quiet_since < std::chrono::seconds(1);
+      cv_.wait_for(lk, std::chrono::microseconds(busy ? 100 : 1000), [&] { return stop_; });
+      if (stop_) return;
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::vector<pskv_shard*> shards_;
+  std::thread th_;
+  bool stop_ = false;
+  uint64_t served_ = 0;
+};
 
 // A call that gives up on a wait (PSKV_ESTATE) or fails after queueing work
 // that still reads or writes the pinned staging buffer (H2D from it, D2H or K1
@@ -783,8 +909,7 @@ uint32_t next_epoch(pskv_shard* s) {
   // that every old stamp still loses to the new epoch 1.
   if (s->epoch == 0xFFFFFFFFu) {
     if (s->owner) (void)hipMemsetAsync(s->owner, 0, s->range * sizeof(unsigned long long), s->stream);
-    (void)hipMemsetAsync(s->ovf.owner, 0, s->ocap * sizeof(unsigned long long), s->stream);
-    (void)hipMemsetAsync(s->flag, 0, sizeof(uint32_t), s->stream);
+    (void)hipMemsetAsync(s->flag, 0, 2 * sizeof(uint32_t), s->stream);  // both tags
     s->epoch = 0;
   }
   return ++s->epoch;
@@ -950,15 +1075,23 @@ int general_add(pskv_shard* s, const std::vector<pskv_batch>& v, size_t b, size_
   for (size_t i = b; i < e; ++i) elems += v[i].n;
   {
     LaunchTimer t(s, PSKV_K_GENERAL_MARK, elems);
-    PSKV_HIP(launch_general_mark(s->dtype, s->mode, ga, nwg, s->dview(), s->ovf, s->owner, cond,
+    PSKV_HIP(launch_general_mark(s->dtype, s->mode, ga, nwg, s->dview(), s->flag + 1, s->owner, cond,
                                  epoch, s->stream));
     t.done();
   }
   s->n_general++;
   if (s->mode == PSKV_ASSIGN) {
     LaunchTimer t(s, PSKV_K_GENERAL_COMMIT, elems);
-    PSKV_HIP(launch_general_commit(s->vb, ga, nwg, s->dview(), s->ovf, s->owner, cond, epoch,
-                                   s->stream));
+    PSKV_HIP(launch_general_commit(s->vb, ga, nwg, s->dview(), s->owner, cond, epoch, s->stream));
+    t.done();
+    s->n_general++;
+  }
+  // the group's out-of-range keys, which K4a only tagged (flag[1]): one
+  // workgroup applies them in call order, growing the table as it goes
+  {
+    LaunchTimer t(s, PSKV_K_REPLAY, elems);
+    PSKV_HIP(launch_replay(s->dtype, s->mode, ga, s->dview(), s->ovf, s->flag + 1, epoch, s->stream,
+                           /*oor_only=*/true));
     t.done();
     s->n_general++;
   }
@@ -1403,19 +1536,8 @@ int note_frame_uses(pskv_shard* s, const std::vector<pskv_batch>& v) {
 // messages of kInlineMax keys; the caller's buffers are free once the launches
 // are enqueued (the runtime copies the arguments).
 int inline_add(pskv_shard* s, const std::vector<pskv_batch>& v) {
-  uint64_t outside = 0;
-  for (const auto& b : v)
-    for (uint64_t e = 0; e < b.n; ++e) outside += (uint64_t)(uint32_t)(b.keys[e] - s->key_begin) >= s->range;
-  if (outside) {
-    // exact bound on new overflow keys, as for staged host inputs
-    if (2 * (s->ocount_known + outside) > s->ocap) {
-      uint32_t cnt, err;
-      int rc = read_overflow_stat(s, &cnt, &err);
-      if (!rc) rc = grow_overflow(s, cnt + outside);
-      if (rc) return rc;
-    }
-    s->ocount_known += outside;
-  }
+  // (out-of-range keys need no host step: K8 / K9 reserve room in the
+  // overflow table on the device, ovf_reserve)
   const bool serve = serve_on(s);
   if (int rc = serve ? srv_ensure(s) : srv_stop(s)) return rc;
   InlineAdd a;
@@ -1591,17 +1713,9 @@ int add_impl(pskv_shard* s, const std::vector<pskv_batch>& in, int flags) {
         rc = stage_host_batches(s, v, &staged, &host_verified, &outside, &host_dense);
       }
       if (rc) return rc;
-      if (outside) {
-        // exact bound on new overflow keys: grow before the kernels can fill the table
-        if (2 * (s->ocount_known + outside) > s->ocap) {
-          uint32_t cnt, err;
-          rc = read_overflow_stat(s, &cnt, &err);
-          if (rc) return rc;
-          rc = grow_overflow(s, cnt + outside);
-          if (rc) return rc;
-        }
-        s->ocount_known += outside;
-      }
+      // (out-of-range keys need no host step: the single workgroup that
+      // inserts them reserves room on the device, ovf_reserve)
+      (void)outside;
       v.swap(staged);
     }
     bool vec = true;
@@ -2035,6 +2149,7 @@ int set_option(pskv_shard* s, const Option& o, int64_t v) {
   if (std::strcmp(o.name, "RB_BIN_BLOCK") == 0 && v != 512 && v != 1024)
     return fail(PSKV_EINVAL, "option RB_BIN_BLOCK: 512 or 1024");
   o.set(s, v);
+  if (std::strcmp(o.name, "SYNC_TIMEOUT_MS") == 0) refresh_grow_wait(s);
   if (std::strcmp(o.name, "INLINE_ADD_CHUNKS") == 0) s->add_chunks_set = true;
   // a ring slot costs the host ~0.2 us where a K8 launch costs 3-7: with the
   // server, Adds of up to 2 slots (512 keys) take it unless the chunk count
@@ -2168,11 +2283,30 @@ int pskv_shard_create_ex(int device, uint32_t key_begin, uint64_t key_end, int d
     return bail(fail(PSKV_ENOMEM, "flag allocation failed"));
   if (hipMemsetAsync(s->flag, 0, 16, s->stream) != hipSuccess)
     return bail(fail(PSKV_EHIP, "hipMemsetAsync failed"));
+  // the overflow table: control block, growth mailbox, first array set
   s->ocap = next_pow2(std::max<uint64_t>(overflow_slots ? overflow_slots : kDefaultOverflowSlots, 64));
-  rc = alloc_overflow(&s->ovf, s->ocap, vb, s->stream);
+  OvfCtl* ctl = nullptr;
+  if (hipMalloc(&ctl, sizeof(OvfCtl)) != hipSuccess) return bail(fail(PSKV_ENOMEM, "overflow control block allocation failed"));
+  s->ovf.c = ctl;
+  {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, sizeof(OvfMbox), hipHostMallocCoherent) != hipSuccess)
+      return bail(fail(PSKV_ENOMEM, "overflow growth mailbox allocation failed"));
+    std::memset(p, 0, sizeof(OvfMbox));
+    s->mbox = static_cast<OvfMbox*>(p);
+  }
+  if (hipDeviceGetAttribute(&s->wall_khz, hipDeviceAttributeWallClockRate, device) != hipSuccess) s->wall_khz = 100000;
+  refresh_grow_wait(s);
+  rc = alloc_tab(s, s->ocap, &s->cur);
   if (rc) return bail(rc);
+  OvfCtl init{};
+  init.t = s->cur;
+  init.mbox = s->mbox;
+  if (hipMemcpyAsync(ctl, &init, sizeof(init), hipMemcpyHostToDevice, s->stream) != hipSuccess)
+    return bail(fail(PSKV_EHIP, "hipMemcpyAsync failed"));
   if (int wrc = wait_stream(s, s->stream, "shard stream (creation)")) return bail(wrc);
   s->counted = g_queues.add_shard(device, 1);
+  GrowService::get().add(s);
   *out = s;
   return PSKV_OK;
 }
@@ -2185,9 +2319,11 @@ int pskv_shard_create(int device, uint32_t key_begin, uint64_t key_end, int dtyp
 int pskv_shard_destroy(pskv_shard* s) {
   if (!s) return PSKV_OK;
   (void)hipSetDevice(s->device);
+  // (the grow service keeps answering while the streams drain: a growing
+  // workgroup may be waiting for it)
   // every wait is bounded (PSKV_SYNC_TIMEOUT_MS): work that never completes
-  // keeps its device memory and streams (leaked, never freed under a running
-  // kernel), the host objects go, and the call reports what it waited for
+  // keeps its device memory, streams and shard object (leaked, never freed
+  // under a running kernel), and the call reports what it waited for
   std::string stuck;
   auto drain = [&](hipStream_t st, const char* what) {
     if (wait_stream(s, st, what) != PSKV_OK) stuck += (stuck.empty() ? "" : "; ") + g_last_error;
@@ -2205,11 +2341,13 @@ int pskv_shard_destroy(pskv_shard* s) {
   if (!stuck.empty()) {
     // the leaked streams keep their hardware queues: they stay counted in
     // g_queues (pskv_queues.h), so later shards on this device do not plan
-    // with queues that are still held
+    // with queues that are still held.  The shard object itself is leaked
+    // too: the grow service keeps answering its mailbox (stuck work may be a
+    // workgroup waiting for it) and the service holds the pointer.
     std::fprintf(stderr, "pskv: shard destroy: %s; its device memory and streams are not freed\n", stuck.c_str());
-    delete s;
     return fail(PSKV_ESTATE, "pskv_shard_destroy: " + stuck);
   }
+  GrowService::get().remove(s);
   if (s->counted) g_queues.add_shard(s->device, -1);
   if (s->out_stream) g_queues.add_stream(s->device, -1);
   if (s->srv) (void)hipHostFree(s->srv);
@@ -2226,7 +2364,12 @@ int pskv_shard_destroy(pskv_shard* s) {
   if (s->dense) (void)hipFree(s->dense);
   if (s->owner) (void)hipFree(s->owner);
   if (s->flag) (void)hipFree(s->flag);
-  free_overflow(&s->ovf);
+  for (const auto& t : s->tables) {  // (the service no longer touches the list)
+    (void)hipFree(t.keys);
+    (void)hipFree(t.vals);
+  }
+  if (s->ovf.c) (void)hipFree(s->ovf.c);
+  if (s->mbox) (void)hipHostFree(s->mbox);
   if (s->dstage) (void)hipFree(s->dstage);
   if (s->rb_loff) (void)hipFree(s->rb_loff);
   if (s->rb_ent) (void)hipFree(s->rb_ent);
@@ -2295,8 +2438,8 @@ int pskv_sync(pskv_shard* s) {
   if (rc) return rc;
   if (err & kErrOverflowFull)
     return fail(PSKV_ESTATE,
-                "overflow table exhausted: out-of-range keys were dropped; create the shard "
-                "with more overflow slots (pskv_shard_create_ex)");
+                "overflow table exhausted: out-of-range keys were dropped (the device-side growth "
+                "request was not answered within SYNC_TIMEOUT_MS, or its allocation failed)");
   if (2 * (uint64_t)cnt > s->ocap) return grow_overflow(s, cnt);
   return PSKV_OK;
 }
@@ -2305,12 +2448,13 @@ int pskv_clear(pskv_shard* s) {
   if (!s) return fail(PSKV_EINVAL, "pskv_clear: null shard");
   int rc = use_device(s);
   if (rc) return rc;
-  rc = srv_stop(s);
+  uint32_t cnt = 0, err = 0;
+  rc = read_overflow_stat(s, &cnt, &err);  // (adopts the current table; stops the server)
   if (rc) return rc;
   PSKV_HIP(hipMemsetAsync(s->dense, 0, s->range * (size_t)s->vb, s->stream));
-  PSKV_HIP(hipMemsetAsync(s->ovf.keys, 0xFF, s->ocap * sizeof(unsigned long long), s->stream));
-  PSKV_HIP(hipMemsetAsync(s->ovf.vals, 0, s->ocap * (size_t)s->vb, s->stream));
-  PSKV_HIP(hipMemsetAsync(s->ovf.stat, 0, 2 * sizeof(uint32_t), s->stream));
+  PSKV_HIP(hipMemsetAsync(s->cur.keys, 0xFF, s->ocap * sizeof(unsigned long long), s->stream));
+  PSKV_HIP(hipMemsetAsync(s->cur.vals, 0, s->ocap * (size_t)s->vb, s->stream));
+  PSKV_HIP(hipMemsetAsync(s->ovf.c->stat, 0, 2 * sizeof(uint32_t), s->stream));
   s->ocount_known = 0;
   if (int rc2 = wait_stream(s, s->stream, "shard stream (clear)")) return rc2;
   return PSKV_OK;

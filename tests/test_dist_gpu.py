@@ -131,7 +131,10 @@ def test_cfg4_rank_shares_bit_exact(cuda, oracle_mod, world):
     64-producer window sets, the straddling windows at all 7 boundaries, every
     pull and the whole final array bit-exact against the oracle
     (base/range_partition_manager.hpp:19-46, server/map_storage.hpp:17-27)."""
-    res = [_run_share(r, world, 1, cuda) for r in range(world)]
+    res = []
+    for r in range(world):
+        res.append(_run_share(r, world, 1, cuda))
+        print(f"cfg4 N={world} rank {r}: {res[-1][0]} slices, {res[-1][2]} keys, bit-exact", flush=True)
     # every set's windows arrived whole over the ranks (straddling ones in two)
     assert sum(r[2] for r in res) == (2 * 64 + len(straddle_bases(world))) * 1_000_000
     assert all(r[0] > 0 and r[3] > 0 for r in res)

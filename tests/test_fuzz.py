@@ -6,8 +6,10 @@ path) and a random sequence of calls — single, grouped (beyond the 64-batch
 launch group), host, device (unaligned pointers, right and WRONG sorted hints),
 inline-sized and large, uniform / Zipf / sorted / dense-window / out-of-range /
 sentinel keys, sorted look-alikes of windows (a repeated key hiding a missing
-one), empty batches, clears — and checks every Get against the reference state
-right away:
+one), bursts of thousands of NEW out-of-range keys into a 64-slot overflow
+table with no sync between calls (round 6: the table grows on the device),
+empty batches, clears — and checks every Get against the reference state
+right away (and at the end every out-of-range key any call pushed):
 
   assign      the oracle's MapStorage restatement (server/map_storage.hpp:17-45),
               bit-exact
@@ -96,6 +98,14 @@ def _keys(rng, kb, ke, n, kind):
             for i in rng.integers(0, n - 1, size=int(rng.integers(1, 4))).tolist():
                 k[i + 1] = k[i]
         return k
+    if kind == "burst" and size < U32:
+        # fresh out-of-range keys: uniform over [0, kb) and [ke, 2^32), half
+        # of the bursts sorted (the hinted device path then tags and replays)
+        x = rng.integers(0, U32 - size, size=n, dtype=np.int64)
+        k = np.where(x < kb, x, x + size)
+        if rng.random() < 0.5:
+            k = np.sort(k)
+        return k.astype(np.uint32)
     if kind == "zipf":
         hot = rng.integers(kb, ke, size=min(size, 64), dtype=np.int64)
         k = hot[(rng.zipf(1.3, size=n) - 1) % hot.size]
@@ -174,7 +184,8 @@ def _run(cuda, oracle_mod, seed, rng, dt, mode, kb, ke, knobs):
 
     ref = oracle_mod.MapStorageRef(dt) if mode == "assign" else AccRef(dt)
     keep = []  # device buffers stay alive until the final sync (stream-ordered use)
-    kinds = ["uniform", "zipf", "sorted", "dense", "oor", "lookalike"]
+    kinds = ["uniform", "zipf", "sorted", "dense", "oor", "lookalike", "burst"]
+    pushed_out = []  # out-of-range keys of every push (checked at the end)
     where = f"seed {seed} ({np.dtype(dt).name} {mode} [{kb}, {ke}) {knobs})"
 
     def check(q, got, step):
@@ -184,7 +195,15 @@ def _run(cuda, oracle_mod, seed, rng, dt, mode, kb, ke, knobs):
         else:
             ref.check(q, got, what)
 
-    with ps.Shard(kb, ke, dt, mode=mode, overflow_slots=1 << 14, options=knobs) as sh:
+    slots = int(rng.choice([64, 64, 1 << 14]))  # mostly the smallest table: it must grow on the device
+    where = where[:-1] + f", {slots} overflow slots)"
+
+    def pushed(k):
+        out = k[(k < kb) | (k.astype(np.uint64) >= ke)]
+        if out.size:
+            pushed_out.append(out)
+
+    with ps.Shard(kb, ke, dt, mode=mode, overflow_slots=slots, options=knobs) as sh:
         for step in range(N_STEPS):
             op = rng.choice(["add", "add", "add_dev", "add_grouped", "add_grouped_dev", "add_get_dev",
                              "get", "get_dev", "get_grouped", "clear"],
@@ -192,6 +211,7 @@ def _run(cuda, oracle_mod, seed, rng, dt, mode, kb, ke, knobs):
             kind = str(rng.choice(kinds))
             if op == "clear":
                 sh.clear()
+                pushed_out.clear()
                 if mode == "assign":
                     ref.close()
                 ref = oracle_mod.MapStorageRef(dt) if mode == "assign" else AccRef(dt)
@@ -206,8 +226,10 @@ def _run(cuda, oracle_mod, seed, rng, dt, mode, kb, ke, knobs):
                     dk, dv = tdev(k, cuda, off), tdev(v, cuda, off)
                     keep += [dk, dv]
                     sh.add(dk, dv, sorted_hint=hint)
-                    sh.sync()  # grows the overflow table between device calls
+                    if rng.random() < 0.3:
+                        sh.sync()  # (not needed for room: the table grows on the device)
                 ref.add(k, v)
+                pushed(k)
             elif op in ("add_grouped", "add_grouped_dev"):
                 nb = int(rng.choice([1, 2, 7, 64, 65, 70]))
                 dense = kind in ("dense", "lookalike")
@@ -223,9 +245,11 @@ def _run(cuda, oracle_mod, seed, rng, dt, mode, kb, ke, knobs):
                     dev = [(tdev(k, cuda), tdev(v, cuda)) for k, v in batches]
                     keep += [t for kv in dev for t in kv]
                     sh.add_grouped(dev, sorted_hint=bool(rng.random() < 0.7))
-                    sh.sync()
+                    if rng.random() < 0.3:
+                        sh.sync()
                 for k, v in batches:
                     ref.add(k, v)
+                    pushed(k)
             elif op == "add_get_dev":
                 # pskv_add_get_grouped: the grouped Add then the grouped Get;
                 # the pulls see the pushes of the same call
@@ -253,9 +277,11 @@ def _run(cuda, oracle_mod, seed, rng, dt, mode, kb, ke, knobs):
                 sh.add_get_grouped(dev_a, list(zip(dev_q, outs)), sorted_hint=bool(rng.random() < 0.8))
                 for k, v in adds:
                     ref.add(k, v)
+                    pushed(k)
                 for q, o in zip(qs, outs):
                     check(q, o.cpu().numpy(), step)
-                sh.sync()
+                if rng.random() < 0.3:
+                    sh.sync()
             elif op == "get":
                 q = _keys(rng, kb, ke, int(rng.choice(SIZES)), kind)
                 check(q, sh.get(q), step)
@@ -275,6 +301,9 @@ def _run(cuda, oracle_mod, seed, rng, dt, mode, kb, ke, knobs):
         # plus every out-of-range key any call used
         q = np.arange(kb, ke, dtype=np.uint64).astype(np.uint32) if ke - kb <= 65_536 else \
             _keys(rng, kb, ke, 100_000, "uniform")
+        if pushed_out:
+            o = np.unique(np.concatenate(pushed_out))
+            q = np.concatenate([q, o if o.size <= 200_000 else rng.choice(o, 200_000, replace=False)])
         check(q, sh.get(q), "final")
         sh.sync()
         torch.cuda.synchronize()

@@ -580,27 +580,123 @@ def test_overflow_table_growth_and_edges(cuda, oracle_mod):
     assert_bits_equal(got, ref.get(q), "overflow")
 
 
-@pytest.mark.parametrize("path", ["sorted_hint", "unsorted"])
-def test_device_overflow_burst_fails_loudly(cuda, path):
-    """PSKV_DEVICE inputs are not counted on the host: a burst of new
-    out-of-range keys larger than the overflow table is reported by the next
-    sync (PSKV_ESTATE), never silently; a burst that fits, followed by a sync,
-    grows the table for the next one."""
+class _AccRef:
+    """Accumulate-mode model for int32 (wrap-around sums are exact in any
+    order): key -> value, missing keys 0."""
+
+    def __init__(self):
+        self.m = {}
+
+    def add(self, k, v):
+        for kk, vv in zip(k.tolist(), v.astype(np.int64).tolist()):
+            self.m[kk] = (self.m.get(kk, 0) + vv) & 0xFFFFFFFF
+
+    def get(self, k):
+        return np.array([self.m.get(kk, 0) for kk in k.tolist()], dtype=np.uint32).view(np.int32)
+
+
+def _burst(rng, i, kb, ke, n_new, sort):
+    """One push: n_new NEW out-of-range keys (below the range and above it;
+    fresh every burst), every one repeated 1-3 times, plus in-range keys."""
+    below = np.arange(kb - 1 - i * n_new // 2, kb - 1 - (i + 1) * n_new // 2, -1, dtype=np.int64)
+    above = ke + 10 + np.arange(i * (n_new - below.size), (i + 1) * (n_new - below.size), dtype=np.int64) * 3
+    k = np.concatenate([below, above, rng.integers(kb, ke, size=n_new // 4)])
+    k = np.repeat(k, rng.integers(1, 4, size=k.size)).astype(np.uint32)
+    if sort:
+        k.sort(kind="stable")
+    else:
+        rng.shuffle(k)
+    return k
+
+
+# one push / device path of the overflow inserters (each a single workgroup that
+# reserves room, growing the table on the device): K2g + replay (K4r), the
+# replay folded into the Get (K1r), K5's out-of-range bucket, K4 + its
+# oor-only replay, the host K5 path and K8 messages
+BURST_PATHS = ["sorted_hint", "add_get", "unsorted", "stamps", "host", "inline"]
+
+
+@pytest.mark.parametrize("mode", ["assign", "accumulate"])
+@pytest.mark.parametrize("path", BURST_PATHS)
+def test_overflow_burst_parity(cuda, oracle_mod, path, mode):
+    """The reference's last range server stores every key the slicer cannot
+    place, however many (range_partition_manager.hpp:26-27,
+    map_storage.hpp:22-23): bursts of 5,000 NEW out-of-range keys into a
+    64-slot table, with no sync between them, through every inserter, match
+    the reference bit for bit -- assign against MapStorageRef (last occurrence
+    wins), accumulate (int32, exact) against the sequential sum -- read back
+    both by device Gets between the bursts and by a host Get at the end; the
+    table grew on the device."""
+    import torch
+
+    import parameter_server_amd as ps
+
+    rng = np.random.default_rng(100 + 2 * BURST_PATHS.index(path) + (mode == "accumulate"))
+    dt = np.float32 if mode == "assign" else np.int32
+    ref = oracle_mod.MapStorageRef(dt) if mode == "assign" else _AccRef()
+    kb, ke = 1_000_000, 1_010_000
+    opts = {"GENERAL": "stamps"} if path == "stamps" else {}
+    seen = []
+    with ps.Shard(kb, ke, dt, mode=mode, overflow_slots=64, options=opts) as sh:
+        for i in range(3):
+            k = _burst(rng, i, kb, ke, 5000, sort=path in ("sorted_hint", "add_get"))
+            v = (rng.integers(-1000, 1000, size=k.size)).astype(dt)
+            if mode == "assign":
+                v = (rng.standard_normal(k.size) * 100).astype(dt)
+            ref.add(k, v)
+            seen.append(k)
+            q = np.unique(np.concatenate(seen))
+            if path == "inline":  # K8: messages of <= 256 keys
+                for j in range(0, k.size, 200):
+                    sh.add(k[j:j + 200], v[j:j + 200])
+                got = sh.get(q)
+            elif path == "host":
+                sh.add(k, v)
+                got = sh.get(q)
+            elif path == "add_get":
+                out = torch.empty(q.size, dtype=torch.float32 if dt == np.float32 else torch.int32, device=cuda)
+                sh.add_get_grouped([(tdev(k, cuda), tdev(v, cuda))], [(tdev(q, cuda), out)], sorted_hint=True)
+                got = out.cpu().numpy()
+            else:
+                sh.add(tdev(k, cuda), tdev(v, cuda), sorted_hint=path == "sorted_hint")
+                got = sh.get(tdev(q, cuda)).cpu().numpy()
+            assert_bits_equal(got, ref.get(q), f"{path}/{mode} burst {i}")
+        sh.sync()
+        info = sh.info()
+        n_out = int(np.count_nonzero((q < kb) | (q >= ke)))
+        assert info["overflow_count"] == n_out, (info, n_out)
+        assert info["overflow_capacity"] >= 2 * n_out > 64
+        assert_bits_equal(sh.get(q), ref.get(q), f"{path}/{mode} after sync")
+
+
+def test_overflow_growth_timeout_fails_loudly(cuda):
+    """SYNC_TIMEOUT_MS = 1 bounds a growth request's wait on the device at
+    ~1 ms, about the grow service's polling period: a burst far past the table
+    either grows in time or drops keys, and then the next sync says so
+    (PSKV_ESTATE, "dropped") -- never a silent loss: a sync that succeeds
+    means every key is there."""
+    import torch
+
     import parameter_server_amd as ps
     from parameter_server_amd import PskvError, _lib
 
-    hint = path == "sorted_hint"
-    small = np.arange(10_000, 10_020, dtype=np.uint32)          # 20 new keys: fits 64 slots
-    with ps.Shard(0, 1000, np.float32, overflow_slots=64) as sh:
-        sh.add(tdev(small, cuda), tdev(np.ones(small.size, np.float32), cuda), sorted_hint=hint)
-        sh.sync()
-        assert sh.info()["overflow_capacity"] >= 2 * sh.info()["overflow_count"]
-        assert np.all(sh.get(small) == 1.0)
-        burst = np.arange(20_000, 25_000, dtype=np.uint32)      # 5000 new keys: cannot fit
-        sh.add(tdev(burst, cuda), tdev(np.full(burst.size, 2.0, np.float32), cuda), sorted_hint=hint)
-        with pytest.raises(PskvError) as ei:
+    rng = np.random.default_rng(5)
+    with ps.Shard(0, 1000, np.float32, overflow_slots=64, options={"SYNC_TIMEOUT_MS": 1}) as sh:
+        k = np.arange(10_000, 60_000, dtype=np.uint32)
+        rng.shuffle(k)
+        v = np.ones(k.size, np.float32)
+        dk, dv = tdev(k, cuda), tdev(v, cuda)
+        sh.add(dk, dv)
+        torch.cuda.synchronize()  # the Add ran under the 1 ms device bound
+        sh.set_option("SYNC_TIMEOUT_MS", 0)  # (the host waits below are not under test)
+        try:
             sh.sync()
-        assert ei.value.code == _lib.PSKV_ESTATE
+            ok = True
+        except PskvError as e:
+            assert e.code == _lib.PSKV_ESTATE and "dropped" in str(e), str(e)
+            ok = False
+        if ok:
+            assert np.all(sh.get(k) == 1.0)
 
 
 def test_bounded_waits_report_pending_work(cuda):

@@ -92,6 +92,11 @@ for step in "$@"; do
         > "$OUT/tests_addget.log" 2>&1 ;;
     tests_all) timeout -k 10 900 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread "$R/tests" -m gpu \
         > "$OUT/tests_all.log" 2>&1 ;;
+    tests_r6) timeout -k 10 600 python3 -u -m pytest -x -v -s --timeout 300 --timeout-method thread \
+        "$R/tests/test_dist_gpu.py" "$R/tests/test_serve.py" "$R/tests/test_bench_multirank_gpu.py" \
+        -k "rank_shares or holds_staging or bench_ranks_one_gpu" > "$OUT/tests_r6.log" 2>&1 ;;
+    tests_k) timeout -k 10 600 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread "$R/tests" -m gpu \
+        -k "$TESTS_K" > "$OUT/tests_k.log" 2>&1 ;;
     align) timeout -k 10 200 python3 "$R/tools/align_probe.py" 0,1,2,3 20 > "$OUT/align.log" 2>&1 ;;
     foldcold) mkdir -p "$OUT/foldcold" && for i in 1 2 3; do for f in 1 0; do
           PSKV_FOLD_REPLAY=$f timeout -k 10 200 python3 "$R/bench.py" --steps 50 --cold-only \
