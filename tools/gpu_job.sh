@@ -140,8 +140,8 @@ for step in "$@"; do
           cp "$R/ab/libpskv_$v.so" "$L" &&
           timeout -k 10 300 "$R/tools/micro/small_latency" > "$OUT/small_latency_${v}_$rep.log" 2>&1 || { cp "$OUT/.keep.so" "$L"; exit 1; }
         done; done; cp "$OUT/.keep.so" "$L"; rm -f "$OUT/.keep.so" ;;
-    ztrace) for v in 1024 512; do
-          PSKV_RB_BIN_BLOCK=$v PROBE_ROUNDS=5 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/ztrace_$v" \
+    ztrace) for v in ${ZTRACE_BLOCKS:-1024 512}; do
+          PSKV_RB_BIN_BLOCK=$v PROBE_ROUNDS=5 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/ztrace_$v" \
             -o run -- python3 "$R/tools/zipf_probe.py" > "$OUT/ztrace_$v.log" 2>&1 || exit 1
         done ;;
     zpmc) timeout -k 10 600 bash "$R/tools/zipf_pmc.sh" "$(basename "$OUT")/zpmc" > "$OUT/zpmc.log" 2>&1 ;;

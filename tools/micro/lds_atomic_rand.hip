@@ -18,7 +18,9 @@ __device__ __forceinline__ uint32_t mix(uint32_t x) {
   return x;
 }
 
-// hot: of every 64 lanes, this many go to one of 4 hot slots
+// hot: of every 64 lanes, this many go to one of 4 hot slots; hot = -1: random
+// rows but lane l of each 32-lane group on bank l (conflict-free: the bank a
+// random table slot would need to land on to cost one LDS cycle per group)
 template <int OP>
 __global__ __launch_bounds__(1024) void k(uint32_t* out, int passes, int hot) {
   __shared__ uint32_t t[16384];
@@ -30,7 +32,8 @@ __global__ __launch_bounds__(1024) void k(uint32_t* out, int passes, int hot) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const uint32_t h = mix((blockIdx.x * 131u + p) * 8192u + q * 1024u + threadIdx.x);
-      slot[q] = ((threadIdx.x & 63) < (uint32_t)hot) ? (h & 3u) : (h & 16383u);
+      slot[q] = hot < 0 ? (((h & 16383u) & ~31u) | (threadIdx.x & 31u))
+                        : ((threadIdx.x & 63) < (uint32_t)hot) ? (h & 3u) : (h & 16383u);
     }
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -52,7 +55,7 @@ int main() {
   hipEventCreate(&e1);
   const int passes = 200, grid = 256;
   const char* names[] = {"ds_cmpst_rtn_b32", "ds_max_u32", "ds_add_rtn_u32", "ds_read_b32"};
-  for (int hot : {0, 4, 16}) {
+  for (int hot : {0, -1, 4, 16}) {
     for (int op = 0; op < 4; ++op) {
       float best = 1e30f;
       for (int rep = 0; rep < 3; ++rep) {
