@@ -20,7 +20,12 @@
 //
 // usage: ssp_replay [--model ssp|bsp|asp] [--workers W] [--shards S] [--iters I]
 //                   [--batch B] [--staleness T] [--skew K] [--cpu-only] [--known-answers]
-//                   [--partition range|hash]
+//                   [--partition range|hash] [--trace FILE]
+// --trace FILE (not with --threads) writes the second run's model traffic: every
+// message handed to a server's model, the replies that handling pushed, and
+// every shard's final contents, so oracle/consistency_ref.py -- a restatement of
+// the reference models independent of include/ps/consistency.hpp -- can replay
+// the same arrivals and check each reply (tests/test_replay.py).
 // --partition hash slices with the reference Engine's DEFAULT partitioner, the
 // jump consistent hash (base/consistent_hashing_partition_manager.hpp; the LR
 // app's own configuration, driver/engine.hpp:143-150): every shard then owns
@@ -120,6 +125,47 @@ struct Config {
   bool threads = false;  // one ServerThread per shard (concurrent HipStorage use)
   bool frames = false;   // payloads delivered in page-locked frames (HipStorage runs only)
   std::string partition = "range";  // range | hash
+  std::string trace;                // model traffic of the second run (--trace)
+};
+
+// Trace records (little-endian): 'I' (a message handed to server s's model) and
+// 'O' (a message that handling pushed to the reply queue) carry
+//   u8 kind, i32 server, i8 flag, i32 sender, i32 recver, i32 model_id,
+//   u32 ndata, ndata x (u64 bytes, bytes);
+// 'F' (server s's final contents, every key of its range in order) carries
+//   u8 kind, i32 server, u64 n, n x f64.
+class TraceWriter {
+ public:
+  explicit TraceWriter(const std::string& path) : f_(std::fopen(path.c_str(), "wb")) {
+    if (!f_) throw std::runtime_error("cannot open trace file " + path);
+  }
+  ~TraceWriter() { std::fclose(f_); }
+  void message(char kind, int server, const Message& m) {
+    put(kind);
+    put((int32_t)server);
+    put((int8_t)m.meta.flag);
+    put((int32_t)m.meta.sender);
+    put((int32_t)m.meta.recver);
+    put((int32_t)m.meta.model_id);
+    put((uint32_t)m.data.size());
+    for (const auto& d : m.data) {
+      put((uint64_t)d.size());
+      if (d.size()) std::fwrite(d.data(), 1, d.size(), f_);
+    }
+  }
+  void final_vals(int server, const std::vector<double>& v) {
+    put('F');
+    put((int32_t)server);
+    put((uint64_t)v.size());
+    if (!v.empty()) std::fwrite(v.data(), sizeof(double), v.size(), f_);
+  }
+
+ private:
+  template <typename T>
+  void put(T x) {
+    std::fwrite(&x, sizeof(T), 1, f_);
+  }
+  std::FILE* f_;
 };
 
 struct ReplyRecord {
@@ -137,7 +183,7 @@ struct Run {
 
 class Replay {
  public:
-  Replay(const Config& c, bool hip) : c_(c), hip_(hip) {
+  Replay(const Config& c, bool hip, TraceWriter* trace = nullptr) : c_(c), hip_(hip), trace_(trace) {
     const uint64_t step = c.n_features / c.shards;
     const bool hashed = c.partition == "hash";
     for (int s = 0; s < c.shards; ++s) {
@@ -257,6 +303,7 @@ class Replay {
       third_party::SArray<Key> keys(ks);
       auto v = third_party::SArray<double>(storages_[s]->SubGet(keys));
       out_.final_vals.emplace_back(v.begin(), v.end());
+      if (trace_) trace_->final_vals(s, out_.final_vals.back());
       storages_[s]->FinishIter();
     }
     out_.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -329,6 +376,7 @@ class Replay {
           server_q_[s].pop();
           any = true;
           AbstractModel* md = models_[s].get();
+          if (trace_) trace_->message('I', s, m);
           switch (m.meta.flag) {  // server/server_thread.cpp:29-46
             case Flag::kClock: md->Clock(m); break;
             case Flag::kAdd: md->Add(m); break;
@@ -336,16 +384,19 @@ class Replay {
             case Flag::kResetWorkerInModel: md->ResetWorker(m); break;
             default: break;
           }
-          route();
+          route(s);
         }
       }
       if (!any) break;
     }
   }
 
-  void route() {
+  void route(int server) {
     Message r;
-    while (replies_.Pop(&r)) route_one(r);
+    while (replies_.Pop(&r)) {
+      if (trace_) trace_->message('O', server, r);
+      route_one(r);
+    }
   }
 
   void route_one(const Message& r) {
@@ -473,6 +524,7 @@ class Replay {
 
   Config c_;
   bool hip_;
+  TraceWriter* trace_;
   std::vector<std::pair<uint64_t, uint64_t>> ranges_;
   std::vector<uint32_t> ids_;
   std::unique_ptr<AbstractPartitionManager> map_;
@@ -843,6 +895,7 @@ int main(int argc, char** argv) {
     else if (a == "--frames") c.frames = true;
     else if (a == "--known-answers") ka = true;
     else if (a == "--partition") c.partition = nxt();
+    else if (a == "--trace") c.trace = nxt();
   }
   int fails = 0;
   if (ka) {
@@ -851,8 +904,14 @@ int main(int argc, char** argv) {
       fails += known_answers(
           [] { return std::unique_ptr<AbstractStorage>(new HipStorage<int>(0, 0, 1024)); }, "hip");
   }
+  if (!c.trace.empty() && c.threads) {
+    std::fprintf(stderr, "--trace needs the single-threaded scheduler (no --threads)\n");
+    return 2;
+  }
   Run ref = Replay(c, false).run();
-  Run other = c.cpu_only ? Replay(c, false).run() : Replay(c, true).run();
+  std::unique_ptr<TraceWriter> tw(c.trace.empty() ? nullptr : new TraceWriter(c.trace));
+  Run other = Replay(c, !c.cpu_only, tw.get()).run();
+  tw.reset();
   std::string why;
   const bool ok = same(ref, other, &why);
   std::printf("replay model=%s partition=%s%s workers=%d shards=%d iters=%d batch=%d staleness=%d: msgs=%llu "
