@@ -4,7 +4,8 @@
 # is restored to the tree's own build on exit), 3
 # rounds each, under bench.py (default) or, with AB_PROG=zipf, under
 # tools/zipf_probe.py (the cfg-3 K5 / K1 kernel times), with AB_PROG=sizes under
-# tools/size_probe.py (K2g / K1 fixed cost per launch).
+# tools/size_probe.py (K2g / K1 fixed cost per launch), with AB_PROG=e2e under
+# tools/e2e_probe.py (host-buffer Add / Get).
 #   bash tools/ab_lib.sh OUTNAME ["bench.py args"]
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$PWD}
@@ -20,6 +21,8 @@ for i in 1 2 3; do
     cp "$R/ab/libpskv_$v.so" "$R/parameter_server_amd/libpskv.so" || exit 1
     if [ "${AB_PROG:-bench}" = sizes ]; then
       timeout -k 10 200 python3 "$R/tools/size_probe.py" > "$OUT/$v$i.log" 2>&1 || exit 2
+    elif [ "${AB_PROG:-bench}" = e2e ]; then
+      timeout -k 10 200 python3 "$R/tools/e2e_probe.py" > "$OUT/$v$i.log" 2>&1 || exit 2
     elif [ "${AB_PROG:-bench}" = zipf ]; then
       timeout -k 10 200 python3 "$R/tools/zipf_probe.py" > "$OUT/$v$i.log" 2>&1 || exit 2
     else

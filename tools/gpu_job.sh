@@ -161,6 +161,7 @@ for step in "$@"; do
     ldsrand) timeout -k 10 120 "$R/tools/micro/lds_atomic_rand" > "$OUT/lds_atomic_rand.log" 2>&1 ;;
     abz) AB_PROG=zipf timeout -k 10 900 bash "$R/tools/ab_lib.sh" "$(basename "$OUT")/abz" > "$OUT/abz.log" 2>&1 ;;
     sizes) timeout -k 10 300 python3 "$R/tools/size_probe.py" > "$OUT/size_probe.log" 2>&1 ;;
+    abh) AB_PROG=e2e timeout -k 10 900 bash "$R/tools/ab_lib.sh" "$(basename "$OUT")/abh" > "$OUT/abh.log" 2>&1 ;;
     abb) timeout -k 10 900 bash "$R/tools/ab_lib.sh" "$(basename "$OUT")/abb" > "$OUT/abb.log" 2>&1 ;;
     abe) PSKV_BENCH_EMULATE=0/8 timeout -k 10 900 bash "$R/tools/ab_lib.sh" "$(basename "$OUT")/abe" \
           "--no-extra --no-cpu-baseline --no-zipf --steps 50" > "$OUT/abe.log" 2>&1 ;;
