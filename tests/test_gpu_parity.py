@@ -669,6 +669,69 @@ def test_overflow_burst_parity(cuda, oracle_mod, path, mode):
         assert_bits_equal(sh.get(q), ref.get(q), f"{path}/{mode} after sync")
 
 
+def test_overflow_growth_concurrent_shards(cuda, oracle_mod):
+    """The reference runs one server thread per range (simple_id_mapper.cpp:28-31),
+    each with its own storage; here 8 shards on 8 threads push device bursts
+    of new out-of-range keys at once, so growth requests from several shards'
+    kernels (K5's out-of-range bucket, the replay after K2g) are outstanding
+    together and the ONE grow service answers them in turn.  Every shard,
+    read back on its own thread after each burst and again at the end, matches
+    its own MapStorageRef bit for bit."""
+    import threading
+
+    import parameter_server_amd as ps
+
+    n_sh, bursts = 8, 3
+    shards = [ps.Shard(1_000_000 + 20_000 * i, 1_010_000 + 20_000 * i, np.float32, overflow_slots=64)
+              for i in range(n_sh)]
+    pushes = [[] for _ in range(n_sh)]
+    reads = [[] for _ in range(n_sh)]
+    errors = []
+
+    def work(i):
+        try:
+            sh = shards[i]
+            kb, ke = 1_000_000 + 20_000 * i, 1_010_000 + 20_000 * i
+            rng = np.random.default_rng(700 + i)
+            seen = []
+            for b in range(bursts):
+                k = _burst(rng, b, kb, ke, 3000, sort=i % 2 == 1)
+                v = (rng.standard_normal(k.size) * 100).astype(np.float32)
+                pushes[i].append((k, v))
+                seen.append(k)
+                q = np.unique(np.concatenate(seen))
+                sh.add(tdev(k, cuda), tdev(v, cuda), sorted_hint=i % 2 == 1)
+                reads[i].append((q, sh.get(tdev(q, cuda)).cpu().numpy()))
+            sh.sync()
+            reads[i].append((q, sh.get(q)))
+        except Exception as e:  # re-raised on the main thread
+            errors.append((i, e))
+
+    try:
+        th = [threading.Thread(target=work, args=(i,)) for i in range(n_sh)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+        assert not any(t.is_alive() for t in th), "a shard thread did not finish"
+        assert not errors, errors
+        for i, sh in enumerate(shards):
+            ref = oracle_mod.MapStorageRef(np.float32)
+            for b, (k, v) in enumerate(pushes[i]):
+                ref.add(k, v)
+                q, got = reads[i][b]
+                assert_bits_equal(got, ref.get(q), f"shard {i} burst {b}")
+            q, got = reads[i][-1]
+            assert_bits_equal(got, ref.get(q), f"shard {i} after sync")
+            kb, ke = 1_000_000 + 20_000 * i, 1_010_000 + 20_000 * i
+            n_out = int(np.count_nonzero((q < kb) | (q >= ke)))
+            info = sh.info()
+            assert info["overflow_count"] == n_out and info["overflow_capacity"] >= 2 * n_out > 64, (i, info)
+    finally:
+        for sh in shards:
+            sh.close()
+
+
 def test_overflow_growth_timeout_fails_loudly(cuda):
     """SYNC_TIMEOUT_MS = 1 bounds a growth request's wait on the device at
     ~1 ms, about the grow service's polling period: a burst far past the table
