@@ -188,8 +188,9 @@ int pskv_get_grouped(pskv_shard* s, const pskv_batch* batches, uint64_t nb, int 
 int pskv_add_get_grouped(pskv_shard* s, const pskv_batch* adds, uint64_t na, const pskv_batch* gets,
                          uint64_t ng, int flags);
 
-/* Wait for the shard's stream, grow the overflow table if needed, report
- * sticky device errors.  Every host wait of the library (this one, a host
+/* Wait for the shard's stream, adopt the overflow table as the kernels left
+ * it (freeing arrays a device-side growth replaced; trimming its load to
+ * <= 1/2), report sticky device errors.  Every host wait of the library (this one, a host
  * Get's, the staging and scratch waits, destroy's) is bounded by the option
  * SYNC_TIMEOUT_MS (default 120000; 0 = unbounded): work that does not complete
  * in time fails the call with PSKV_ESTATE, and pskv_last_error() names the
