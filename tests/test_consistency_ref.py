@@ -11,12 +11,12 @@ include/ps/consistency.hpp).
    store's.
 """
 import os
+import struct
 import subprocess
+import sys
 
 import numpy as np
 import pytest
-
-import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -151,8 +151,6 @@ def test_trace_checker_catches_a_changed_reply(tmp_path):
     raw = bytearray(trace.read_bytes())
     # find a recorded Get reply with values and flip a byte of its first value
     p = 0
-    import struct
-
     while p < len(raw):
         kind = chr(raw[p])
         if kind == "F":
