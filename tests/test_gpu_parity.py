@@ -669,6 +669,34 @@ def test_overflow_burst_parity(cuda, oracle_mod, path, mode):
         assert_bits_equal(sh.get(q), ref.get(q), f"{path}/{mode} after sync")
 
 
+@pytest.mark.parametrize("path", ["unsorted", "sorted_hint"])
+def test_overflow_growth_many_doublings_in_one_launch(cuda, path):
+    """One device Add of 2 Mi NEW out-of-range keys into a 64-slot table: the
+    single inserting workgroup (K5's out-of-range bucket, or the replay behind
+    K2g) asks the grow service again and again inside ONE launch (64 -> 8 Mi
+    slots: 17 requests through the same mailbox) and every key lands; values
+    bit-exact (each key once, so last-write-wins is the value itself)."""
+    import torch
+
+    import parameter_server_amd as ps
+
+    n = 2 << 20
+    rng = np.random.default_rng(77)
+    k = (np.uint64(3_000_000) + np.arange(n, dtype=np.uint64) * np.uint64(7)).astype(np.uint32)  # all above the range
+    if path == "unsorted":
+        rng.shuffle(k)
+    v = rng.standard_normal(n).astype(np.float32)
+    with ps.Shard(0, 1_000_000, np.float32, overflow_slots=64) as sh:
+        sh.add(tdev(k, cuda), tdev(v, cuda), sorted_hint=path == "sorted_hint")
+        got = sh.get(tdev(k, cuda)).cpu().numpy()
+        torch.cuda.synchronize()
+        sh.sync()
+        info = sh.info()
+        assert info["overflow_count"] == n and info["overflow_capacity"] >= 2 * n, info
+        assert_bits_equal(got, v, f"{path}: 2 Mi new out-of-range keys")
+        assert_bits_equal(sh.get(k[::97]), v[::97], f"{path}: host Get after sync")
+
+
 def test_overflow_growth_concurrent_shards(cuda, oracle_mod):
     """The reference runs one server thread per range (simple_id_mapper.cpp:28-31),
     each with its own storage; here 8 shards on 8 threads push device bursts
