@@ -673,8 +673,9 @@ def test_overflow_burst_parity(cuda, oracle_mod, path, mode):
 def test_overflow_growth_many_doublings_in_one_launch(cuda, path):
     """One device Add of 2 Mi NEW out-of-range keys into a 64-slot table: the
     single inserting workgroup (K5's out-of-range bucket, or the replay behind
-    K2g) asks the grow service again and again inside ONE launch (64 -> 8 Mi
-    slots: 17 requests through the same mailbox) and every key lands; values
+    K2g) reserves room for everything it is about to insert, so the table goes
+    from 64 slots to >= 4 Mi inside ONE launch (a 65 536-fold growth, the
+    whole rehash and fill done by that workgroup) and every key lands; values
     bit-exact (each key once, so last-write-wins is the value itself)."""
     import torch
 
