@@ -110,8 +110,10 @@ def test_serve_idle_restart_and_ring_wrap(cuda, oracle_mod, serve):
 
 def test_serve_overflow_growth(cuda, oracle_mod, serve):
     """Small messages full of out-of-range keys grow the overflow table many
-    times (the server is stopped, the table rehashed, the server restarted
-    with the new table)."""
+    times: ~40 K new keys from 64 slots, 200 messages.  With the request
+    server (K9) one resident launch takes the messages and grows the table
+    itself, request after request through the same mailbox (round 6); with
+    K8 every launch reserves for its own message."""
     import parameter_server_amd as ps
 
     rng = np.random.default_rng(17)
