@@ -565,7 +565,7 @@ def test_overflow_table_growth_and_edges(cuda, oracle_mod):
             k[:10] = 0xFFFFFFFF                                         # the LDS sentinel key, in range
             k[10:20] = 2**32 - 1000
             v = rng.standard_normal(k.size).astype(np.float32)
-            sh.add(k, v)                     # host path sizes the table itself
+            sh.add(k, v)                     # host path: the inserting workgroup grows the table
             ref.add(k, v)
             sh.sync()
         info = sh.info()
