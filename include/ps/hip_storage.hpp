@@ -124,7 +124,8 @@ class HipStorage : public AbstractStorage {
   }
 
   // The reference's FinishIter is a no-op (map_storage.hpp:47); here it is the
-  // point where deferred device errors surface and the overflow table grows.
+  // point where deferred device errors surface and the overflow table, which
+  // grows on the device as keys arrive, is trimmed and its old arrays freed.
   void FinishIter() override { pskv_check(pskv_sync(shard_), "pskv_sync"); }
 
   pskv_shard* shard() const { return shard_; }
